@@ -1,0 +1,70 @@
+"""Build the HIP extension libarslam_lm.so in-tree (gfx950).
+
+The product is a plain C-ABI shared library (include/arslam_lm.h) compiled
+by hipcc; nothing is JIT-compiled at import time, so the .so built here
+travels with the repository snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libarslam_lm.so")
+SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "debug_api.hip"]
+ARCH = os.environ.get("ARSLAM_ARCH", "gfx950")
+
+
+def hipcc():
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", f) for f in ("arslam_lm.h", "arslam_lm_debug.h")]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    objdir = os.path.join(HERE, "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
+             "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    objs = []
+    procs = []
+    for src in SOURCES:
+        obj = os.path.join(objdir, src.replace(".hip", ".o"))
+        cmd = [hipcc()] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+    errs = []
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            errs.append(f"--- {src} ---\n{out.decode()}")
+        elif verbose and out:
+            print(out.decode())
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", LIB] + objs + \
+          ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
+    print(LIB)

@@ -1,0 +1,84 @@
+// debug_api.hip -- component entry points (include/arslam_lm_debug.h) that run
+// one device stage in isolation so the parity tests can pin it to the oracle.
+#include "lm_internal.h"
+#include "arslam_lm.h"
+#include "arslam_lm_debug.h"
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace arslam {
+void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,
+                             const double *corners, double *r, double *J, hipStream_t s);
+}
+
+namespace {
+int hip_fail(hipError_t e) { return e == hipSuccess ? ARSLAM_OK : ARSLAM_E_HIP; }
+}
+
+#define DBG_CHECK(x)                 \
+  do {                               \
+    hipError_t _e = (x);             \
+    if (_e != hipSuccess) return hip_fail(_e); \
+  } while (0)
+
+extern "C" int arslam_debug_residual_jacobian(int n, const double *cam, const double *cap,
+                                              const double *tag, const double *corners, double *r,
+                                              double *J) {
+  if (n < 0 || (n && (!cam || !cap || !tag || !corners || !r || !J))) return ARSLAM_E_INVALID_ARG;
+  if (n == 0) return ARSLAM_OK;
+  double *d_in = nullptr, *d_r = nullptr, *d_J = nullptr;
+  const size_t in_n = (size_t)n * 23;
+  DBG_CHECK(hipMalloc(&d_in, in_n * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_r, (size_t)n * 8 * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_J, (size_t)n * 120 * sizeof(double)));
+  std::vector<double> h(in_n);
+  std::memcpy(h.data(), cam, (size_t)n * 3 * sizeof(double));
+  std::memcpy(h.data() + 3L * n, cap, (size_t)n * 6 * sizeof(double));
+  std::memcpy(h.data() + 9L * n, tag, (size_t)n * 6 * sizeof(double));
+  std::memcpy(h.data() + 15L * n, corners, (size_t)n * 8 * sizeof(double));
+  DBG_CHECK(hipMemcpy(d_in, h.data(), in_n * sizeof(double), hipMemcpyHostToDevice));
+  arslam::debug_residual_jacobian(n, d_in, d_in + 3L * n, d_in + 9L * n, d_in + 15L * n, d_r, d_J, 0);
+  DBG_CHECK(hipGetLastError());
+  DBG_CHECK(hipDeviceSynchronize());
+  DBG_CHECK(hipMemcpy(r, d_r, (size_t)n * 8 * sizeof(double), hipMemcpyDeviceToHost));
+  DBG_CHECK(hipMemcpy(J, d_J, (size_t)n * 120 * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(d_in);
+  (void)hipFree(d_r);
+  (void)hipFree(d_J);
+  return ARSLAM_OK;
+}
+
+extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double *y, int *info) {
+  if (n <= 0 || !A || !b || !y || !info) return ARSLAM_E_INVALID_ARG;
+  const long N = (n + 1 + arslam::kTile - 1) / arslam::kTile * arslam::kTile;
+  std::vector<double> h((size_t)N * N, 0.0);
+  for (long i = 0; i < n; ++i)
+    for (long j = 0; j <= i; ++j) h[i * N + j] = A[i * n + j];
+  for (long j = 0; j < n; ++j) h[n * N + j] = b[j];
+  h[n * N + n] = 1e300;
+  for (long i = n + 1; i < N; ++i) h[i * N + i] = 1.0;
+  double *d_S = nullptr, *d_z = nullptr, *d_y = nullptr;
+  int *d_flag = nullptr;
+  DBG_CHECK(hipMalloc(&d_S, (size_t)N * N * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_z, N * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_y, N * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_flag, sizeof(int)));
+  DBG_CHECK(hipMemcpy(d_S, h.data(), (size_t)N * N * sizeof(double), hipMemcpyHostToDevice));
+  DBG_CHECK(hipMemset(d_flag, 0, sizeof(int)));
+  arslam::launch_dense_llt(d_S, N, N, d_flag, nullptr, 0);
+  arslam::launch_dense_back_solve(d_S, N, N, n, d_z, d_y, d_flag, nullptr, 0);
+  DBG_CHECK(hipGetLastError());
+  DBG_CHECK(hipDeviceSynchronize());
+  DBG_CHECK(hipMemcpy(h.data(), d_S, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost));
+  DBG_CHECK(hipMemcpy(y, d_y, n * sizeof(double), hipMemcpyDeviceToHost));
+  DBG_CHECK(hipMemcpy(info, d_flag, sizeof(int), hipMemcpyDeviceToHost));
+  for (long i = 0; i < n; ++i)
+    for (long j = 0; j < n; ++j) A[i * n + j] = j <= i ? h[i * N + j] : 0.0;
+  (void)hipFree(d_S);
+  (void)hipFree(d_z);
+  (void)hipFree(d_y);
+  (void)hipFree(d_flag);
+  return ARSLAM_OK;
+}

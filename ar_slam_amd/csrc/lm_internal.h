@@ -1,0 +1,92 @@
+// lm_internal.h -- device problem layout and kernel launch wrappers shared by
+// the LM driver (lm_solver.hip), the per-capture kernels (lm_kernels.hip) and
+// the reduced-system Cholesky (dense_llt.hip).
+//
+// Parameter slots (one contiguous f64 vector, x):
+//   [0,3)                camera  f, l1, l2
+//   [3 + 6c, 9 + 6c)     capture c inv_pose  t_c, w_c
+//   [3 + 6Nc + 6t, ...)  tag t pose  t_t, w_t
+// Reduced (f-side) index: tag t -> 6t + a, camera -> 6Nt + b (camera last, so
+// the dense system is an arrow-head: banded tag block + one border).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace arslam {
+
+constexpr int kWave = 64;
+constexpr int kTile = 64;          // reduced-system Cholesky tile
+constexpr int kRowStride = 14;     // LDS row: 13 Jacobian entries + residual
+constexpr int kMaxTagsPerCapture = 64;
+
+// number of per-capture partial sums written by the per-capture kernels
+enum PartIdx {
+  P_COST = 0,        // sum 0.5|r|^2 over active observations
+  P_FIXED = 1,       // same, observations whose blocks are all constant
+  P_GF = 2,          // camera-f gradient partial
+  P_CF = 3,          // camera-f squared column norm partial
+  P_MODEL = 4,       // model cost change partial  p.(r - p/2)
+  P_STEP2 = 5,       // squared step norm (capture slots)
+  P_YBAD = 6,        // non-finite step flag (max)
+  P_CBAD = 7,        // non-finite candidate residual flag (max)
+  NPART = 8
+};
+
+struct DevProblem {
+  int nc, nt, nb;
+  long n;              // number of parameter slots 3 + 6nc + 6nt
+  long nF;             // reduced size 6nt + 3
+  long N;              // padded reduced size (multiple of kTile, > nF: row nF holds the rhs)
+  long lda;            // leading dimension of S
+  int max_obs_per_cap;
+  const int *cap_start;      // [nc+1]  CSR of observations by capture
+  const int *obs_tag;        // [nb]
+  const int *obs_lblk;       // [nb]    local f-block (1..) of the observation's tag in its capture
+  const int *cap_blk_start;  // [nc+1]  CSR of distinct tags per capture
+  const int *blk_tag;        // [sum]   tag of each local block
+  const unsigned char *obs_active;   // [nb]
+  const unsigned char *slot_free;    // [n]
+  const int *tag_start;      // [nt+1]  CSR of observations by tag (capture-major order inside)
+  const int *tag_obs;        // [nb]
+  const double *corners;     // [nb*8]
+};
+
+// ---- lm_kernels.hip ----
+void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
+                      double *obs_tg, double *parts, hipStream_t s);
+void launch_tag_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
+                       hipStream_t s);
+void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale,
+                  hipStream_t s);
+void launch_lm_diag(const DevProblem &P, const double *scale, const double *colnorm, double dmin,
+                    double dmax, double *diag, hipStream_t s);
+void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
+                  double radius, double *S, hipStream_t s);
+void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
+                         hipStream_t s);
+void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
+                    double radius, const double *yF, double *xc, double *parts, hipStream_t s);
+void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,
+                     double *xc, double *fparts, hipStream_t s);
+void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_t s);
+// reduce per-capture partials [NPART][nc] (+ f-slot partials) into out[NPART]
+void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts,
+                         double *out, hipStream_t s);
+void launch_camera_slots(const DevProblem &P, const double *red, double *g, double *colnorm,
+                         hipStream_t s);
+// norms over free parameter slots: out[0..2] = max|g|, sum g^2, sum x^2 over capture slots,
+// out[3..5] the same over camera + tag slots
+void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out,
+                       hipStream_t s);
+
+// ---- dense_llt.hip ----
+// Cholesky of the lower triangle of S (N x N, row-major, lda), in place.  Row
+// nF carries the right-hand side, so on exit row nF = (L^{-1} b)^T.  *flag is
+// set non-zero if a pivot is not positive.  Then y = L^{-T} z into yF[0..nF).
+void launch_dense_llt(double *S, long N, long lda, int *flag, const uint8_t *tile_nz,
+                      hipStream_t s);
+void launch_dense_back_solve(const double *S, long N, long lda, long nF, double *z, double *yF,
+                             const int *flag, const uint8_t *tile_nz, hipStream_t s);
+void launch_zero_lower(double *S, long N, long lda, const uint8_t *tile_nz, hipStream_t s);
+
+}  // namespace arslam

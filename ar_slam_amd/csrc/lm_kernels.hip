@@ -1,0 +1,910 @@
+// lm_kernels.hip -- per-capture kernels of the LM step (fp64, gfx950).
+//
+// One 64-lane wavefront per capture (the eliminated Schur e-block).  Lane l
+// of a 64-row chunk owns residual row l = 8*obs + 2*corner + {x,y} of that
+// capture's observations, so the k = 8 observations of a synthetic capture
+// are exactly one wave.  Each lane evaluates its row of the reference's
+// residual (projectCorner, ar_slam_util.cpp:131-172; ArucoReprojectionError
+// :198-211) and the analytic Jacobian into LDS; the
+// wave then forms the capture's normal-equation blocks from LDS:
+//   U_c = E'E + D_c^2 (6x6), W_c = E'F (6 x (1 + 6 n_tags)), F'F, E'r, F'r
+// and scatters its Schur contribution F'F - W'U^{-1}W (lower triangle) and
+// F'r - W'U^{-1}E'r into the dense reduced system with fp64 atomics.
+//
+// Every reduction that feeds an LM decision (cost, model cost change, step
+// and gradient norms) is a fixed-order tree, so the control flow is
+// deterministic; only the S/rhs scatter order (atomics) varies run to run.
+#include "lm_internal.h"
+
+#include <cfloat>
+#include <cmath>
+
+namespace arslam {
+
+namespace {
+
+constexpr double kArucoSize = 0.0635;  // ar_slam_util.hpp:319
+
+__device__ __forceinline__ double corner_dx(int i) { return (i == 1 || i == 2) ? 1.0 : -1.0; }
+__device__ __forceinline__ double corner_dy(int i) { return (i >= 2) ? 1.0 : -1.0; }
+
+// Angle-axis trigonometry with Ceres' branch (rotation.h AngleAxisRotatePoint).
+struct AngleAxis {
+  double w[3];
+  double th2, th, c, s, ti;
+  bool big;
+};
+
+__device__ __forceinline__ AngleAxis aa_prepare(const double *w) {
+  AngleAxis a;
+  a.w[0] = w[0]; a.w[1] = w[1]; a.w[2] = w[2];
+  a.th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  a.big = a.th2 > DBL_EPSILON;
+  if (a.big) {
+    a.th = sqrt(a.th2);
+    sincos(a.th, &a.s, &a.c);
+    a.ti = 1.0 / a.th;
+  } else {
+    a.th = 0.0; a.s = 0.0; a.c = 1.0; a.ti = 0.0;
+  }
+  return a;
+}
+
+// rotate point p by the angle-axis (Ceres operation order)
+__device__ __forceinline__ void aa_rotate(const AngleAxis &a, const double *p, double *out) {
+  if (a.big) {
+    const double u0 = a.w[0] * a.ti, u1 = a.w[1] * a.ti, u2 = a.w[2] * a.ti;
+    const double c0 = u1 * p[2] - u2 * p[1], c1 = u2 * p[0] - u0 * p[2], c2 = u0 * p[1] - u1 * p[0];
+    const double tmp = (u0 * p[0] + u1 * p[1] + u2 * p[2]) * (1.0 - a.c);
+    out[0] = p[0] * a.c + c0 * a.s + u0 * tmp;
+    out[1] = p[1] * a.c + c1 * a.s + u1 * tmp;
+    out[2] = p[2] * a.c + c2 * a.s + u2 * tmp;
+  } else {
+    out[0] = p[0] + (a.w[1] * p[2] - a.w[2] * p[1]);
+    out[1] = p[1] + (a.w[2] * p[0] - a.w[0] * p[2]);
+    out[2] = p[2] + (a.w[0] * p[1] - a.w[1] * p[0]);
+  }
+}
+
+// rotation matrix M of the map p -> rotate(p): R(w) or I + [w]x (small branch)
+__device__ __forceinline__ void aa_matrix(const AngleAxis &a, double M[9]) {
+  if (a.big) {
+    const double u0 = a.w[0] * a.ti, u1 = a.w[1] * a.ti, u2 = a.w[2] * a.ti;
+    const double omc = 1.0 - a.c;
+    M[0] = a.c + omc * u0 * u0;  M[1] = -a.s * u2 + omc * u0 * u1;  M[2] = a.s * u1 + omc * u0 * u2;
+    M[3] = a.s * u2 + omc * u1 * u0;  M[4] = a.c + omc * u1 * u1;  M[5] = -a.s * u0 + omc * u1 * u2;
+    M[6] = -a.s * u1 + omc * u2 * u0;  M[7] = a.s * u0 + omc * u2 * u1;  M[8] = a.c + omc * u2 * u2;
+  } else {
+    M[0] = 1.0;     M[1] = -a.w[2]; M[2] = a.w[1];
+    M[3] = a.w[2];  M[4] = 1.0;     M[5] = -a.w[0];
+    M[6] = -a.w[1]; M[7] = a.w[0];  M[8] = 1.0;
+  }
+}
+
+// right Jacobian of SO(3): Jr = I - A [w]x + B [w]x^2 (big branch only)
+__device__ __forceinline__ void aa_right_jacobian(const AngleAxis &a, double Jr[9]) {
+  double A, B;
+  if (a.th < 0.5) {
+    double t = 1.0, fa = 2.0, fb = 6.0;
+    A = 0.0; B = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      A += t / fa;
+      B += t / fb;
+      t *= -a.th2;
+      fa *= (double)(2 * k + 3) * (2 * k + 4);
+      fb *= (double)(2 * k + 4) * (2 * k + 5);
+    }
+  } else {
+    const double sh = sin(0.5 * a.th);
+    A = 2.0 * sh * sh / a.th2;
+    B = (a.th - a.s) / (a.th2 * a.th);
+  }
+  const double w0 = a.w[0], w1 = a.w[1], w2 = a.w[2];
+  // [w]x and [w]x^2 = w w^T - th2 I
+  Jr[0] = 1.0 + B * (w0 * w0 - a.th2);
+  Jr[1] = A * w2 + B * (w0 * w1);
+  Jr[2] = -A * w1 + B * (w0 * w2);
+  Jr[3] = -A * w2 + B * (w1 * w0);
+  Jr[4] = 1.0 + B * (w1 * w1 - a.th2);
+  Jr[5] = A * w0 + B * (w1 * w2);
+  Jr[6] = A * w1 + B * (w2 * w0);
+  Jr[7] = -A * w0 + B * (w2 * w1);
+  Jr[8] = 1.0 + B * (w2 * w2 - a.th2);
+}
+
+__device__ __forceinline__ void cross3(const double *u, const double *v, double *o) {
+  o[0] = u[1] * v[2] - u[2] * v[1];
+  o[1] = u[2] * v[0] - u[0] * v[2];
+  o[2] = u[0] * v[1] - u[1] * v[0];
+}
+
+// row vector (1x3) times 3x3 matrix
+__device__ __forceinline__ void vecmat3(const double *v, const double *M, double *o) {
+  o[0] = v[0] * M[0] + v[1] * M[3] + v[2] * M[6];
+  o[1] = v[0] * M[1] + v[1] * M[4] + v[2] * M[7];
+  o[2] = v[0] * M[2] + v[1] * M[5] + v[2] * M[8];
+}
+
+// Residual of one row (corner, comp) of ArucoReprojectionError.
+__device__ __forceinline__ double residual_row(const AngleAxis &ac, const double *cap,
+                                               const AngleAxis &at, const double *tag, double f,
+                                               int corner, int comp, double obs, double *a_out,
+                                               double *p_out) {
+  const double cpt[3] = {0.5 * kArucoSize * corner_dx(corner), 0.5 * kArucoSize * corner_dy(corner), 0.0};
+  double a[3], p[3];
+  aa_rotate(at, cpt, a);
+  a[0] += tag[0]; a[1] += tag[1]; a[2] += tag[2];   // ar_slam_util.cpp:146-148
+  a[0] += cap[0]; a[1] += cap[1]; a[2] += cap[2];   // :152-154
+  aa_rotate(ac, a, p);                              // :155
+  const double xy = (comp == 0 ? p[0] : p[1]) / p[2];
+  if (a_out) { a_out[0] = a[0]; a_out[1] = a[1]; a_out[2] = a[2]; }
+  if (p_out) { p_out[0] = p[0]; p_out[1] = p[1]; p_out[2] = p[2]; }
+  return f * xy - obs;
+}
+
+// Residual row and its 13 non-zero Jacobian entries: [f, t_c(3), w_c(3), t_t(3), w_t(3)].
+__device__ __forceinline__ double residual_jacobian_row(const double *cam, const double *cap,
+                                                        const double *tag, int corner, int comp,
+                                                        double obs, double J[13]) {
+  const AngleAxis ac = aa_prepare(cap + 3);
+  const AngleAxis at = aa_prepare(tag + 3);
+  double a[3], p[3];
+  const double f = cam[0];
+  const double r = residual_row(ac, cap, at, tag, f, corner, comp, obs, a, p);
+  const double x = p[0] / p[2], y = p[1] / p[2];
+  const double fz = f / p[2];
+  const double P[3] = {comp == 0 ? fz : 0.0, comp == 0 ? 0.0 : fz, comp == 0 ? -fz * x : -fz * y};
+  double Mc[9];
+  aa_matrix(ac, Mc);
+  double PM[3];
+  vecmat3(P, Mc, PM);
+  J[0] = comp == 0 ? x : y;
+  J[1] = PM[0]; J[2] = PM[1]; J[3] = PM[2];
+  J[7] = PM[0]; J[8] = PM[1]; J[9] = PM[2];
+  // d/dw_c = -((P Mc) x a) Jr_c   (small branch: -(P x a))
+  double v[3];
+  if (ac.big) {
+    cross3(PM, a, v);
+    double Jr[9], o[3];
+    aa_right_jacobian(ac, Jr);
+    vecmat3(v, Jr, o);
+    J[4] = -o[0]; J[5] = -o[1]; J[6] = -o[2];
+  } else {
+    cross3(P, a, v);
+    J[4] = -v[0]; J[5] = -v[1]; J[6] = -v[2];
+  }
+  // d/dw_t = -((P Mc Mt) x c) Jr_t   (small branch: -((P Mc) x c))
+  const double cpt[3] = {0.5 * kArucoSize * corner_dx(corner), 0.5 * kArucoSize * corner_dy(corner), 0.0};
+  if (at.big) {
+    double Mt[9], PMM[3], o[3], Jr[9];
+    aa_matrix(at, Mt);
+    vecmat3(PM, Mt, PMM);
+    cross3(PMM, cpt, v);
+    aa_right_jacobian(at, Jr);
+    vecmat3(v, Jr, o);
+    J[10] = -o[0]; J[11] = -o[1]; J[12] = -o[2];
+  } else {
+    cross3(PM, cpt, v);
+    J[10] = -v[0]; J[11] = -v[1]; J[12] = -v[2];
+  }
+  return r;
+}
+
+__device__ __forceinline__ long slot_cap(const DevProblem &P, int c) { return 3 + 6L * c; }
+__device__ __forceinline__ long slot_tag(const DevProblem &P, int t) { return 3 + 6L * P.nc + 6L * t; }
+
+__device__ __forceinline__ double lm_d2(const double *diag, long slot, double radius) {
+  const double d = sqrt(diag[slot] / radius);   // lm_diagonal_ = sqrt(diag / radius)
+  return d * d;
+}
+
+// Fill LDS rows [nrows][kRowStride] of capture c: 13 Jacobian entries (scaled
+// by the Jacobi scale if scale != nullptr) and the residual in column 13.
+__device__ void fill_rows(const DevProblem &P, const double *x, const double *scale, int c,
+                          int o0, int nrows, double *rows) {
+  const double *cam = x;
+  const double *cap = x + slot_cap(P, c);
+  for (int row = threadIdx.x; row < nrows; row += kWave) {
+    const int q = row >> 3, corner = (row >> 1) & 3, comp = row & 1;
+    const int obs = o0 + q;
+    const int t = P.obs_tag[obs];
+    const double *tag = x + slot_tag(P, t);
+    double J[13];
+    const double r = residual_jacobian_row(cam, cap, tag, corner, comp,
+                                           P.corners[8L * obs + 2 * corner + comp], J);
+    double *dst = rows + (long)row * kRowStride;
+    if (scale) {
+      const double *sc = scale + slot_cap(P, c);
+      const double *st = scale + slot_tag(P, t);
+      dst[0] = J[0] * scale[0];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        dst[1 + j] = J[1 + j] * sc[j];
+        dst[7 + j] = J[7 + j] * st[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 13; ++j) dst[j] = J[j];
+    }
+    dst[13] = r;
+  }
+}
+
+// (a,b) of the e-th entry of the upper triangle of a 6x6 matrix, row-major
+__device__ __forceinline__ void upper6(int e, int &a, int &b) {
+  a = 0;
+  int rem = e;
+  while (rem >= 6 - a) { rem -= 6 - a; ++a; }
+  b = a + rem;
+}
+
+// 6x6 SPD inverse by LLT + two triangular solves against I (Ceres'
+// InvertPSDMatrix<full rank>); single lane.
+__device__ void inv6(const double *U, double *Ui) {
+  double L[36];
+#pragma unroll
+  for (int i = 0; i < 36; ++i) L[i] = U[i];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double xj = L[6 * j + j];
+#pragma unroll
+    for (int p = 0; p < j; ++p) xj -= L[6 * j + p] * L[6 * j + p];
+    const double d = sqrt(xj);
+    L[6 * j + j] = d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double v = L[6 * i + j];
+#pragma unroll
+      for (int p = 0; p < j; ++p) v -= L[6 * i + p] * L[6 * j + p];
+      L[6 * i + j] = v / d;
+    }
+  }
+#pragma unroll
+  for (int col = 0; col < 6; ++col) {
+    double e[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      double v = (i == col) ? 1.0 : 0.0;
+#pragma unroll
+      for (int p = 0; p < i; ++p) v -= L[6 * i + p] * e[p];
+      e[i] = v / L[6 * i + i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+      double v = e[i];
+#pragma unroll
+      for (int p = i + 1; p < 6; ++p) v -= L[6 * p + i] * e[p];
+      e[i] = v / L[6 * i + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) Ui[6 * i + col] = e[i];
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// Sum of rows[r][i]*rows[r][j] (i, j row columns) over the rows of local block u
+// (u = 0: every row).
+__device__ __forceinline__ double block_dot(const double *rows, const int *lblk, int k, int u,
+                                            int i, int j) {
+  double s = 0.0;
+  for (int q = 0; q < k; ++q) {
+    if (u != 0 && lblk[q] != u) continue;
+    const double *rq = rows + (long)q * 8 * kRowStride;
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + i] * rq[rr * kRowStride + j];
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+
+// Linearize at x: per-observation tag gradient/column norms, per-capture
+// gradient/column norms, cost and camera partials.  Unscaled Jacobian.
+__global__ __launch_bounds__(kWave) void k_linearize(DevProblem P, const double *__restrict__ x,
+                                                     double *__restrict__ g,
+                                                     double *__restrict__ colnorm,
+                                                     double *__restrict__ obs_tg,
+                                                     double *__restrict__ parts) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
+  const int nrows = 8 * k;
+  double *rows = sm;
+  double *ocost = rows + (long)nrows * kRowStride;   // [k]
+  fill_rows(P, x, nullptr, c, o0, nrows, rows);
+  __syncthreads();
+  // per observation: cost, tag gradient (6), tag column norms (6)
+  for (int e = lane; e < 13 * k; e += kWave) {
+    const int q = e / 13, it = e % 13;
+    const double *rq = rows + (long)q * 8 * kRowStride;
+    double s = 0.0;
+    if (it == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + 13] * rq[rr * kRowStride + 13];
+      ocost[q] = 0.5 * s;
+    } else if (it <= 6) {
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + 6 + it] * rq[rr * kRowStride + 13];
+      obs_tg[12L * (o0 + q) + (it - 1)] = s;
+    } else {
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const double v = rq[rr * kRowStride + it];
+        s += v * v;
+      }
+      obs_tg[12L * (o0 + q) + (it - 1)] = s;
+    }
+  }
+  // per capture: capture gradient (6), capture column norms (6), f gradient, f column norm
+  if (lane < 14) {
+    double s = 0.0;
+    for (int r = 0; r < nrows; ++r) {
+      const double *rr = rows + (long)r * kRowStride;
+      if (lane < 6) s += rr[1 + lane] * rr[13];
+      else if (lane < 12) s += rr[1 + lane - 6] * rr[1 + lane - 6];
+      else if (lane == 12) s += rr[0] * rr[13];
+      else s += rr[0] * rr[0];
+    }
+    if (lane < 12) {
+      const long slot = slot_cap(P, c) + (lane % 6);
+      const double v = P.slot_free[slot] ? s : 0.0;
+      if (lane < 6) g[slot] = v; else colnorm[slot] = v;
+    } else if (lane == 12) {
+      parts[(long)P_GF * P.nc + c] = s;
+    } else {
+      parts[(long)P_CF * P.nc + c] = s;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    double act = 0.0, fix = 0.0;
+    for (int q = 0; q < k; ++q) {
+      if (P.obs_active[o0 + q]) act += ocost[q]; else fix += ocost[q];
+    }
+    parts[(long)P_COST * P.nc + c] = act;
+    parts[(long)P_FIXED * P.nc + c] = fix;
+  }
+  if (k == 0 && lane < 12) {
+    const long slot = slot_cap(P, c) + (lane % 6);
+    if (lane < 6) g[slot] = 0.0; else colnorm[slot] = 0.0;
+  }
+}
+
+__global__ void k_tag_reduce(DevProblem P, const double *__restrict__ obs_tg,
+                             double *__restrict__ g, double *__restrict__ colnorm) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 12L * P.nt) return;
+  const int t = (int)(e / 12), j = (int)(e % 12);
+  double s = 0.0;
+  for (int q = P.tag_start[t]; q < P.tag_start[t + 1]; ++q) s += obs_tg[12L * P.tag_obs[q] + j];
+  const long slot = slot_tag(P, t) + (j % 6);
+  const double v = P.slot_free[slot] ? s : 0.0;
+  if (j < 6) g[slot] = v; else colnorm[slot] = v;
+}
+
+__global__ void k_scale(long n, const unsigned char *__restrict__ free_, const double *__restrict__ colnorm,
+                        int jacobi, double *__restrict__ scale) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // jacobian_scaling = 1 / (1 + sqrt(SquaredColumnNorm)) at iteration 0
+  scale[i] = free_[i] ? (jacobi ? 1.0 / (1.0 + sqrt(colnorm[i])) : 1.0) : 0.0;
+}
+
+__global__ void k_lm_diag(long n, const double *__restrict__ scale, const double *__restrict__ colnorm,
+                          double dmin, double dmax, double *__restrict__ diag) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double d = scale[i] * scale[i] * colnorm[i];   // squared column norm of J * diag(s)
+  diag[i] = fmin(fmax(d, dmin), dmax);
+}
+
+// Schur elimination of capture c into the dense reduced system S (lower,
+// row-major, lda); row nF of S accumulates the reduced right-hand side.
+__global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ x,
+                                                 const double *__restrict__ scale,
+                                                 const double *__restrict__ diag, double radius,
+                                                 double *__restrict__ S) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
+  if (k == 0) return;
+  const int nrows = 8 * k;
+  const int b0 = P.cap_blk_start[c], nblk = P.cap_blk_start[c + 1] - b0;
+  const int m = 1 + 6 * nblk;   // local f-side columns: f, then 6 per distinct tag
+  double *rows = sm;
+  double *U = rows + (long)nrows * kRowStride;   // 36
+  double *Ui = U + 36;                           // 36
+  double *Etr = Ui + 36;                         // 8
+  double *UiE = Etr + 8;                         // 8
+  double *W = UiE + 8;                           // 6*m
+  double *Z = W + 6 * m;                         // 6*m
+  double *Ftr = Z + 6 * m;                       // m (+pad)
+  int *lblk = (int *)(Ftr + m + (m & 1));        // k
+  long *gidx = (long *)(lblk + k + (k & 1));     // m
+
+  for (int q = lane; q < k; q += kWave) lblk[q] = P.obs_lblk[o0 + q];
+  for (int p = lane; p < m; p += kWave) {
+    if (p == 0) gidx[p] = 6L * P.nt;
+    else gidx[p] = 6L * P.blk_tag[b0 + (p - 1) / 6] + (p - 1) % 6;
+  }
+  fill_rows(P, x, scale, c, o0, nrows, rows);
+  __syncthreads();
+  // U = E'E (21 unique) and E'r
+  if (lane < 27) {
+    if (lane < 21) {
+      int a, b;
+      upper6(lane, a, b);
+      const double s = block_dot(rows, lblk, k, 0, 1 + a, 1 + b);
+      U[6 * a + b] = s;
+      U[6 * b + a] = s;
+    } else {
+      const int a = lane - 21;
+      Etr[a] = block_dot(rows, lblk, k, 0, 1 + a, 13);
+    }
+  }
+  // W = E'F and F'r (local column 0 = f over all rows; 1+6u+j = tag block u+1)
+  for (int e = lane; e < 7 * m; e += kWave) {
+    const int a = e / m, col = e % m;   // a == 6 -> F'r
+    const int u = col == 0 ? 0 : 1 + (col - 1) / 6;
+    const int fcol = col == 0 ? 0 : 7 + (col - 1) % 6;
+    const int ecol = a < 6 ? 1 + a : 13;
+    const double s = block_dot(rows, lblk, k, u, ecol, fcol);
+    if (a < 6) W[a * m + col] = s; else Ftr[col] = s;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    const long sc = slot_cap(P, c);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) U[7 * a] += lm_d2(diag, sc + a, radius);
+    inv6(U, Ui);
+  }
+  __syncthreads();
+  // Z = Ui W ; UiE = Ui E'r
+  for (int e = lane; e < 6 * m + 6; e += kWave) {
+    if (e < 6 * m) {
+      const int a = e / m, col = e % m;
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * W[b * m + col];
+      Z[a * m + col] = s;
+    } else {
+      const int a = e - 6 * m;
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * Etr[b];
+      UiE[a] = s;
+    }
+  }
+  __syncthreads();
+  const long lda = P.lda;
+  double *rhs = S + P.nF * lda;
+  // reduced rhs: F'r - W' Ui E'r
+  for (int p = lane; p < m; p += kWave) {
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) s += W[a * m + p] * UiE[a];
+    atomicAdd(rhs + gidx[p], Ftr[p] - s);
+  }
+  // reduced matrix: F'F - W' Ui W, local pairs p >= q
+  const int npairs = m * (m + 1) / 2;
+  for (int e = lane; e < npairs; e += kWave) {
+    int p = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    while (p * (p + 1) / 2 > e) --p;
+    while ((p + 1) * (p + 2) / 2 <= e) ++p;
+    const int q = e - p * (p + 1) / 2;
+    // F'F entry
+    double ff = 0.0;
+    const int up = p == 0 ? 0 : 1 + (p - 1) / 6, uq = q == 0 ? 0 : 1 + (q - 1) / 6;
+    if (up == 0 || uq == 0 || up == uq) {
+      const int u = up == 0 ? uq : up;   // rows shared by both columns
+      const int ip = p == 0 ? 0 : 7 + (p - 1) % 6, iq = q == 0 ? 0 : 7 + (q - 1) % 6;
+      ff = block_dot(rows, lblk, k, u, ip, iq);
+    }
+    double wz = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) wz += W[a * m + p] * Z[a * m + q];
+    const long gi = gidx[p], gj = gidx[q];
+    const long hi = gi > gj ? gi : gj, lo = gi > gj ? gj : gi;
+    atomicAdd(S + hi * lda + lo, ff - wz);
+  }
+}
+
+// S[i][i] += D_f^2 for the reduced (tag + camera) index; padding rows become
+// identity rows; the rhs row gets a pivot large enough to stay positive.
+__global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, double radius,
+                               double *__restrict__ S) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.N) return;
+  double *d = S + i * P.lda + i;
+  if (i < P.nF) {
+    const long slot = i < 6L * P.nt ? slot_tag(P, (int)(i / 6)) + i % 6 : (i - 6L * P.nt);
+    *d += lm_d2(diag, slot, radius);
+  } else if (i == P.nF) {
+    *d = 1e300;
+  } else {
+    *d = 1.0;
+  }
+}
+
+// Back substitution for capture c, candidate update of its slots and its
+// share of the model cost change.
+__global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *__restrict__ x,
+                                                   const double *__restrict__ scale,
+                                                   const double *__restrict__ diag, double radius,
+                                                   const double *__restrict__ yF,
+                                                   double *__restrict__ xc,
+                                                   double *__restrict__ parts) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
+  const long sc = slot_cap(P, c);
+  if (k == 0) {
+    if (lane < 6) xc[sc + lane] = x[sc + lane];
+    if (lane == 0) {
+      parts[(long)P_MODEL * P.nc + c] = 0.0;
+      parts[(long)P_STEP2 * P.nc + c] = 0.0;
+      parts[(long)P_YBAD * P.nc + c] = 0.0;
+    }
+    return;
+  }
+  const int nrows = 8 * k;
+  double *rows = sm;
+  double *qv = rows + (long)nrows * kRowStride;   // [nrows]
+  double *U = qv + nrows;                         // 36
+  double *Ui = U + 36;                            // 36
+  double *v = Ui + 36;                            // 8
+  double *yc = v + 8;                             // 8
+  fill_rows(P, x, scale, c, o0, nrows, rows);
+  __syncthreads();
+  const double yf = yF[6L * P.nt];
+  for (int row = lane; row < nrows; row += kWave) {
+    const double *rr = rows + (long)row * kRowStride;
+    const long tb = 6L * P.obs_tag[o0 + (row >> 3)];
+    double q = rr[0] * yf;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) q += rr[7 + j] * yF[tb + j];
+    qv[row] = q;
+  }
+  __syncthreads();
+  if (lane < 27) {
+    double s = 0.0;
+    if (lane < 21) {
+      int a, b;
+      upper6(lane, a, b);
+      for (int r = 0; r < nrows; ++r) s += rows[(long)r * kRowStride + 1 + a] * rows[(long)r * kRowStride + 1 + b];
+      U[6 * a + b] = s;
+      U[6 * b + a] = s;
+    } else {
+      const int a = lane - 21;
+      for (int r = 0; r < nrows; ++r) {
+        const double *rr = rows + (long)r * kRowStride;
+        s += rr[1 + a] * (rr[13] - qv[r]);   // E'(b - F z)
+      }
+      v[a] = s;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 6; ++a) U[7 * a] += lm_d2(diag, sc + a, radius);
+    inv6(U, Ui);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * v[b];
+      yc[a] = s;
+    }
+  }
+  __syncthreads();
+  // model cost change share: p = Jt y (= -Jt step), sum p (r - p/2)
+  double mpart = 0.0;
+  for (int row = lane; row < nrows; row += kWave) {
+    const double *rr = rows + (long)row * kRowStride;
+    double p = qv[row];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) p += rr[1 + a] * yc[a];
+    mpart += p * (rr[13] - p / 2.0);
+  }
+  mpart = wave_sum(mpart);
+  double st = 0.0, bad = 0.0;
+  if (lane < 6) {
+    const double yv = yc[lane];
+    const double d = -yv * scale[sc + lane];
+    const double xo = x[sc + lane];
+    const double xn = xo + d;
+    xc[sc + lane] = xn;
+    if (P.slot_free[sc + lane]) st = (xo - xn) * (xo - xn);
+    bad = isfinite(yv) ? 0.0 : 1.0;
+  }
+  st = wave_sum(st);
+  bad = wave_max(bad);
+  if (lane == 0) {
+    parts[(long)P_MODEL * P.nc + c] = mpart;
+    parts[(long)P_STEP2 * P.nc + c] = st;
+    parts[(long)P_YBAD * P.nc + c] = bad;
+  }
+}
+
+// Candidate update of the tag and camera slots from the reduced solution.
+__global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__restrict__ x,
+                                                  const double *__restrict__ scale,
+                                                  const double *__restrict__ yF,
+                                                  double *__restrict__ xc,
+                                                  double *__restrict__ fparts) {
+  __shared__ double red[2][256];
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  double st = 0.0, bad = 0.0;
+  if (i < P.nF) {
+    const long slot = i < 6L * P.nt ? slot_tag(P, (int)(i / 6)) + i % 6 : (i - 6L * P.nt);
+    const double yv = yF[i];
+    const double xo = x[slot];
+    const double xn = xo + (-yv * scale[slot]);
+    xc[slot] = xn;
+    if (P.slot_free[slot]) st = (xo - xn) * (xo - xn);
+    bad = isfinite(yv) ? 0.0 : 1.0;
+  }
+  red[0][threadIdx.x] = st;
+  red[1][threadIdx.x] = bad;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + off];
+      red[1][threadIdx.x] = fmax(red[1][threadIdx.x], red[1][threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    fparts[2L * blockIdx.x] = red[0][0];
+    fparts[2L * blockIdx.x + 1] = red[1][0];
+  }
+}
+
+// Cost at x (candidate evaluation): per-capture active / fixed cost, finiteness.
+__global__ __launch_bounds__(kWave) void k_cost(DevProblem P, const double *__restrict__ x,
+                                                double *__restrict__ parts) {
+  __shared__ double sq[kWave];
+  __shared__ double ocost[kMaxTagsPerCapture];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
+  const int nrows = 8 * k;
+  const double *cam = x;
+  const double *cap = x + slot_cap(P, c);
+  const AngleAxis ac = aa_prepare(cap + 3);
+  double bad = 0.0;
+  for (int base = 0; base < nrows; base += kWave) {
+    const int row = base + lane;
+    double r2 = 0.0;
+    if (row < nrows) {
+      const int q = row >> 3, corner = (row >> 1) & 3, comp = row & 1;
+      const int obs = o0 + q;
+      const double *tag = x + slot_tag(P, P.obs_tag[obs]);
+      const AngleAxis at = aa_prepare(tag + 3);
+      const double r = residual_row(ac, cap, at, tag, cam[0], corner, comp,
+                                    P.corners[8L * obs + 2 * corner + comp], nullptr, nullptr);
+      if (!isfinite(r)) bad = 1.0;
+      r2 = r * r;
+    }
+    sq[lane] = r2;
+    __syncthreads();
+    if (lane < 8 && base / 8 + lane < k) {
+      double s = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) s += sq[8 * lane + rr];
+      ocost[base / 8 + lane] = 0.5 * s;
+    }
+    __syncthreads();
+  }
+  bad = wave_max(bad);
+  if (lane == 0) {
+    double act = 0.0, fix = 0.0;
+    for (int q = 0; q < k; ++q) {
+      if (P.obs_active[o0 + q]) act += ocost[q]; else fix += ocost[q];
+    }
+    parts[(long)P_COST * P.nc + c] = act;
+    parts[(long)P_FIXED * P.nc + c] = fix;
+    parts[(long)P_CBAD * P.nc + c] = bad;
+  }
+}
+
+// Deterministic single-block reduction of the per-capture partials.
+// out[p] for p < NPART: sum (max for the *BAD flags); out[NPART] = F-side step^2,
+// out[NPART+1] = F-side non-finite flag.
+__global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
+                                                       const double *__restrict__ fparts,
+                                                       int nfparts, double *__restrict__ out) {
+  __shared__ double red[1024];
+  const int t = threadIdx.x;
+  for (int p = 0; p < NPART + 2; ++p) {
+    const bool is_max = (p == P_YBAD || p == P_CBAD || p == NPART + 1);
+    double acc = 0.0;
+    if (p < NPART) {
+      for (int i = t; i < nc; i += 1024) {
+        const double v = parts[(long)p * nc + i];
+        acc = is_max ? fmax(acc, v) : acc + v;
+      }
+    } else if (fparts) {
+      for (int i = t; i < nfparts; i += 1024) {
+        const double v = fparts[2L * i + (p - NPART)];
+        acc = is_max ? fmax(acc, v) : acc + v;
+      }
+    }
+    red[t] = acc;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+      if (t < off) red[t] = is_max ? fmax(red[t], red[t + off]) : red[t] + red[t + off];
+      __syncthreads();
+    }
+    if (t == 0) out[p] = red[0];
+    __syncthreads();
+  }
+}
+
+// Norms over free parameter slots, split into capture slots (out[0..2]) and
+// camera + tag slots (out[3..5]): max |g|, sum g^2, sum x^2.  The split lets
+// the capture-sharded path reduce only the disjoint capture part across ranks.
+__global__ __launch_bounds__(1024) void k_slot_norms(long n, long cap_lo, long cap_hi,
+                                                     const unsigned char *__restrict__ free_,
+                                                     const double *__restrict__ g,
+                                                     const double *__restrict__ x,
+                                                     double *__restrict__ out) {
+  __shared__ double red[6][1024];
+  const int t = threadIdx.x;
+  double v[6] = {0, 0, 0, 0, 0, 0};
+  for (long i = t; i < n; i += 1024) {
+    if (!free_[i]) continue;
+    const int o = (i >= cap_lo && i < cap_hi) ? 0 : 3;
+    const double gv = g[i], xv = x[i];
+    v[o] = fmax(v[o], fabs(gv));
+    v[o + 1] += gv * gv;
+    v[o + 2] += xv * xv;
+  }
+  for (int q = 0; q < 6; ++q) red[q][t] = v[q];
+  __syncthreads();
+  for (int off = 512; off > 0; off >>= 1) {
+    if (t < off) {
+      red[0][t] = fmax(red[0][t], red[0][t + off]);
+      red[1][t] += red[1][t + off];
+      red[2][t] += red[2][t + off];
+      red[3][t] = fmax(red[3][t], red[3][t + off]);
+      red[4][t] += red[4][t + off];
+      red[5][t] += red[5][t + off];
+    }
+    __syncthreads();
+  }
+  if (t < 6) out[t] = red[t][0];
+}
+
+// camera slots from the reduced per-capture partials (masked by freedom)
+__global__ void k_camera_slots(const unsigned char *__restrict__ free_, const double *__restrict__ red,
+                               double *__restrict__ g, double *__restrict__ colnorm) {
+  if (threadIdx.x == 0) {
+    g[0] = free_[0] ? red[P_GF] : 0.0;
+    colnorm[0] = free_[0] ? red[P_CF] : 0.0;
+    g[1] = g[2] = 0.0;
+    colnorm[1] = colnorm[2] = 0.0;
+  }
+}
+
+// one thread per (observation, row): residual and 15-column Jacobian row
+__global__ void k_debug_rj(int n, const double *__restrict__ cam, const double *__restrict__ cap,
+                           const double *__restrict__ tag, const double *__restrict__ corners,
+                           double *__restrict__ r, double *__restrict__ J) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 8L * n) return;
+  const long o = e / 8;
+  const int row = (int)(e % 8), corner = row >> 1, comp = row & 1;
+  double j13[13];
+  r[e] = residual_jacobian_row(cam + 3 * o, cap + 6 * o, tag + 6 * o, corner, comp,
+                               corners[8 * o + row], j13);
+  double *out = J + e * 15;
+  out[0] = j13[0];
+  out[1] = 0.0;
+  out[2] = 0.0;
+  for (int j = 0; j < 12; ++j) out[3 + j] = j13[1 + j];
+}
+
+size_t lds_rows(int maxk) { return (size_t)8 * maxk * kRowStride * sizeof(double); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+
+void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
+                      double *obs_tg, double *parts, hipStream_t s) {
+  if (P.nc == 0) return;
+  const size_t lds = lds_rows(P.max_obs_per_cap) + sizeof(double) * (P.max_obs_per_cap + 2);
+  hipLaunchKernelGGL(k_linearize, dim3(P.nc), dim3(kWave), lds, s, P, x, g, colnorm, obs_tg, parts);
+}
+
+void launch_tag_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
+                       hipStream_t s) {
+  if (P.nt == 0) return;
+  const long n = 12L * P.nt;
+  hipLaunchKernelGGL(k_tag_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, obs_tg, g, colnorm);
+}
+
+void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale, dim3((unsigned)((P.n + 255) / 256)), dim3(256), 0, s, P.n, P.slot_free,
+                     colnorm, jacobi, scale);
+}
+
+void launch_lm_diag(const DevProblem &P, const double *scale, const double *colnorm, double dmin,
+                    double dmax, double *diag, hipStream_t s) {
+  hipLaunchKernelGGL(k_lm_diag, dim3((unsigned)((P.n + 255) / 256)), dim3(256), 0, s, P.n, scale,
+                     colnorm, dmin, dmax, diag);
+}
+
+void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
+                  double radius, double *S, hipStream_t s) {
+  if (P.nc == 0) return;
+  const int maxk = P.max_obs_per_cap;
+  const int m = 1 + 6 * maxk;
+  const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 8 + 13L * m + 4) +
+                     sizeof(int) * (maxk + 2) + sizeof(long) * m + 64;
+  hipLaunchKernelGGL(k_schur, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, S);
+}
+
+void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_prep_reduced, dim3((unsigned)((P.N + 255) / 256)), dim3(256), 0, s, P, diag,
+                     radius, S);
+}
+
+void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
+                    double radius, const double *yF, double *xc, double *parts, hipStream_t s) {
+  if (P.nc == 0) return;
+  const int maxk = P.max_obs_per_cap;
+  const size_t lds = lds_rows(maxk) + sizeof(double) * (8L * maxk + 36 + 36 + 16);
+  hipLaunchKernelGGL(k_backsub, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts);
+}
+
+void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,
+                     double *xc, double *fparts, hipStream_t s) {
+  if (P.nF == 0) return;
+  hipLaunchKernelGGL(k_update_f, dim3((unsigned)((P.nF + 255) / 256)), dim3(256), 0, s, P, x, scale, yF,
+                     xc, fparts);
+}
+
+void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_t s) {
+  if (P.nc == 0) return;
+  hipLaunchKernelGGL(k_cost, dim3(P.nc), dim3(kWave), 0, s, P, x, parts);
+}
+
+void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_parts, dim3(1), dim3(1024), 0, s, parts, nc, fparts, nfparts, out);
+}
+
+void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_slot_norms, dim3(1), dim3(1024), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g, x, out);
+}
+
+void launch_camera_slots(const DevProblem &P, const double *red, double *g, double *colnorm,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_camera_slots, dim3(1), dim3(64), 0, s, P.slot_free, red, g, colnorm);
+}
+
+void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,
+                             const double *corners, double *r, double *J, hipStream_t s) {
+  const long m = 8L * n;
+  hipLaunchKernelGGL(k_debug_rj, dim3((unsigned)((m + 127) / 128)), dim3(128), 0, s, n, cam, cap, tag,
+                     corners, r, J);
+}
+
+}  // namespace arslam

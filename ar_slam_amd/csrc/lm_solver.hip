@@ -1,0 +1,817 @@
+// lm_solver.hip -- host side of the MI355X LM bundle adjuster and its C-ABI
+// (include/arslam_lm.h).
+//
+// The trust-region loop restates Ceres 2.0's TrustRegionMinimizer +
+// LevenbergMarquardtStrategy as configured by ArSlamSolver::optimize
+// (ar_slam_util.cpp:1001-1018).  Only scalars cross
+// PCIe per step (cost, model cost change, norms, the Cholesky flag); the
+// problem, the parameters and the reduced system stay resident in HBM.
+#include "lm_internal.h"
+#include "arslam_lm.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                      \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      throw Error(_e == hipErrorOutOfMemory ? ARSLAM_E_OUT_OF_MEMORY : ARSLAM_E_HIP,         \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));                       \
+  } while (0)
+
+#define NCCL_CHECK(expr)                                                                     \
+  do {                                                                                       \
+    ncclResult_t _r = (expr);                                                                \
+    if (_r != ncclSuccess)                                                                   \
+      throw Error(ARSLAM_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(_r));       \
+  } while (0)
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <class T>
+struct DevBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    release();
+    n = count;
+    if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+  }
+  void upload(const T *h, size_t count, hipStream_t s) {
+    if (count) HIP_CHECK(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DevBuf() { release(); }
+};
+
+struct Timer {
+  hipEvent_t a = nullptr, b = nullptr;
+  double acc_ms = 0.0;
+  bool pending = false;
+  void init() {
+    if (!a) {
+      HIP_CHECK(hipEventCreate(&a));
+      HIP_CHECK(hipEventCreate(&b));
+    }
+  }
+  void start(hipStream_t s) { HIP_CHECK(hipEventRecord(a, s)); }
+  void stop(hipStream_t s) {
+    HIP_CHECK(hipEventRecord(b, s));
+    pending = true;
+  }
+  void collect() {  // call after the stream was synchronized
+    if (!pending) return;
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    acc_ms += ms;
+    pending = false;
+  }
+  void destroy() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    a = b = nullptr;
+  }
+};
+
+enum { PH_LIN, PH_SCHUR, PH_CHOL, PH_SOLVE, PH_BACK, PH_COST, PH_N };
+
+}  // namespace
+
+struct arslam_lm {
+  arslam_lm_options opt;
+
+  // ---- pointer-keyed problem (Ceres API mirror) ----
+  double *camera_ptr = nullptr;
+  std::unordered_map<double *, int> cap_of, tag_of;
+  std::vector<double *> cap_ptrs, tag_ptrs;
+  std::vector<int> pk_obs_cap, pk_obs_tag;
+  std::vector<double> pk_corners;
+  std::unordered_set<double *> constant;
+
+  // ---- loaded problem ----
+  bool loaded = false;
+  arslam_soa_problem soa{};
+  int nc = 0, nt = 0, nb = 0;
+  long n = 0, nF = 0, N = 0;
+  bool has_f = false;
+  std::vector<unsigned char> slot_free;
+  std::vector<double> x0;   // initial slots
+  arslam::DevProblem P{};
+  hipStream_t stream = nullptr;
+  int device = 0;
+
+  DevBuf<int> d_cap_start, d_obs_tag, d_obs_lblk, d_cap_blk_start, d_blk_tag, d_tag_start, d_tag_obs;
+  DevBuf<unsigned char> d_obs_active, d_slot_free;
+  DevBuf<double> d_corners, d_x0, d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
+  DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_norms, d_S, d_z, d_yF;
+  DevBuf<int> d_flag;
+  double *x = nullptr, *xc = nullptr;
+  int n_fparts = 0;
+
+  Timer timers[PH_N];
+
+  // ---- multi-GPU ----
+  int rank = 0, nranks = 1;
+  ncclComm_t comm = nullptr;
+
+  ~arslam_lm() {
+    for (auto &t : timers) t.destroy();
+    if (comm) (void)ncclCommDestroy(comm);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  void allreduce(double *buf, size_t count, ncclRedOp_t op) {
+    if (!comm || nranks <= 1 || count == 0) return;
+    NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclDouble, op, comm, stream));
+  }
+
+  void ensure_stream() {
+    if (opt.device >= 0) HIP_CHECK(hipSetDevice(opt.device));
+    HIP_CHECK(hipGetDevice(&device));
+    if (!stream) HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (auto &t : timers) t.init();
+  }
+
+  void load(const arslam_soa_problem *p);
+  void linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
+  void solve(arslam_lm_summary *s);
+  void write_back(const double *d_src);
+};
+
+namespace {
+
+void fail_if(bool cond, int code, const std::string &msg) {
+  if (cond) throw Error(code, msg);
+}
+
+long round_up(long v, long m) { return (v + m - 1) / m * m; }
+
+}  // namespace
+
+void arslam_lm::load(const arslam_soa_problem *p) {
+  fail_if(!p, ARSLAM_E_INVALID_ARG, "null problem");
+  fail_if(p->n_cap < 0 || p->n_tag < 0 || p->n_obs < 0, ARSLAM_E_INVALID_ARG, "negative sizes");
+  fail_if(!p->camera || (p->n_cap && !p->cap) || (p->n_tag && !p->tag), ARSLAM_E_INVALID_ARG,
+          "null parameter arrays");
+  fail_if(p->n_obs && (!p->obs_cap || !p->obs_tag || !p->corners), ARSLAM_E_INVALID_ARG,
+          "null observation arrays");
+  ensure_stream();
+  soa = *p;
+  nc = p->n_cap;
+  nt = p->n_tag;
+  nb = p->n_obs;
+  n = 3 + 6L * nc + 6L * nt;
+  nF = 6L * nt + 3;
+
+  // capture-major observation order (stable)
+  std::vector<int> cap_start(nc + 1, 0);
+  for (int b = 0; b < nb; ++b) {
+    fail_if(p->obs_cap[b] < 0 || p->obs_cap[b] >= nc, ARSLAM_E_INVALID_ARG, "obs_cap out of range");
+    fail_if(p->obs_tag[b] < 0 || p->obs_tag[b] >= nt, ARSLAM_E_INVALID_ARG, "obs_tag out of range");
+    cap_start[p->obs_cap[b] + 1]++;
+  }
+  int maxk = 0;
+  for (int c = 0; c < nc; ++c) {
+    maxk = std::max(maxk, cap_start[c + 1]);
+    cap_start[c + 1] += cap_start[c];
+  }
+  fail_if(maxk > arslam::kMaxTagsPerCapture, ARSLAM_E_UNSUPPORTED,
+          "more than 64 observations in one capture");
+  std::vector<int> order(nb);
+  {
+    std::vector<int> fill(cap_start.begin(), cap_start.end() - 1);
+    for (int b = 0; b < nb; ++b) order[fill[p->obs_cap[b]]++] = b;
+  }
+  std::vector<int> obs_tag(nb), obs_lblk(nb), cap_blk_start(nc + 1, 0), blk_tag;
+  std::vector<double> corners(8L * nb);
+  blk_tag.reserve(nb);
+  for (int c = 0; c < nc; ++c) {
+    cap_blk_start[c] = (int)blk_tag.size();
+    for (int q = cap_start[c]; q < cap_start[c + 1]; ++q) {
+      const int b = order[q];
+      const int t = p->obs_tag[b];
+      obs_tag[q] = t;
+      std::memcpy(&corners[8L * q], p->corners + 8L * b, 8 * sizeof(double));
+      int u = -1;
+      for (int i = cap_blk_start[c]; i < (int)blk_tag.size(); ++i)
+        if (blk_tag[i] == t) { u = i - cap_blk_start[c]; break; }
+      if (u < 0) { u = (int)blk_tag.size() - cap_blk_start[c]; blk_tag.push_back(t); }
+      obs_lblk[q] = u + 1;
+    }
+  }
+  cap_blk_start[nc] = (int)blk_tag.size();
+  // tag CSR over the capture-major order
+  std::vector<int> tag_start(nt + 1, 0), tag_obs(nb);
+  for (int q = 0; q < nb; ++q) tag_start[obs_tag[q] + 1]++;
+  for (int t = 0; t < nt; ++t) tag_start[t + 1] += tag_start[t];
+  {
+    std::vector<int> fill(tag_start.begin(), tag_start.end() - 1);
+    for (int q = 0; q < nb; ++q) tag_obs[fill[obs_tag[q]]++] = q;
+  }
+  // Free slots: a block is a parameter iff a residual uses it and it is not
+  // held constant (Ceres removes unused and constant blocks).  Tag use and
+  // the observation count are global over ranks.
+  std::vector<double> tag_deg(nt + 1, 0.0);
+  for (int q = 0; q < nb; ++q) tag_deg[obs_tag[q]] += 1.0;
+  tag_deg[nt] = nb;
+  if (comm && nranks > 1) {
+    DevBuf<double> tmp;
+    tmp.alloc(nt + 1);
+    tmp.upload(tag_deg.data(), nt + 1, stream);
+    allreduce(tmp.p, nt + 1, ncclSum);
+    HIP_CHECK(hipMemcpyAsync(tag_deg.data(), tmp.p, (nt + 1) * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+  }
+  slot_free.assign(n, 0);
+  const bool cam_free = !p->camera_const && tag_deg[nt] > 0;
+  for (int j = 0; j < 3; ++j) slot_free[j] = cam_free;
+  for (int c = 0; c < nc; ++c) {
+    const bool f = cap_start[c + 1] > cap_start[c] && !(p->cap_const && p->cap_const[c]);
+    for (int j = 0; j < 6; ++j) slot_free[3 + 6L * c + j] = f;
+  }
+  has_f = cam_free;
+  for (int t = 0; t < nt; ++t) {
+    const bool f = tag_deg[t] > 0 && !(p->tag_const && p->tag_const[t]);
+    for (int j = 0; j < 6; ++j) slot_free[3 + 6L * nc + 6L * t + j] = f;
+    has_f = has_f || f;
+  }
+  std::vector<unsigned char> obs_active(nb);
+  for (int q = 0; q < nb; ++q) {
+    const int c = p->obs_cap[order[q]];
+    obs_active[q] = slot_free[0] || slot_free[3 + 6L * c] || slot_free[3 + 6L * nc + 6L * obs_tag[q]];
+  }
+  x0.resize(n);
+  std::memcpy(x0.data(), p->camera, 3 * sizeof(double));
+  if (nc) std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
+  if (nt) std::memcpy(x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
+
+  // ---- device upload ----
+  d_cap_start.alloc(nc + 1); d_cap_start.upload(cap_start.data(), nc + 1, stream);
+  d_obs_tag.alloc(nb); d_obs_tag.upload(obs_tag.data(), nb, stream);
+  d_obs_lblk.alloc(nb); d_obs_lblk.upload(obs_lblk.data(), nb, stream);
+  d_cap_blk_start.alloc(nc + 1); d_cap_blk_start.upload(cap_blk_start.data(), nc + 1, stream);
+  d_blk_tag.alloc(std::max<size_t>(blk_tag.size(), 1)); d_blk_tag.upload(blk_tag.data(), blk_tag.size(), stream);
+  d_tag_start.alloc(nt + 1); d_tag_start.upload(tag_start.data(), nt + 1, stream);
+  d_tag_obs.alloc(std::max(nb, 1)); d_tag_obs.upload(tag_obs.data(), nb, stream);
+  d_obs_active.alloc(std::max(nb, 1)); d_obs_active.upload(obs_active.data(), nb, stream);
+  d_slot_free.alloc(n); d_slot_free.upload(slot_free.data(), n, stream);
+  d_corners.alloc(std::max(8L * nb, 1L)); d_corners.upload(corners.data(), 8L * nb, stream);
+  d_x0.alloc(n); d_x0.upload(x0.data(), n, stream);
+  d_xa.alloc(n); d_xb.alloc(n); d_xbest.alloc(n);
+  d_g.alloc(n); d_colnorm.alloc(n); d_scale.alloc(n); d_diag.alloc(n);
+  d_obs_tg.alloc(std::max(12L * nb, 1L));
+  d_parts.alloc((size_t)arslam::NPART * std::max(nc, 1));
+  n_fparts = (int)((nF + 255) / 256);
+  d_fparts.alloc(2L * std::max(n_fparts, 1));
+  d_red.alloc(16);
+  d_norms.alloc(8);
+  d_flag.alloc(1);
+  if (has_f) {
+    N = round_up(nF + 1, arslam::kTile);
+    d_S.alloc((size_t)N * N);
+    HIP_CHECK(hipMemsetAsync(d_S.p, 0, (size_t)N * N * sizeof(double), stream));
+    d_z.alloc(N);
+    d_yF.alloc(N);
+  } else {
+    N = 0;
+    d_S.release();
+    d_z.release();
+    d_yF.alloc(nF);
+    HIP_CHECK(hipMemsetAsync(d_yF.p, 0, nF * sizeof(double), stream));
+  }
+  HIP_CHECK(hipMemsetAsync(d_parts.p, 0, d_parts.n * sizeof(double), stream));
+
+  P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nF = nF; P.N = N; P.lda = N;
+  P.max_obs_per_cap = std::max(maxk, 1);
+  P.cap_start = d_cap_start.p; P.obs_tag = d_obs_tag.p; P.obs_lblk = d_obs_lblk.p;
+  P.cap_blk_start = d_cap_blk_start.p; P.blk_tag = d_blk_tag.p;
+  P.obs_active = d_obs_active.p; P.slot_free = d_slot_free.p;
+  P.tag_start = d_tag_start.p; P.tag_obs = d_tag_obs.p; P.corners = d_corners.p;
+  HIP_CHECK(hipStreamSynchronize(stream));
+  loaded = true;
+}
+
+// Evaluate residuals/Jacobian at x: cost, gradient (unscaled), column norms
+// and the norms the minimizer reads.  Ceres EvaluateGradientAndJacobian.
+void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
+                          double *xnorm) {
+  timers[PH_LIN].start(stream);
+  arslam::launch_linearize(P, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
+  arslam::launch_tag_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, stream);
+  arslam::launch_reduce_parts(d_parts.p, nc, nullptr, 0, d_red.p, stream);
+  if (nranks > 1) {
+    const long t0 = 3 + 6L * nc;
+    allreduce(d_g.p + t0, n - t0, ncclSum);
+    allreduce(d_colnorm.p + t0, n - t0, ncclSum);
+    allreduce(d_red.p, 4, ncclSum);   // cost, fixed, g_f, col_f
+  }
+  arslam::launch_camera_slots(P, d_red.p, d_g.p, d_colnorm.p, stream);
+  arslam::launch_slot_norms(P, d_g.p, x, d_norms.p, stream);
+  timers[PH_LIN].stop(stream);
+  double red[4], norms[6];
+  HIP_CHECK(hipMemcpyAsync(red, d_red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipMemcpyAsync(norms, d_norms.p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  if (nranks > 1) {
+    // capture slots are disjoint across ranks, tag/camera slots replicated:
+    // norms[0..2] cover captures, norms[3..5] the rest
+    double cap_part[3] = {norms[0], norms[1], norms[2]};
+    DevBuf<double> tmp;
+    tmp.alloc(3);
+    tmp.upload(cap_part, 3, stream);
+    allreduce(tmp.p, 1, ncclMax);
+    allreduce(tmp.p + 1, 2, ncclSum);
+    HIP_CHECK(hipMemcpyAsync(cap_part, tmp.p, 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    norms[0] = cap_part[0]; norms[1] = cap_part[1]; norms[2] = cap_part[2];
+  }
+  *x_cost = red[arslam::P_COST];
+  *fixed_cost = red[arslam::P_FIXED];
+  *gmax = std::max(norms[0], norms[3]);
+  *gnorm = std::sqrt(norms[1] + norms[4]);
+  *xnorm = std::sqrt(norms[2] + norms[5]);
+  timers[PH_LIN].collect();
+}
+
+void arslam_lm::write_back(const double *d_src) {
+  std::vector<double> h(n);
+  HIP_CHECK(hipMemcpyAsync(h.data(), d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  std::memcpy(soa.camera, h.data(), 3 * sizeof(double));
+  if (nc) std::memcpy(soa.cap, h.data() + 3, 6L * nc * sizeof(double));
+  if (nt) std::memcpy(soa.tag, h.data() + 3 + 6L * nc, 6L * nt * sizeof(double));
+}
+
+namespace {
+
+void print_header() {
+  std::printf("iter      cost      cost_change  |gradient|   |step|    tr_ratio  tr_radius  ls_iter  iter_time  total_time\n");
+}
+
+void print_row(const arslam_lm_iteration &it) {
+  std::printf("% 4d % 8e   % 3.2e   % 3.2e  % 3.2e  % 3.2e % 3.2e     % 4d   % 3.2e   % 3.2e\n",
+              it.iteration, it.cost, it.cost_change, it.gradient_max_norm, it.step_norm,
+              it.relative_decrease, it.trust_region_radius, 0, it.iteration_time, it.cumulative_time);
+  std::fflush(stdout);
+}
+
+}  // namespace
+
+void arslam_lm::solve(arslam_lm_summary *s) {
+  fail_if(!loaded, ARSLAM_E_STATE, "no problem loaded");
+  const arslam_lm_options &o = opt;
+  const double t_start = now_s();
+  std::memset(s, 0, sizeof(*s));
+  for (auto &t : timers) t.acc_ms = 0.0;
+  s->n_obs = nb;
+  s->n_reduced = has_f ? (int)nF : 0;
+  x = d_xa.p;
+  xc = d_xb.p;
+  HIP_CHECK(hipMemcpyAsync(x, d_x0.p, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(d_xbest.p, d_x0.p, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
+  const bool root = rank == 0;
+  if (o.minimizer_progress_to_stdout && root) print_header();
+
+  // ---- iteration 0 ----
+  double x_cost, fixed_cost, gmax, gnorm, x_norm;
+  linearize(&x_cost, &fixed_cost, &gmax, &gnorm, &x_norm);
+  s->fixed_cost = fixed_cost;
+  s->initial_cost = x_cost + fixed_cost;
+  s->final_cost = s->initial_cost;
+  if (!std::isfinite(x_cost)) {
+    s->termination = ARSLAM_FAILURE;
+    s->rule = ARSLAM_RULE_EVAL_FAILED;
+    s->total_time_s = now_s() - t_start;
+    return;
+  }
+  arslam::launch_scale(P, d_colnorm.p, o.jacobi_scaling, d_scale.p, stream);
+
+  double radius = o.initial_trust_region_radius, decrease_factor = 2.0;
+  bool reuse_diag = false;
+  int n_invalid = 0;
+  double minimum_cost = x_cost;
+  arslam_lm_iteration it{};
+  it.iteration = 0;
+  it.cost = x_cost + fixed_cost;
+  it.gradient_max_norm = gmax;
+  it.gradient_norm = gnorm;
+  it.step_is_valid = 1;
+  it.step_is_successful = 1;
+  double t_iter = t_start;
+
+  for (;;) {
+    // ---- FinalizeIterationAndCheckIfMinimizerCanContinue ----
+    if (it.step_is_successful) {
+      if (it.iteration > 0) s->num_successful_steps++;
+      if (x_cost < minimum_cost || it.iteration == 0) {
+        minimum_cost = x_cost;
+        HIP_CHECK(hipMemcpyAsync(d_xbest.p, x, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
+        if (o.update_state_every_iteration) write_back(d_xbest.p);
+      }
+    } else {
+      s->num_unsuccessful_steps++;
+    }
+    it.trust_region_radius = radius;
+    const double tn = now_s();
+    it.iteration_time = tn - t_iter;
+    it.cumulative_time = tn - t_start;
+    t_iter = tn;
+    if (s->n_iters <= ARSLAM_LM_MAX_ITERS) s->iters[s->n_iters++] = it;
+    if (o.minimizer_progress_to_stdout && root) print_row(it);
+    if (it.iteration >= o.max_num_iterations) {
+      s->termination = ARSLAM_NO_CONVERGENCE; s->rule = ARSLAM_RULE_MAX_ITERS; break;
+    }
+    if (it.step_is_successful && it.gradient_max_norm <= o.gradient_tolerance) {
+      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_GRADIENT; break;
+    }
+    if (radius <= o.min_trust_region_radius) {
+      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_MIN_RADIUS; break;
+    }
+    const double prev_gmax = it.gradient_max_norm, prev_gnorm = it.gradient_norm;
+    const int next_iter = it.iteration + 1;
+    it = arslam_lm_iteration{};
+    it.iteration = next_iter;
+
+    // ---- ComputeTrustRegionStep: LM diagonal, DENSE_SCHUR solve ----
+    s->num_linear_solves++;
+    if (!reuse_diag)
+      arslam::launch_lm_diag(P, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal, d_diag.p, stream);
+    reuse_diag = true;
+    HIP_CHECK(hipMemsetAsync(d_flag.p, 0, sizeof(int), stream));
+    if (has_f) {
+      timers[PH_SCHUR].start(stream);
+      arslam::launch_zero_lower(d_S.p, N, N, nullptr, stream);
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream);
+      if (nranks > 1) allreduce(d_S.p, (size_t)N * N, ncclSum);
+      arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
+      timers[PH_SCHUR].stop(stream);
+      timers[PH_CHOL].start(stream);
+      arslam::launch_dense_llt(d_S.p, N, N, d_flag.p, nullptr, stream);
+      timers[PH_CHOL].stop(stream);
+      timers[PH_SOLVE].start(stream);
+      arslam::launch_dense_back_solve(d_S.p, N, N, nF, d_z.p, d_yF.p, d_flag.p, nullptr, stream);
+      timers[PH_SOLVE].stop(stream);
+    }
+    timers[PH_BACK].start(stream);
+    arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream);
+    arslam::launch_update_f(P, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
+    timers[PH_BACK].stop(stream);
+    timers[PH_COST].start(stream);
+    arslam::launch_cost(P, xc, d_parts.p, stream);
+    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream);
+    if (nranks > 1) {
+      // model change, capture step^2, candidate cost, fixed; flags by max
+      allreduce(d_red.p + arslam::P_COST, 2, ncclSum);
+      allreduce(d_red.p + arslam::P_MODEL, 2, ncclSum);
+      allreduce(d_red.p + arslam::P_YBAD, 2, ncclMax);
+    }
+    timers[PH_COST].stop(stream);
+    double red[16];
+    int flag = 0;
+    HIP_CHECK(hipMemcpyAsync(red, d_red.p, (arslam::NPART + 2) * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipMemcpyAsync(&flag, d_flag.p, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    for (int ph = PH_SCHUR; ph < PH_N; ++ph) timers[ph].collect();
+
+    const bool lin_fail = flag != 0;
+    const bool ybad = red[arslam::P_YBAD] != 0.0 || red[arslam::NPART + 1] != 0.0;
+    const double model_cost_change = red[arslam::P_MODEL];
+    const bool valid = !lin_fail && !ybad && model_cost_change > 0.0;
+    if (!valid) {
+      ++n_invalid;
+      if (n_invalid > o.max_num_consecutive_invalid_steps) {
+        s->termination = ARSLAM_FAILURE; s->rule = ARSLAM_RULE_INVALID_STEPS; break;
+      }
+      radius = radius / decrease_factor;   // StepIsInvalid
+      decrease_factor *= 2.0;
+      reuse_diag = true;
+      it.cost = x_cost + fixed_cost;
+      it.gradient_max_norm = prev_gmax;
+      it.gradient_norm = prev_gnorm;
+      it.step_is_valid = 0;
+      it.step_is_successful = 0;
+      continue;
+    }
+    n_invalid = 0;
+    it.step_is_valid = 1;
+    double candidate_cost = red[arslam::P_COST];
+    if (!std::isfinite(candidate_cost) || red[arslam::P_CBAD] != 0.0) candidate_cost = DBL_MAX;
+    it.step_norm = std::sqrt(red[arslam::P_STEP2] + red[arslam::NPART]);
+    // ---- ParameterToleranceReached ----
+    if (it.step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) {
+      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_PARAMETER; break;
+    }
+    // ---- FunctionToleranceReached ----
+    it.cost_change = x_cost - candidate_cost;
+    if (std::fabs(it.cost_change) <= o.function_tolerance * x_cost) {
+      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_FUNCTION; break;
+    }
+    // ---- IsStepSuccessful ----
+    it.relative_decrease = candidate_cost >= DBL_MAX ? -DBL_MAX
+                                                     : (x_cost - candidate_cost) / model_cost_change;
+    if (it.relative_decrease > o.min_relative_decrease) {
+      std::swap(x, xc);
+      double fc;
+      linearize(&x_cost, &fc, &gmax, &gnorm, &x_norm);
+      it.cost = x_cost + fixed_cost;
+      it.gradient_max_norm = gmax;
+      it.gradient_norm = gnorm;
+      it.step_is_successful = 1;
+      const double q = 2.0 * it.relative_decrease - 1.0;
+      radius = radius / std::max(1.0 / 3.0, 1.0 - q * q * q);
+      radius = std::min(o.max_trust_region_radius, radius);
+      decrease_factor = 2.0;
+      reuse_diag = false;
+    } else {
+      it.step_is_successful = 0;
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+      reuse_diag = true;
+      it.cost = candidate_cost + fixed_cost;
+      it.gradient_max_norm = prev_gmax;
+      it.gradient_norm = prev_gnorm;
+    }
+  }
+  s->final_cost = minimum_cost + fixed_cost;
+  s->minimizer_time_s = now_s() - t_start;
+  write_back(d_xbest.p);
+  s->total_time_s = now_s() - t_start;
+  long nb_all = nb;
+  if (nranks > 1) {
+    double v = nb;
+    DevBuf<double> tmp;
+    tmp.alloc(1);
+    tmp.upload(&v, 1, stream);
+    allreduce(tmp.p, 1, ncclSum);
+    HIP_CHECK(hipMemcpyAsync(&v, tmp.p, sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    nb_all = (long)v;
+  }
+  s->n_obs = (int)nb_all;
+  s->final_rms_px = nb_all ? std::sqrt(2.0 * s->final_cost / (4.0 * nb_all)) : 0.0;
+  s->t_linearize_ms = timers[PH_LIN].acc_ms;
+  s->t_schur_ms = timers[PH_SCHUR].acc_ms;
+  s->t_cholesky_ms = timers[PH_CHOL].acc_ms;
+  s->t_solve_ms = timers[PH_SOLVE].acc_ms;
+  s->t_backsub_ms = timers[PH_BACK].acc_ms;
+  s->t_cost_ms = timers[PH_COST].acc_ms;
+}
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+
+namespace {
+
+template <class F>
+int guarded(F &&f) {
+  try {
+    f();
+    return ARSLAM_OK;
+  } catch (const Error &e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    g_last_error = "host out of memory";
+    return ARSLAM_E_OUT_OF_MEMORY;
+  } catch (const std::exception &e) {
+    g_last_error = e.what();
+    return ARSLAM_E_HIP;
+  } catch (...) {
+    g_last_error = "unknown error";
+    return ARSLAM_E_HIP;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int arslam_lm_options_init(arslam_lm_options *o) {
+  if (!o) return ARSLAM_E_INVALID_ARG;
+  std::memset(o, 0, sizeof(*o));
+  o->max_num_iterations = 50;              // ar_slam_util.cpp:1004
+  o->function_tolerance = 1e-6;            // Ceres 2.0 defaults below
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_relative_decrease = 1e-3;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->jacobi_scaling = 1;
+  o->elimination = ARSLAM_ELIM_AUTO;       // DENSE_SCHUR, ar_slam_util.cpp:1011
+  o->minimizer_progress_to_stdout = 0;
+  o->update_state_every_iteration = 0;
+  o->device = -1;
+  o->cholesky_skip_zero_tiles = 0;
+  return ARSLAM_OK;
+}
+
+int arslam_lm_create(arslam_lm **out, const arslam_lm_options *opt) {
+  if (!out) return ARSLAM_E_INVALID_ARG;
+  *out = nullptr;
+  return guarded([&] {
+    auto *h = new arslam_lm();
+    if (opt) h->opt = *opt; else arslam_lm_options_init(&h->opt);
+    if (h->opt.elimination != ARSLAM_ELIM_AUTO && h->opt.elimination != ARSLAM_ELIM_CAPTURES) {
+      delete h;
+      throw Error(ARSLAM_E_UNSUPPORTED, "only capture elimination is implemented");
+    }
+    *out = h;
+  });
+}
+
+void arslam_lm_destroy(arslam_lm *h) { delete h; }
+
+int arslam_lm_add_residual_block(arslam_lm *h, const double corners[8], double *camera,
+                                 double *capture, double *tag) {
+  if (!h || !corners || !camera || !capture || !tag) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    fail_if(h->camera_ptr && h->camera_ptr != camera, ARSLAM_E_UNSUPPORTED,
+            "one shared camera block per problem (ArSlamSolver::camera_)");
+    fail_if(capture == camera || tag == camera || capture == tag, ARSLAM_E_INVALID_ARG,
+            "parameter blocks must be distinct");
+    fail_if(h->tag_of.count(capture) || h->cap_of.count(tag), ARSLAM_E_INVALID_ARG,
+            "a block cannot be both a capture and a tag");
+    h->camera_ptr = camera;
+    auto ci = h->cap_of.find(capture);
+    int c;
+    if (ci == h->cap_of.end()) {
+      c = (int)h->cap_ptrs.size();
+      h->cap_of.emplace(capture, c);
+      h->cap_ptrs.push_back(capture);
+    } else {
+      c = ci->second;
+    }
+    auto ti = h->tag_of.find(tag);
+    int t;
+    if (ti == h->tag_of.end()) {
+      t = (int)h->tag_ptrs.size();
+      h->tag_of.emplace(tag, t);
+      h->tag_ptrs.push_back(tag);
+    } else {
+      t = ti->second;
+    }
+    h->pk_obs_cap.push_back(c);
+    h->pk_obs_tag.push_back(t);
+    h->pk_corners.insert(h->pk_corners.end(), corners, corners + 8);
+  });
+}
+
+int arslam_lm_set_parameter_block_constant(arslam_lm *h, double *block) {
+  if (!h || !block) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    fail_if(block != h->camera_ptr && !h->cap_of.count(block) && !h->tag_of.count(block),
+            ARSLAM_E_INVALID_ARG, "parameter block is not part of the problem");
+    h->constant.insert(block);
+  });
+}
+
+int arslam_lm_set_parameter_block_variable(arslam_lm *h, double *block) {
+  if (!h || !block) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] { h->constant.erase(block); });
+}
+
+int arslam_lm_num_residual_blocks(const arslam_lm *h) {
+  return h ? (int)h->pk_obs_cap.size() : 0;
+}
+
+int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
+  if (!h || !summary) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    std::memset(summary, 0, sizeof(*summary));
+    if (h->pk_obs_cap.empty()) {   // empty problem: nothing to do (Ceres returns immediately)
+      summary->termination = ARSLAM_CONVERGENCE;
+      return;
+    }
+    const int nc = (int)h->cap_ptrs.size(), nt = (int)h->tag_ptrs.size();
+    std::vector<double> cam(h->camera_ptr, h->camera_ptr + 3), cap(6L * nc), tag(6L * nt);
+    std::vector<unsigned char> cc(nc), tc(nt);
+    for (int c = 0; c < nc; ++c) {
+      std::memcpy(&cap[6L * c], h->cap_ptrs[c], 6 * sizeof(double));
+      cc[c] = h->constant.count(h->cap_ptrs[c]) ? 1 : 0;
+    }
+    for (int t = 0; t < nt; ++t) {
+      std::memcpy(&tag[6L * t], h->tag_ptrs[t], 6 * sizeof(double));
+      tc[t] = h->constant.count(h->tag_ptrs[t]) ? 1 : 0;
+    }
+    arslam_soa_problem p{};
+    p.n_cap = nc; p.n_tag = nt; p.n_obs = (int)h->pk_obs_cap.size();
+    p.camera = cam.data(); p.cap = cap.data(); p.tag = tag.data();
+    p.obs_cap = h->pk_obs_cap.data(); p.obs_tag = h->pk_obs_tag.data();
+    p.corners = h->pk_corners.data();
+    p.camera_const = h->constant.count(h->camera_ptr) ? 1 : 0;
+    p.cap_const = cc.data(); p.tag_const = tc.data();
+    h->load(&p);
+    h->solve(summary);
+    // write the final state into the caller's blocks (Ceres writes parameters back)
+    std::memcpy(h->camera_ptr, cam.data(), 3 * sizeof(double));
+    for (int c = 0; c < nc; ++c) std::memcpy(h->cap_ptrs[c], &cap[6L * c], 6 * sizeof(double));
+    for (int t = 0; t < nt; ++t) std::memcpy(h->tag_ptrs[t], &tag[6L * t], 6 * sizeof(double));
+    h->loaded = false;   // the SoA buffers above go out of scope
+  });
+}
+
+int arslam_lm_reset(arslam_lm *h) {
+  if (!h) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    h->camera_ptr = nullptr;
+    h->cap_of.clear(); h->tag_of.clear();
+    h->cap_ptrs.clear(); h->tag_ptrs.clear();
+    h->pk_obs_cap.clear(); h->pk_obs_tag.clear(); h->pk_corners.clear();
+    h->constant.clear();
+    h->loaded = false;
+  });
+}
+
+int arslam_lm_load_soa(arslam_lm *h, const arslam_soa_problem *p) {
+  if (!h || !p) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] { h->load(p); });
+}
+
+int arslam_lm_solve_loaded(arslam_lm *h, arslam_lm_summary *summary) {
+  if (!h || !summary) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] { h->solve(summary); });
+}
+
+int arslam_lm_solve_soa(arslam_soa_problem *p, const arslam_lm_options *opt,
+                        arslam_lm_summary *summary) {
+  if (!p || !summary) return ARSLAM_E_INVALID_ARG;
+  arslam_lm *h = nullptr;
+  int rc = arslam_lm_create(&h, opt);
+  if (rc) return rc;
+  rc = guarded([&] {
+    h->load(p);
+    h->solve(summary);
+  });
+  arslam_lm_destroy(h);
+  return rc;
+}
+
+int arslam_comm_unique_id(unsigned char id[ARSLAM_COMM_ID_BYTES]) {
+  if (!id) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    static_assert(sizeof(ncclUniqueId) <= ARSLAM_COMM_ID_BYTES, "id size");
+    ncclUniqueId u;
+    NCCL_CHECK(ncclGetUniqueId(&u));
+    std::memset(id, 0, ARSLAM_COMM_ID_BYTES);
+    std::memcpy(id, &u, sizeof(u));
+  });
+}
+
+int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks, const unsigned char id[ARSLAM_COMM_ID_BYTES]) {
+  if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    h->ensure_stream();
+    if (h->comm) { (void)ncclCommDestroy(h->comm); h->comm = nullptr; }
+    h->rank = rank;
+    h->nranks = nranks;
+    if (nranks > 1) {
+      ncclUniqueId u;
+      std::memcpy(&u, id, sizeof(u));
+      NCCL_CHECK(ncclCommInitRank(&h->comm, nranks, u, rank));
+    }
+  });
+}
+
+int arslam_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char *arslam_lm_last_error(void) { return g_last_error.c_str(); }
+
+const char *arslam_lm_version(void) { return "arslam_lm 0.1 (gfx950, fp64)"; }
+
+}  // extern "C"

@@ -1,0 +1,333 @@
+"""Python binding of libarslam_lm.so (ctypes over the C-ABI in include/arslam_lm.h).
+
+This is the host-side mirror of the reference's solver interface used by the
+tests, the benchmark and smoke():
+
+* :class:`Problem` mirrors ``ceres::Problem`` as ArSlamSolver drives it --
+  ``add_residual_block(corners, camera, capture, tag)`` is
+  ``AddResidualBlock(AutoDiff<ArucoReprojectionError,8,3,6,6>, nullptr,
+  camera, capture, aruco)`` (ar_slam_util.cpp:720-727),
+  ``set_parameter_block_constant`` is ``SetParameterBlockConstant``
+  (:965, :972) and ``solve`` is ``ceres::Solve`` (:1015); parameter blocks
+  are caller-owned float64 numpy arrays updated in place.
+* :func:`solve_soa` / :class:`ResidentProblem` are the bulk struct-of-arrays
+  path (problem uploaded once to HBM, solved many times).
+
+There is no CPU fallback: if the HIP library is missing or no GPU is
+present, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libarslam_lm.so")
+MAX_ITERS = 1024
+COMM_ID_BYTES = 128
+
+TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE"}
+RULES = {0: "none", 1: "gradient_tolerance", 2: "parameter_tolerance", 3: "function_tolerance",
+         4: "min_trust_region_radius", 5: "max_num_iterations", 6: "invalid_steps",
+         7: "evaluation_failed"}
+ERRORS = {-1: "INVALID_ARG", -2: "UNSUPPORTED", -3: "NO_DEVICE", -4: "HIP", -5: "OUT_OF_MEMORY",
+          -6: "COMM", -7: "STATE"}
+
+# Every symbol include/arslam_lm.h declares (checked by the CPU tests).
+EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
+           "arslam_lm_add_residual_block", "arslam_lm_set_parameter_block_constant",
+           "arslam_lm_set_parameter_block_variable", "arslam_lm_solve", "arslam_lm_reset",
+           "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
+           "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm",
+           "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
+           "arslam_debug_residual_jacobian", "arslam_debug_dense_llt"]
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+_up = C.POINTER(C.c_ubyte)
+
+
+class LMError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"arslam_lm error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Options(C.Structure):
+    _fields_ = [("max_num_iterations", C.c_int),
+                ("function_tolerance", C.c_double), ("gradient_tolerance", C.c_double),
+                ("parameter_tolerance", C.c_double),
+                ("initial_trust_region_radius", C.c_double),
+                ("max_trust_region_radius", C.c_double),
+                ("min_trust_region_radius", C.c_double),
+                ("min_relative_decrease", C.c_double),
+                ("min_lm_diagonal", C.c_double), ("max_lm_diagonal", C.c_double),
+                ("max_num_consecutive_invalid_steps", C.c_int),
+                ("jacobi_scaling", C.c_int), ("elimination", C.c_int),
+                ("minimizer_progress_to_stdout", C.c_int),
+                ("update_state_every_iteration", C.c_int),
+                ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int)]
+
+
+class Iteration(C.Structure):
+    _fields_ = [("iteration", C.c_int),
+                ("cost", C.c_double), ("cost_change", C.c_double),
+                ("gradient_max_norm", C.c_double), ("gradient_norm", C.c_double),
+                ("step_norm", C.c_double), ("relative_decrease", C.c_double),
+                ("trust_region_radius", C.c_double),
+                ("step_is_valid", C.c_int), ("step_is_successful", C.c_int),
+                ("iteration_time", C.c_double), ("cumulative_time", C.c_double)]
+
+
+class Summary(C.Structure):
+    _fields_ = [("termination", C.c_int), ("rule", C.c_int),
+                ("num_successful_steps", C.c_int), ("num_unsuccessful_steps", C.c_int),
+                ("num_linear_solves", C.c_int),
+                ("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("fixed_cost", C.c_double), ("final_rms_px", C.c_double),
+                ("n_obs", C.c_int), ("n_reduced", C.c_int),
+                ("setup_time_s", C.c_double), ("minimizer_time_s", C.c_double),
+                ("total_time_s", C.c_double),
+                ("t_linearize_ms", C.c_double), ("t_schur_ms", C.c_double),
+                ("t_cholesky_ms", C.c_double), ("t_solve_ms", C.c_double),
+                ("t_backsub_ms", C.c_double), ("t_cost_ms", C.c_double),
+                ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
+
+    def to_dict(self):
+        its = [{f: getattr(self.iters[i], f) for f, _ in Iteration._fields_}
+               for i in range(self.n_iters)]
+        d = {f: getattr(self, f) for f, _ in Summary._fields_ if f not in ("iters", "termination", "rule")}
+        d["termination"] = TERMINATION[self.termination]
+        d["rule"] = RULES[self.rule]
+        d["iterations"] = its
+        return d
+
+
+class SoaProblem(C.Structure):
+    _fields_ = [("n_cap", C.c_int), ("n_tag", C.c_int), ("n_obs", C.c_int),
+                ("camera", _dp), ("cap", _dp), ("tag", _dp),
+                ("obs_cap", _ip), ("obs_tag", _ip), ("corners", _dp),
+                ("camera_const", C.c_int), ("cap_const", _up), ("tag_const", _up)]
+
+
+_lib = None
+
+
+def library_path():
+    return LIB_PATH
+
+
+def lib():
+    """Load the HIP library (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -m ar_slam_amd.build` "
+                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    L.arslam_lm_options_init.argtypes = [C.POINTER(Options)]
+    L.arslam_lm_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
+    L.arslam_lm_destroy.argtypes = [C.c_void_p]
+    L.arslam_lm_destroy.restype = None
+    L.arslam_lm_add_residual_block.argtypes = [C.c_void_p, _dp, _dp, _dp, _dp]
+    L.arslam_lm_set_parameter_block_constant.argtypes = [C.c_void_p, _dp]
+    L.arslam_lm_set_parameter_block_variable.argtypes = [C.c_void_p, _dp]
+    L.arslam_lm_solve.argtypes = [C.c_void_p, C.POINTER(Summary)]
+    L.arslam_lm_reset.argtypes = [C.c_void_p]
+    L.arslam_lm_num_residual_blocks.argtypes = [C.c_void_p]
+    L.arslam_lm_load_soa.argtypes = [C.c_void_p, C.POINTER(SoaProblem)]
+    L.arslam_lm_solve_loaded.argtypes = [C.c_void_p, C.POINTER(Summary)]
+    L.arslam_lm_solve_soa.argtypes = [C.POINTER(SoaProblem), C.POINTER(Options), C.POINTER(Summary)]
+    L.arslam_comm_unique_id.argtypes = [C.c_char_p]
+    L.arslam_lm_set_comm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+    L.arslam_device_count.argtypes = []
+    L.arslam_lm_last_error.restype = C.c_char_p
+    L.arslam_lm_version.restype = C.c_char_p
+    L.arslam_debug_residual_jacobian.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp, _dp]
+    L.arslam_debug_dense_llt.argtypes = [C.c_long, _dp, _dp, _dp, C.POINTER(C.c_int)]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise LMError(rc, lib().arslam_lm_last_error().decode(errors="replace"))
+
+
+def device_count():
+    return lib().arslam_device_count()
+
+
+def make_options(**kw):
+    o = Options()
+    lib().arslam_lm_options_init(C.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise AttributeError(f"unknown solver option {k}")
+        setattr(o, k, v)
+    return o
+
+
+def _f64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a if shape is None else a.reshape(shape)
+
+
+class _Soa:
+    def __init__(self, camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False,
+                 cap_const=None, tag_const=None):
+        self.camera = _f64(camera).copy()
+        self.cap = _f64(cap, (-1, 6)).copy()
+        self.tag = _f64(tag, (-1, 6)).copy()
+        self.obs_cap = np.ascontiguousarray(obs_cap, np.int32)
+        self.obs_tag = np.ascontiguousarray(obs_tag, np.int32)
+        self.corners = _f64(corners, (-1, 8))
+        self.cap_const = None if cap_const is None else np.ascontiguousarray(cap_const, np.uint8)
+        self.tag_const = None if tag_const is None else np.ascontiguousarray(tag_const, np.uint8)
+        self.s = SoaProblem(self.cap.shape[0], self.tag.shape[0], self.obs_cap.shape[0],
+                            self.camera.ctypes.data_as(_dp), self.cap.ctypes.data_as(_dp),
+                            self.tag.ctypes.data_as(_dp), self.obs_cap.ctypes.data_as(_ip),
+                            self.obs_tag.ctypes.data_as(_ip), self.corners.ctypes.data_as(_dp),
+                            int(bool(camera_const)),
+                            None if self.cap_const is None else self.cap_const.ctypes.data_as(_up),
+                            None if self.tag_const is None else self.tag_const.ctypes.data_as(_up))
+
+
+def solve_soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, cap_const=None,
+              tag_const=None, **opts):
+    """One-shot bulk solve.  Returns (camera, cap, tag, summary dict)."""
+    A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const, cap_const, tag_const)
+    s = Summary()
+    _check(lib().arslam_lm_solve_soa(C.byref(A.s), C.byref(make_options(**opts)), C.byref(s)))
+    return A.camera, A.cap, A.tag, s.to_dict()
+
+
+def solve_graph(g, **opts):
+    return solve_soa(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, **opts)
+
+
+class _Handle:
+    def __init__(self, **opts):
+        self._h = C.c_void_p()
+        _check(lib().arslam_lm_create(C.byref(self._h), C.byref(make_options(**opts))))
+
+    def close(self):
+        if self._h:
+            lib().arslam_lm_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_comm(self, rank, nranks, uid: bytes):
+        _check(lib().arslam_lm_set_comm(self._h, rank, nranks, uid))
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().arslam_comm_unique_id(buf))
+    return buf.raw
+
+
+class ResidentProblem(_Handle):
+    """SoA problem uploaded once to HBM; ``solve()`` restarts from the loaded state."""
+
+    def __init__(self, camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False,
+                 cap_const=None, tag_const=None, comm=None, **opts):
+        super().__init__(**opts)
+        if comm is not None:
+            self.set_comm(*comm)
+        self.A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const, cap_const, tag_const)
+        _check(lib().arslam_lm_load_soa(self._h, C.byref(self.A.s)))
+
+    def solve(self):
+        s = Summary()
+        _check(lib().arslam_lm_solve_loaded(self._h, C.byref(s)))
+        return s.to_dict()
+
+    @property
+    def camera(self):
+        return self.A.camera
+
+    @property
+    def cap(self):
+        return self.A.cap
+
+    @property
+    def tag(self):
+        return self.A.tag
+
+
+class Problem(_Handle):
+    """ceres::Problem mirror with pointer-keyed parameter blocks (numpy arrays)."""
+
+    def __init__(self, **opts):
+        super().__init__(**opts)
+        self._keep = []
+
+    @staticmethod
+    def _block(a, n):
+        if not (isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous
+                and a.size == n):
+            raise TypeError(f"parameter block must be a C-contiguous float64 array of size {n}")
+        return a.ctypes.data_as(_dp)
+
+    def add_residual_block(self, corners, camera, capture, tag):
+        c = _f64(corners).reshape(8)
+        self._keep += [camera, capture, tag]
+        _check(lib().arslam_lm_add_residual_block(self._h, c.ctypes.data_as(_dp),
+                                                  self._block(camera, 3), self._block(capture, 6),
+                                                  self._block(tag, 6)))
+
+    def set_parameter_block_constant(self, block):
+        _check(lib().arslam_lm_set_parameter_block_constant(self._h, block.ctypes.data_as(_dp)))
+
+    def set_parameter_block_variable(self, block):
+        _check(lib().arslam_lm_set_parameter_block_variable(self._h, block.ctypes.data_as(_dp)))
+
+    def num_residual_blocks(self):
+        return lib().arslam_lm_num_residual_blocks(self._h)
+
+    def solve(self):
+        s = Summary()
+        _check(lib().arslam_lm_solve(self._h, C.byref(s)))
+        return s.to_dict()
+
+    def reset(self):
+        _check(lib().arslam_lm_reset(self._h))
+        self._keep = []
+
+
+# ---- component entry points (include/arslam_lm_debug.h) ----
+
+def debug_residual_jacobian(cam, cap, tag, corners):
+    """Device residuals (n,8) and Jacobians (n,8,15) of n independent observations."""
+    cap = _f64(cap, (-1, 6))
+    n = cap.shape[0]
+    cam = _f64(np.broadcast_to(np.asarray(cam, np.float64), (n, 3)))
+    tag = _f64(tag, (-1, 6))
+    corners = _f64(corners, (-1, 8))
+    r = np.zeros((n, 8))
+    J = np.zeros((n, 8, 15))
+    _check(lib().arslam_debug_residual_jacobian(n, cam.ctypes.data_as(_dp), cap.ctypes.data_as(_dp),
+                                                tag.ctypes.data_as(_dp), corners.ctypes.data_as(_dp),
+                                                r.ctypes.data_as(_dp), J.ctypes.data_as(_dp)))
+    return r, J
+
+
+def debug_dense_llt(A, b):
+    """Device Cholesky + solve of the SPD matrix A (lower triangle used). Returns (L, y, info)."""
+    A = _f64(A).copy()
+    n = A.shape[0]
+    b = _f64(b).reshape(n)
+    y = np.zeros(n)
+    info = C.c_int(0)
+    _check(lib().arslam_debug_dense_llt(n, A.ctypes.data_as(_dp), b.ctypes.data_as(_dp),
+                                        y.ctypes.data_as(_dp), C.byref(info)))
+    return A, y, info.value

@@ -1,0 +1,181 @@
+/*
+ * arslam_lm.h -- C-ABI of the MI355X-native Levenberg-Marquardt bundle
+ * adjuster that replaces ar_slam's ceres::Solve call.
+ *
+ * Drop-in boundary.  The reference builds a ceres::Problem
+ * and hands it to ceres::Solve:
+ *
+ *   AddResidualBlock(AutoDiff<ArucoReprojectionError,8,3,6,6>, nullptr,
+ *                    camera, capture.inv_pose, aruco.pose)
+ *        ar_slam_util.cpp:720-727, 829-836, 956-963
+ *   SetParameterBlockConstant(block)       ar_slam_util.cpp:965, 972
+ *   ceres::Solve(options, &problem_, &s)   ar_slam_util.cpp:1001-1018
+ *   resetProblem()                         ar_slam_util.cpp:1021-1025
+ *
+ * Each entry point below replaces one of those calls with the same argument
+ * meaning: parameter blocks are caller-owned double arrays keyed by their
+ * address (camera[3] = f,l1,l2; capture[6] = inv_pose t,w; tag[6] = pose
+ * t,w), observations are copied (as the functor copies its ArucoRect,
+ * ar_slam_util.cpp:194-196), and results are written back into the caller's
+ * arrays when the solve ends (Ceres' default; update_state_every_iteration
+ * writes them after every improving step).
+ *
+ * Conventions: every function returns 0 (ARSLAM_OK) or a negative
+ * ARSLAM_E_* code; no C++ exception crosses the ABI; a handle is not
+ * thread-safe.  arslam_lm_last_error() returns the message of the most
+ * recent failure on the calling thread.
+ */
+#ifndef ARSLAM_LM_H
+#define ARSLAM_LM_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ARSLAM_LM_MAX_ITERS 1024
+#define ARSLAM_COMM_ID_BYTES 128
+
+enum {
+  ARSLAM_OK = 0,
+  ARSLAM_E_INVALID_ARG = -1,
+  ARSLAM_E_UNSUPPORTED = -2,
+  ARSLAM_E_NO_DEVICE = -3,
+  ARSLAM_E_HIP = -4,
+  ARSLAM_E_OUT_OF_MEMORY = -5,
+  ARSLAM_E_COMM = -6,
+  ARSLAM_E_STATE = -7
+};
+
+/* which side of the camera/tag graph the Schur complement eliminates */
+enum { ARSLAM_ELIM_AUTO = 0, ARSLAM_ELIM_CAPTURES = 1 };
+
+/* Ceres termination types (ceres::TerminationType) */
+enum { ARSLAM_CONVERGENCE = 0, ARSLAM_NO_CONVERGENCE = 1, ARSLAM_FAILURE = 2 };
+
+/* which termination test fired */
+enum {
+  ARSLAM_RULE_NONE = 0, ARSLAM_RULE_GRADIENT = 1, ARSLAM_RULE_PARAMETER = 2,
+  ARSLAM_RULE_FUNCTION = 3, ARSLAM_RULE_MIN_RADIUS = 4, ARSLAM_RULE_MAX_ITERS = 5,
+  ARSLAM_RULE_INVALID_STEPS = 6, ARSLAM_RULE_EVAL_FAILED = 7
+};
+
+/* ceres::Solver::Options subset used by ArSlamSolver::optimize
+ * (ar_slam_util.cpp:1003-1012); defaults from arslam_lm_options_init are
+ * the reference's values (max_num_iterations = 50, DENSE_SCHUR) plus Ceres
+ * 2.0 defaults for everything it leaves unset. */
+typedef struct {
+  int max_num_iterations;
+  double function_tolerance;
+  double gradient_tolerance;
+  double parameter_tolerance;
+  double initial_trust_region_radius;
+  double max_trust_region_radius;
+  double min_trust_region_radius;
+  double min_relative_decrease;
+  double min_lm_diagonal;
+  double max_lm_diagonal;
+  int max_num_consecutive_invalid_steps;
+  int jacobi_scaling;
+  int elimination;                   /* ARSLAM_ELIM_* */
+  int minimizer_progress_to_stdout;  /* Ceres progress table */
+  int update_state_every_iteration;  /* write improving iterates back */
+  int device;                        /* HIP device ordinal, -1 = current */
+  int cholesky_skip_zero_tiles;      /* 1: skip structurally-zero tiles of the reduced system */
+} arslam_lm_options;
+
+/* ceres::IterationSummary subset */
+typedef struct {
+  int iteration;
+  double cost, cost_change, gradient_max_norm, gradient_norm, step_norm;
+  double relative_decrease, trust_region_radius;
+  int step_is_valid, step_is_successful;
+  double iteration_time, cumulative_time;
+} arslam_lm_iteration;
+
+/* ceres::Solver::Summary subset plus per-phase device timings */
+typedef struct {
+  int termination;              /* ARSLAM_CONVERGENCE ... */
+  int rule;                     /* ARSLAM_RULE_* */
+  int num_successful_steps, num_unsuccessful_steps;
+  int num_linear_solves;        /* trust-region step computations = LM iterations of the metric */
+  double initial_cost, final_cost, fixed_cost;
+  double final_rms_px;          /* sqrt(2 final_cost / (4 n_obs)) */
+  int n_obs, n_reduced;         /* residual blocks; size of the reduced (tag+camera) system */
+  double setup_time_s;          /* host assembly + upload */
+  double minimizer_time_s;      /* first evaluation to termination */
+  double total_time_s;
+  /* accumulated device time per phase (ms), from HIP events */
+  double t_linearize_ms, t_schur_ms, t_cholesky_ms, t_solve_ms, t_backsub_ms, t_cost_ms;
+  int n_iters;                  /* entries in iters[], iteration 0 included */
+  arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
+} arslam_lm_summary;
+
+/* Whole problem in struct-of-arrays form (bulk / benchmark path). */
+typedef struct {
+  int n_cap, n_tag, n_obs;
+  double *camera;                  /* [3], updated in place */
+  double *cap;                     /* [n_cap*6], updated in place */
+  double *tag;                     /* [n_tag*6], updated in place */
+  const int *obs_cap;              /* [n_obs] */
+  const int *obs_tag;              /* [n_obs] */
+  const double *corners;           /* [n_obs*8] centred pixels x0,y0..x3,y3 */
+  int camera_const;
+  const unsigned char *cap_const;  /* [n_cap] or NULL */
+  const unsigned char *tag_const;  /* [n_tag] or NULL */
+} arslam_soa_problem;
+
+typedef struct arslam_lm arslam_lm;
+
+/* Fill *opt with the reference's solver options. */
+int arslam_lm_options_init(arslam_lm_options *opt);
+
+/* new ceres::Problem (ArSlamSolver::problem_, ar_slam_util.hpp:473) */
+int arslam_lm_create(arslam_lm **out, const arslam_lm_options *opt);
+void arslam_lm_destroy(arslam_lm *h);
+
+/* problem_.AddResidualBlock(new AutoDiffCostFunction<ArucoReprojectionError,
+ * 8,3,6,6>(new ArucoReprojectionError(rect)), nullptr, camera, capture, tag)
+ * -- ar_slam_util.cpp:720-727.  corners = ArucoRect x0,y0,..,x3,y3. */
+int arslam_lm_add_residual_block(arslam_lm *h, const double corners[8], double *camera,
+                                 double *capture, double *tag);
+
+/* problem_.SetParameterBlockConstant(block) -- ar_slam_util.cpp:965, 972 */
+int arslam_lm_set_parameter_block_constant(arslam_lm *h, double *block);
+int arslam_lm_set_parameter_block_variable(arslam_lm *h, double *block);
+
+/* ceres::Solve(options, &problem_, &summary) -- ar_slam_util.cpp:1015 */
+int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary);
+
+/* ArSlamSolver::resetProblem -- ar_slam_util.cpp:1021-1025 */
+int arslam_lm_reset(arslam_lm *h);
+
+int arslam_lm_num_residual_blocks(const arslam_lm *h);
+
+/* Bulk path: load an SoA problem into device memory once (HBM-resident), then
+ * solve it any number of times from the loaded initial state; results are
+ * written to the SoA arrays given at load time. */
+int arslam_lm_load_soa(arslam_lm *h, const arslam_soa_problem *p);
+int arslam_lm_solve_loaded(arslam_lm *h, arslam_lm_summary *summary);
+
+/* One-shot bulk solve. */
+int arslam_lm_solve_soa(arslam_soa_problem *p, const arslam_lm_options *opt,
+                        arslam_lm_summary *summary);
+
+/* Multi-GPU (capture-sharded, one process per GPU): each rank loads the
+ * observations of its capture shard plus every tag; the reduced tag+camera
+ * system is all-reduced over RCCL every step. */
+int arslam_comm_unique_id(unsigned char id[ARSLAM_COMM_ID_BYTES]);
+int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks,
+                       const unsigned char id[ARSLAM_COMM_ID_BYTES]);
+
+/* Diagnostics */
+int arslam_device_count(void);
+const char *arslam_lm_last_error(void);
+const char *arslam_lm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ARSLAM_LM_H */

@@ -1,0 +1,158 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Tolerances (fp64 everywhere; the oracle restates Ceres' arithmetic, the
+device sums in a different order and scatters the reduced system with
+atomics, so agreement is to rounding, not bitwise):
+  * residual / Jacobian rows: 1e-12 relative to the row scale;
+  * dense Cholesky solve: 1e-10 relative residual on SPD test matrices;
+  * LM traces: per-iteration cost 1e-9 relative for the first 5 iterations,
+    final cost 1e-8 relative, same termination type and rule, iteration
+    count +-1, focal 1e-8 relative, gauge-aligned tag positions 1e-6 m
+    (SURVEY.md §8c proposal).
+"""
+import numpy as np
+import pytest
+
+from ar_slam_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_obs(rng, n):
+    cam = np.stack([rng.uniform(500, 3000, n), np.zeros(n), np.zeros(n)], 1)
+    tag = np.concatenate([rng.normal(0, 1, (n, 3)), rng.normal(0, 1, (n, 3))], 1)
+    w = rng.normal(0, 1, (n, 3)) * rng.choice([1.0, 1e-2, 0.0, 3.0], (n, 1))
+    cap = np.concatenate([-tag[:, :3] + rng.normal(0, 0.2, (n, 3)) + [0, 0, 1.0], w], 1)
+    tag[::5, 3:] = 0.0          # small-angle branch exactly at w = 0
+    corners = rng.normal(0, 100, (n, 8))
+    return cam, cap, tag, corners
+
+
+def test_residual_jacobian_matches_oracle(lm, oracle):
+    rng = np.random.default_rng(7)
+    cam, cap, tag, corners = _random_obs(rng, 512)
+    r, J = lm.debug_residual_jacobian(cam, cap, tag, corners)
+    for i in range(cam.shape[0]):
+        ro, Jo = oracle.residual_jacobian(cam[i], cap[i], tag[i], corners[i])
+        np.testing.assert_allclose(r[i], ro, rtol=1e-12, atol=1e-9)
+        scale = np.abs(Jo).max(axis=1, keepdims=True) + 1e-300
+        assert np.max(np.abs(J[i] - Jo) / scale) < 1e-12
+
+
+@pytest.mark.parametrize("n", [5, 64, 200, 777])
+def test_dense_llt_matches_numpy(lm, n):
+    rng = np.random.default_rng(n)
+    B = rng.normal(size=(n, n))
+    A = B @ B.T + n * np.eye(n)
+    b = rng.normal(size=n)
+    L, y, info = lm.debug_dense_llt(A, b)
+    assert info == 0
+    Lref = np.linalg.cholesky(A)
+    np.testing.assert_allclose(L, Lref, rtol=1e-10, atol=1e-10 * np.abs(Lref).max())
+    np.testing.assert_allclose(A @ y, b, rtol=1e-9, atol=1e-9 * np.abs(b).max())
+
+
+def test_dense_llt_reports_indefinite(lm):
+    A = np.eye(100)
+    A[70, 70] = -1.0
+    _, _, info = lm.debug_dense_llt(A, np.ones(100))
+    assert info == 71
+
+
+def _align_rigid(P, Q):
+    """Rigid (Kabsch) alignment of point sets P -> Q; returns aligned P."""
+    pc, qc = P.mean(0), Q.mean(0)
+    H = (P - pc).T @ (Q - qc)
+    U, _, Vt = np.linalg.svd(H)
+    d = np.sign(np.linalg.det(Vt.T @ U.T))
+    R = Vt.T @ np.diag([1, 1, d]) @ U.T
+    return (R @ (P - pc).T).T + qc
+
+
+def _compare_solves(g, ours, ref, n_cost_iters=5):
+    cam_o, cap_o, tag_o, s_o = ours
+    cam_r, cap_r, tag_r, s_r = ref
+    assert s_o["termination"] == s_r["termination"]
+    assert s_o["rule"] == s_r["rule"]
+    assert abs(len(s_o["iterations"]) - len(s_r["iterations"])) <= 1
+    co = [it["cost"] for it in s_o["iterations"]]
+    cr = [it["cost"] for it in s_r["iterations"]]
+    for a, b in list(zip(co, cr))[:n_cost_iters]:
+        assert abs(a - b) <= 1e-9 * abs(b), (co, cr)
+    assert abs(s_o["final_cost"] - s_r["final_cost"]) <= 1e-8 * s_r["final_cost"]
+    assert abs(cam_o[0] - cam_r[0]) <= 1e-8 * cam_r[0]
+    used = np.unique(g.obs_tag)
+    A = _align_rigid(tag_o[used, :3], tag_r[used, :3])
+    assert np.abs(A - tag_r[used, :3]).max() < 1e-6
+
+
+@pytest.mark.parametrize("name", ["tiny", "small", "medium", "cfg2"])
+def test_lm_solve_matches_oracle(lm, oracle, name):
+    g = synth.config_graph(name)
+    ref = oracle.solve_graph(g)
+    ours = lm.solve_graph(g)
+    _compare_solves(g, ours, ref)
+    assert ours[3]["termination"] == "CONVERGENCE"
+
+
+def test_pointer_api_matches_soa(lm):
+    """Problem (AddResidualBlock / Solve, caller-owned blocks) == bulk SoA path."""
+    g = synth.config_graph("small")
+    camera = g.camera.copy()
+    caps = [g.cap[c].copy() for c in range(g.n_cap)]
+    tags = [g.tag[t].copy() for t in range(g.n_tag)]
+    prob = lm.Problem()
+    for b in range(g.n_obs):
+        prob.add_residual_block(g.corners[b], camera, caps[g.obs_cap[b]], tags[g.obs_tag[b]])
+    assert prob.num_residual_blocks() == g.n_obs
+    s = prob.solve()
+    cam2, cap2, tag2, s2 = lm.solve_graph(g)
+    assert s["termination"] == s2["termination"]
+    assert abs(s["final_cost"] - s2["final_cost"]) <= 1e-10 * s2["final_cost"]
+    np.testing.assert_allclose(camera, cam2, rtol=1e-10)
+    np.testing.assert_allclose(np.stack(caps), cap2, rtol=1e-8, atol=1e-9)
+
+
+def test_localize_constant_map(lm, oracle):
+    """localizeOne: tags and camera constant (ar_slam_util.cpp:965,972), one free capture each."""
+    g = synth.config_graph("medium")
+    tag_const = np.ones(g.n_tag, np.uint8)
+    kw = dict(camera_const=True, tag_const=tag_const)
+    cam_t = g.camera_true.copy()
+    ref = oracle.solve(cam_t, g.cap, g.tag_true, g.obs_cap, g.obs_tag, g.corners, **kw)
+    ours = lm.solve_soa(cam_t, g.cap, g.tag_true, g.obs_cap, g.obs_tag, g.corners, **kw)
+    assert ours[3]["termination"] == ref[3]["termination"]
+    assert abs(ours[3]["final_cost"] - ref[3]["final_cost"]) <= 1e-8 * ref[3]["final_cost"]
+    np.testing.assert_allclose(ours[1], ref[1], rtol=1e-7, atol=1e-8)
+    np.testing.assert_array_equal(ours[2], g.tag_true)   # constant blocks untouched
+    assert ours[0][0] == cam_t[0]
+
+
+def test_edge_cases_match_oracle(lm, oracle):
+    """Unobserved tag, duplicate tag in one capture, a constant capture, empty capture."""
+    g = synth.config_graph("small")
+    obs_cap = np.concatenate([g.obs_cap, [3]]).astype(np.int32)
+    obs_tag = np.concatenate([g.obs_tag, [g.obs_tag[8 * 3]]]).astype(np.int32)   # duplicate
+    corners = np.concatenate([g.corners, g.corners[8 * 3:8 * 3 + 1] + 0.3])
+    tag = np.concatenate([g.tag, [[9.0, 9.0, 0.0, 0.0, 0.0, 0.3]]])            # unobserved
+    cap = np.concatenate([g.cap, [[0.0, 0.0, -1.0, 3.1, 0.0, 0.0]]])            # no observations
+    cap_const = np.zeros(cap.shape[0], np.uint8)
+    cap_const[5] = 1
+    kw = dict(cap_const=cap_const)
+    ref = oracle.solve(g.camera, cap, tag, obs_cap, obs_tag, corners, **kw)
+    ours = lm.solve_soa(g.camera, cap, tag, obs_cap, obs_tag, corners, **kw)
+    assert ours[3]["termination"] == ref[3]["termination"]
+    assert abs(ours[3]["final_cost"] - ref[3]["final_cost"]) <= 1e-8 * ref[3]["final_cost"]
+    np.testing.assert_array_equal(ours[1][5], cap[5])
+    np.testing.assert_array_equal(ours[1][-1], cap[-1])
+    np.testing.assert_array_equal(ours[2][-1], tag[-1])
+
+
+def test_resident_problem_resolves_identically(lm):
+    g = synth.config_graph("medium")
+    rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
+    s1 = rp.solve()
+    c1 = rp.cap.copy()
+    s2 = rp.solve()
+    assert [i["cost"] for i in s1["iterations"]] == pytest.approx([i["cost"] for i in s2["iterations"]], rel=1e-12)
+    np.testing.assert_allclose(rp.cap, c1, rtol=1e-9, atol=1e-12)
