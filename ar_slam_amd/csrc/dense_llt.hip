@@ -220,7 +220,8 @@ void launch_zero_lower(double *S, long N, long lda, const uint8_t *tile_nz, hipS
   hipLaunchKernelGGL(k_zero_tiles, dim3((unsigned)ntiles), dim3(256), 0, s, S, lda, T, tile_nz);
 }
 
-void launch_dense_llt(double *S, long N, long lda, int *flag, const uint8_t *tile_nz, hipStream_t s) {
+void launch_dense_llt(double *S, long N, long lda, int *flag, const uint8_t *tile_nz, hipStream_t s,
+                      LaunchTiming *timing) {
   const int T = (int)(N / T64);
   for (int k = 0; k < T; ++k) {
     hipLaunchKernelGGL(k_potrf, dim3(1), dim3(256), 0, s, S, lda, k, flag);
@@ -228,7 +229,15 @@ void launch_dense_llt(double *S, long N, long lda, int *flag, const uint8_t *til
     if (m == 0) break;
     hipLaunchKernelGGL(k_trsm, dim3(m), dim3(256), 0, s, S, lda, k, T, tile_nz, flag);
     const long nt = (long)m * (m + 1) / 2;
+    const bool rec = timing && timing->used < timing->cap;
+    if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
     hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(256), 0, s, S, lda, k, T, tile_nz, flag);
+    if (rec) {
+      (void)hipEventRecord(timing->ev[2 * timing->used + 1], s);
+      timing->used++;
+      // useful flops: off-diagonal tiles 2*64^3, diagonal tiles (lower incl. diagonal) 64*65*64
+      timing->flops += 2.0 * T64 * T64 * T64 * ((double)m * (m - 1) / 2) + (double)T64 * (T64 + 1) * T64 * m;
+    }
   }
 }
 

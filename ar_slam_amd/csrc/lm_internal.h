@@ -79,12 +79,20 @@ void launch_camera_slots(const DevProblem &P, const double *red, double *g, doub
 void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out,
                        hipStream_t s);
 
+// Optional per-launch event pairs around the dominant kernel (trailing update).
+struct LaunchTiming {
+  hipEvent_t *ev = nullptr;   // 2 * cap events
+  int cap = 0;
+  int used = 0;
+  double flops = 0.0;         // algorithmic flops of the recorded launches
+};
+
 // ---- dense_llt.hip ----
 // Cholesky of the lower triangle of S (N x N, row-major, lda), in place.  Row
 // nF carries the right-hand side, so on exit row nF = (L^{-1} b)^T.  *flag is
 // set non-zero if a pivot is not positive.  Then y = L^{-T} z into yF[0..nF).
 void launch_dense_llt(double *S, long N, long lda, int *flag, const uint8_t *tile_nz,
-                      hipStream_t s);
+                      hipStream_t s, LaunchTiming *timing = nullptr);
 void launch_dense_back_solve(const double *S, long N, long lda, long nF, double *z, double *yF,
                              const int *flag, const uint8_t *tile_nz, hipStream_t s);
 void launch_zero_lower(double *S, long N, long lda, const uint8_t *tile_nz, hipStream_t s);

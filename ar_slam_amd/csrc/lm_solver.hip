@@ -136,6 +136,36 @@ struct arslam_lm {
   int n_fparts = 0;
 
   Timer timers[PH_N];
+  arslam::LaunchTiming upd_timing;
+  std::vector<hipEvent_t> upd_events;
+  double dom_ms = 0.0, dom_flops = 0.0;
+  long dom_launches = 0;
+
+  void timing_begin() {
+    if (!opt.kernel_timing || !has_f) return;
+    const int need = (int)(N / arslam::kTile) + 1;
+    if ((int)upd_events.size() < 2 * need) {
+      for (auto e : upd_events) (void)hipEventDestroy(e);
+      upd_events.assign(2 * need, nullptr);
+      for (auto &e : upd_events) HIP_CHECK(hipEventCreate(&e));
+    }
+    upd_timing.ev = upd_events.data();
+    upd_timing.cap = need;
+    upd_timing.used = 0;
+    upd_timing.flops = 0.0;
+  }
+  void timing_collect() {   // after a stream synchronize
+    if (!opt.kernel_timing || !has_f) return;
+    for (int i = 0; i < upd_timing.used; ++i) {
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, upd_events[2 * i], upd_events[2 * i + 1]));
+      dom_ms += ms;
+    }
+    dom_launches += upd_timing.used;
+    dom_flops += upd_timing.flops;
+    upd_timing.used = 0;
+    upd_timing.flops = 0.0;
+  }
 
   // ---- multi-GPU ----
   int rank = 0, nranks = 1;
@@ -143,6 +173,7 @@ struct arslam_lm {
 
   ~arslam_lm() {
     for (auto &t : timers) t.destroy();
+    for (auto e : upd_events) (void)hipEventDestroy(e);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -390,6 +421,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   const double t_start = now_s();
   std::memset(s, 0, sizeof(*s));
   for (auto &t : timers) t.acc_ms = 0.0;
+  dom_ms = dom_flops = 0.0;
+  dom_launches = 0;
   s->n_obs = nb;
   s->n_reduced = has_f ? (int)nF : 0;
   x = d_xa.p;
@@ -473,7 +506,9 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
-      arslam::launch_dense_llt(d_S.p, N, N, d_flag.p, nullptr, stream);
+      timing_begin();
+      arslam::launch_dense_llt(d_S.p, N, N, d_flag.p, nullptr, stream,
+                               opt.kernel_timing ? &upd_timing : nullptr);
       timers[PH_CHOL].stop(stream);
       timers[PH_SOLVE].start(stream);
       arslam::launch_dense_back_solve(d_S.p, N, N, nF, d_z.p, d_yF.p, d_flag.p, nullptr, stream);
@@ -499,6 +534,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     HIP_CHECK(hipMemcpyAsync(&flag, d_flag.p, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
     for (int ph = PH_SCHUR; ph < PH_N; ++ph) timers[ph].collect();
+    timing_collect();
 
     const bool lin_fail = flag != 0;
     const bool ybad = red[arslam::P_YBAD] != 0.0 || red[arslam::NPART + 1] != 0.0;
@@ -582,6 +618,9 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->t_solve_ms = timers[PH_SOLVE].acc_ms;
   s->t_backsub_ms = timers[PH_BACK].acc_ms;
   s->t_cost_ms = timers[PH_COST].acc_ms;
+  s->t_dominant_ms = dom_ms;
+  s->dominant_flops = dom_flops;
+  s->n_dominant_launches = dom_launches;
 }
 
 // ===========================================================================
@@ -634,6 +673,7 @@ int arslam_lm_options_init(arslam_lm_options *o) {
   o->update_state_every_iteration = 0;
   o->device = -1;
   o->cholesky_skip_zero_tiles = 0;
+  o->kernel_timing = 0;
   return ARSLAM_OK;
 }
 

@@ -68,7 +68,8 @@ class Options(C.Structure):
                 ("jacobi_scaling", C.c_int), ("elimination", C.c_int),
                 ("minimizer_progress_to_stdout", C.c_int),
                 ("update_state_every_iteration", C.c_int),
-                ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int)]
+                ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int),
+                ("kernel_timing", C.c_int)]
 
 
 class Iteration(C.Structure):
@@ -93,6 +94,8 @@ class Summary(C.Structure):
                 ("t_linearize_ms", C.c_double), ("t_schur_ms", C.c_double),
                 ("t_cholesky_ms", C.c_double), ("t_solve_ms", C.c_double),
                 ("t_backsub_ms", C.c_double), ("t_cost_ms", C.c_double),
+                ("t_dominant_ms", C.c_double), ("dominant_flops", C.c_double),
+                ("n_dominant_launches", C.c_long),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 
     def to_dict(self):

@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X LM bundle adjuster on BASELINE.json's headline workload.
+
+Metric (BASELINE.json): "LM iterations/sec + ms-to-converged reproj-RMS,
+10k-capture synthetic graph".  One *step* is one complete ceres::Solve
+equivalent (ar_slam_util.cpp:1001-1018) of cfg3 -- 10,000 captures, 2,000
+tags, k = 8 observations per capture (80,000 residual blocks), seed 2 --
+from the same initial state to the Ceres termination rule.  The problem is
+uploaded to HBM before the timed region; every solve restarts from the
+resident initial state.
+
+  value        = LM iterations (trust-region step computations) of the K
+                 timed solves / wall time of the K solves (max over ranks)
+  ms_per_step  = ms-to-converged of one solve
+
+Multi-GPU (torchrun, one process per GPU): captures are sharded in
+contiguous ranges; every step all-reduces the reduced tag+camera system over
+RCCL (the path has a real exchange step, so total work is fixed: strong
+scaling).
+
+The JSON line also carries the dominant kernel's roofline (the MFMA fp64
+trailing update of the reduced-system Cholesky, timed with HIP events around
+each of its launches inside the timed region) and a CPU baseline: the CPU
+oracle (oracle/, a C port of the same algorithm, NOT Ceres) timed on a
+bounded sample of the same workload on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "LM iterations/sec + ms-to-converged reproj-RMS, 10k-capture synthetic graph"
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X datasheet fp64 matrix (no f64 row in MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def shard_graph(g, rank, world):
+    """Contiguous capture range of this rank; all tags replicated."""
+    lo = (g.n_cap * rank) // world
+    hi = (g.n_cap * (rank + 1)) // world
+    sel = (g.obs_cap >= lo) & (g.obs_cap < hi)
+    return dict(camera=g.camera, cap=g.cap[lo:hi], tag=g.tag,
+                obs_cap=(g.obs_cap[sel] - lo).astype(np.int32), obs_tag=g.obs_tag[sel],
+                corners=g.corners[sel])
+
+
+def cpu_baseline(g, threads, sample_iters=1):
+    """CPU oracle on a bounded sample: the first `sample_iters` LM iterations of the workload."""
+    from oracle import oracle as O
+    O.build()
+    t0 = time.perf_counter()
+    _, _, _, s = O.solve_graph(g, max_num_iterations=sample_iters, num_threads=threads)
+    dt = time.perf_counter() - t0
+    iters = s["num_linear_solves"]
+    return {"value": iters / dt, "unit": "LM iterations/s", "cores": threads, "kind": "port",
+            "sample": f"first {iters} LM iteration(s) of the same workload incl. iteration-0 "
+                      f"linearization, CPU oracle (C, OpenMP dense LLT on {threads} threads), "
+                      f"{dt:.1f} s"}
+
+
+def load_pmc_traffic():
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_dominant.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--skip-zero-tiles", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from ar_slam_amd import build, lm, synth
+    build.build()
+    g = synth.config_graph(args.config)
+    part = shard_graph(g, rank, world) if world > 1 else dict(
+        camera=g.camera, cap=g.cap, tag=g.tag, obs_cap=g.obs_cap, obs_tag=g.obs_tag, corners=g.corners)
+    comm = None
+    if world > 1:
+        obj = [lm.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = (rank, world, obj[0])
+    rp = lm.ResidentProblem(**part, comm=comm, device=local_rank,
+                            kernel_timing=0 if args.no_kernel_timing else 1,
+                            cholesky_skip_zero_tiles=args.skip_zero_tiles)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        rp.solve()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sums = []
+    for _ in range(args.steps):
+        sums.append(rp.solve())
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    iters = sum(s["num_linear_solves"] for s in sums)
+    last = sums[-1]
+    dom_ms = sum(s["t_dominant_ms"] for s in sums)
+    dom_launches = sum(s["n_dominant_launches"] for s in sums)
+    dom_flops = sum(s["dominant_flops"] for s in sums)
+    roofline = None
+    if dom_launches:
+        avg_ms = dom_ms / dom_launches
+        flops_per_launch = dom_flops / dom_launches
+        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": "k_update (reduced-system Cholesky trailing update, "
+                                               "v_mfma_f64_16x16x4_f64)",
+                    "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_pmc_traffic(),
+                    "avg_launch_us": avg_ms * 1e3, "flops_per_launch": flops_per_launch,
+                    "launches": dom_launches}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": iters / elapsed,
+            "unit": "LM iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded generator, SURVEY.md §8d)",
+            "config": {"workload": f"{args.config}: {g.n_cap} captures / {g.n_tag} tags / "
+                                   f"{g.n_obs} observations (k=8), one full LM solve per step",
+                       "n_obs": int(g.n_obs), "n_reduced": int(last["n_reduced"]),
+                       "parallelism": f"capture-shard x{world}" if world > 1 else "single GPU"},
+            "ms_to_converged": 1e3 * elapsed / args.steps,
+            "final_rms_px": last["final_rms_px"],
+            "termination": f"{last['termination']} ({last['rule']})",
+            "lm_iterations_per_solve": last["num_linear_solves"],
+            "phase_ms_per_solve": {k: last[f"t_{k}_ms"] for k in
+                                   ("linearize", "schur", "cholesky", "solve", "backsub", "cost")},
+            "roofline": roofline,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(g, threads)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

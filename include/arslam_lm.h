@@ -83,6 +83,7 @@ typedef struct {
   int update_state_every_iteration;  /* write improving iterates back */
   int device;                        /* HIP device ordinal, -1 = current */
   int cholesky_skip_zero_tiles;      /* 1: skip structurally-zero tiles of the reduced system */
+  int kernel_timing;                 /* 1: HIP events around every launch of the dominant kernel */
 } arslam_lm_options;
 
 /* ceres::IterationSummary subset */
@@ -108,6 +109,10 @@ typedef struct {
   double total_time_s;
   /* accumulated device time per phase (ms), from HIP events */
   double t_linearize_ms, t_schur_ms, t_cholesky_ms, t_solve_ms, t_backsub_ms, t_cost_ms;
+  /* dominant kernel (reduced-system trailing update on MFMA), kernel_timing = 1 only */
+  double t_dominant_ms;         /* sum of its launch durations */
+  double dominant_flops;        /* algorithmic flops of those launches */
+  long n_dominant_launches;
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
 } arslam_lm_summary;
