@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libarslam_lm.so")
-SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "debug_api.hip"]
+SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "debug_api.hip", "llt_plan.cpp"]
 ARCH = os.environ.get("ARSLAM_ARCH", "gfx950")
 
 
@@ -44,8 +44,8 @@ def build(force=False, verbose=False):
     objs = []
     procs = []
     for src in SOURCES:
-        obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = [hipcc()] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc()] + flags + (["-x", "hip"] if src.endswith(".cpp") else []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

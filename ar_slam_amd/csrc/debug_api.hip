@@ -67,8 +67,18 @@ extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double
   DBG_CHECK(hipMalloc(&d_flag, sizeof(int)));
   DBG_CHECK(hipMemcpy(d_S, h.data(), (size_t)N * N * sizeof(double), hipMemcpyHostToDevice));
   DBG_CHECK(hipMemset(d_flag, 0, sizeof(int)));
-  arslam::launch_dense_llt(d_S, N, N, d_flag, nullptr, 0);
-  arslam::launch_dense_back_solve(d_S, N, N, n, d_z, d_y, d_flag, nullptr, 0);
+  const int T = (int)(N / arslam::kTile);
+  std::vector<uint8_t> pattern((size_t)T * T, 0);
+  for (int i = 0; i < T; ++i)
+    for (int j = 0; j <= i; ++j) pattern[(size_t)i * T + j] = 1;
+  arslam::LltPlan plan;
+  try {
+    arslam::llt_plan_build(plan, T, N, pattern, 0);
+  } catch (...) {
+    return ARSLAM_E_HIP;
+  }
+  arslam::launch_dense_llt(plan, d_S, d_flag, 0);
+  arslam::launch_dense_back_solve(plan, d_S, n, d_z, d_y, d_flag, 0);
   DBG_CHECK(hipGetLastError());
   DBG_CHECK(hipDeviceSynchronize());
   DBG_CHECK(hipMemcpy(h.data(), d_S, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost));
@@ -76,6 +86,7 @@ extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double
   DBG_CHECK(hipMemcpy(info, d_flag, sizeof(int), hipMemcpyDeviceToHost));
   for (long i = 0; i < n; ++i)
     for (long j = 0; j < n; ++j) A[i * n + j] = j <= i ? h[i * N + j] : 0.0;
+  arslam::llt_plan_free(plan);
   (void)hipFree(d_S);
   (void)hipFree(d_z);
   (void)hipFree(d_y);

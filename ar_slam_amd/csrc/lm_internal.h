@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <vector>
 
 namespace arslam {
 
@@ -49,7 +50,40 @@ struct DevProblem {
   const int *tag_start;      // [nt+1]  CSR of observations by tag (capture-major order inside)
   const int *tag_obs;        // [nb]
   const double *corners;     // [nb*8]
+  const int *tag_pos;        // [nt]    position of tag t in the reduced ordering (F index 6*pos)
+  const int *pos_tag;        // [nt]    inverse
 };
+
+// reduced index of parameter j (0..5) of tag t, and the slot of reduced index i
+__device__ inline long fidx_tag(const DevProblem &P, int t, int j) { return 6L * P.tag_pos[t] + j; }
+__device__ inline long fslot(const DevProblem &P, long i) {
+  return i < 6L * P.nt ? 3 + 6L * P.nc + 6L * P.pos_tag[i / 6] + i % 6 : i - 6L * P.nt;
+}
+
+// Tile plan of the reduced-system Cholesky (see dense_llt.hip).  Per step k:
+// the tile rows i > k of column k (TRSM), the (i,j) pairs it updates, and the
+// tile columns of row k (backward solve).  Device arrays, host offsets.
+struct LltPlan {
+  int T = 0;
+  long lda = 0;
+  int *trsm_rows = nullptr;
+  int2 *upd_pairs = nullptr;
+  int *bs_cols = nullptr;
+  int2 *tiles = nullptr;     // every tile of the factor (zeroed before assembly)
+  long n_tiles = 0;
+  std::vector<int> h_trsm_off;
+  std::vector<long> h_upd_off;
+  std::vector<int> h_bs_off;
+  std::vector<double> h_upd_flops;   // useful flops of each step's update
+  double total_upd_flops = 0.0;
+  long total_upd_tiles = 0;
+};
+
+// Symbolic tile fill of the lower pattern (T*T bytes, in/out) and device lists.
+void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern, hipStream_t s);
+void llt_plan_free(LltPlan &plan);
+// Reverse Cuthill-McKee order of an undirected graph (adjacency lists).
+std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj);
 
 // ---- lm_kernels.hip ----
 void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
@@ -88,13 +122,14 @@ struct LaunchTiming {
 };
 
 // ---- dense_llt.hip ----
-// Cholesky of the lower triangle of S (N x N, row-major, lda), in place.  Row
-// nF carries the right-hand side, so on exit row nF = (L^{-1} b)^T.  *flag is
-// set non-zero if a pivot is not positive.  Then y = L^{-T} z into yF[0..nF).
-void launch_dense_llt(double *S, long N, long lda, int *flag, const uint8_t *tile_nz,
-                      hipStream_t s, LaunchTiming *timing = nullptr);
-void launch_dense_back_solve(const double *S, long N, long lda, long nF, double *z, double *yF,
-                             const int *flag, const uint8_t *tile_nz, hipStream_t s);
-void launch_zero_lower(double *S, long N, long lda, const uint8_t *tile_nz, hipStream_t s);
+// Cholesky of the lower triangle of S (row-major, lda) over the plan's tiles,
+// in place.  Row nF carries the right-hand side, so on exit row nF =
+// (L^{-1} b)^T.  *flag is set non-zero if a pivot is not positive.  Then
+// y = L^{-T} z into yF[0..nF).
+void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
+                      LaunchTiming *timing = nullptr);
+void launch_dense_back_solve(const LltPlan &P, const double *S, long nF, double *z, double *yF,
+                             const int *flag, hipStream_t s);
+void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s);
 
 }  // namespace arslam

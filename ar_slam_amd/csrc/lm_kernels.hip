@@ -438,7 +438,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   for (int q = lane; q < k; q += kWave) lblk[q] = P.obs_lblk[o0 + q];
   for (int p = lane; p < m; p += kWave) {
     if (p == 0) gidx[p] = 6L * P.nt;
-    else gidx[p] = 6L * P.blk_tag[b0 + (p - 1) / 6] + (p - 1) % 6;
+    else gidx[p] = fidx_tag(P, P.blk_tag[b0 + (p - 1) / 6], (p - 1) % 6);
   }
   fill_rows(P, x, scale, c, o0, nrows, rows);
   __syncthreads();
@@ -530,8 +530,7 @@ __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, do
   if (i >= P.N) return;
   double *d = S + i * P.lda + i;
   if (i < P.nF) {
-    const long slot = i < 6L * P.nt ? slot_tag(P, (int)(i / 6)) + i % 6 : (i - 6L * P.nt);
-    *d += lm_d2(diag, slot, radius);
+    *d += lm_d2(diag, fslot(P, i), radius);
   } else if (i == P.nF) {
     *d = 1e300;
   } else {
@@ -572,7 +571,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   const double yf = yF[6L * P.nt];
   for (int row = lane; row < nrows; row += kWave) {
     const double *rr = rows + (long)row * kRowStride;
-    const long tb = 6L * P.obs_tag[o0 + (row >> 3)];
+    const long tb = fidx_tag(P, P.obs_tag[o0 + (row >> 3)], 0);
     double q = rr[0] * yf;
 #pragma unroll
     for (int j = 0; j < 6; ++j) q += rr[7 + j] * yF[tb + j];
@@ -649,7 +648,7 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0;
   if (i < P.nF) {
-    const long slot = i < 6L * P.nt ? slot_tag(P, (int)(i / 6)) + i % 6 : (i - 6L * P.nt);
+    const long slot = fslot(P, i);
     const double yv = yF[i];
     const double xo = x[slot];
     const double xn = xo + (-yv * scale[slot]);

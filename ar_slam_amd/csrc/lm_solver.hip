@@ -131,7 +131,8 @@ struct arslam_lm {
   DevBuf<unsigned char> d_obs_active, d_slot_free;
   DevBuf<double> d_corners, d_x0, d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_norms, d_S, d_z, d_yF;
-  DevBuf<int> d_flag;
+  DevBuf<int> d_flag, d_tag_pos, d_pos_tag;
+  arslam::LltPlan plan;
   double *x = nullptr, *xc = nullptr;
   int n_fparts = 0;
 
@@ -143,7 +144,7 @@ struct arslam_lm {
 
   void timing_begin() {
     if (!opt.kernel_timing || !has_f) return;
-    const int need = (int)(N / arslam::kTile) + 1;
+    const int need = plan.T + 1;
     if ((int)upd_events.size() < 2 * need) {
       for (auto e : upd_events) (void)hipEventDestroy(e);
       upd_events.assign(2 * need, nullptr);
@@ -174,6 +175,7 @@ struct arslam_lm {
   ~arslam_lm() {
     for (auto &t : timers) t.destroy();
     for (auto e : upd_events) (void)hipEventDestroy(e);
+    arslam::llt_plan_free(plan);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -303,6 +305,87 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   if (nc) std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
   if (nt) std::memcpy(x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
 
+  // ---- reduced-system ordering and tile plan ----
+  std::vector<int> tag_pos(std::max(nt, 1)), pos_tag(std::max(nt, 1));
+  const bool sparse = opt.cholesky_skip_zero_tiles != 0;
+  {
+    std::vector<int> order(nt);
+    for (int t = 0; t < nt; ++t) order[t] = t;
+    if (sparse && nt > 1) {
+      std::vector<std::vector<int>> adj(nt);
+      if (nranks > 1) {
+        fail_if(nt > 16384, ARSLAM_E_UNSUPPORTED, "sparse multi-GPU plan limited to 16384 tags");
+        std::vector<uint8_t> bm((size_t)nt * nt, 0);
+        for (int c = 0; c < nc; ++c)
+          for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a)
+            for (int b = cap_blk_start[c]; b < cap_blk_start[c + 1]; ++b)
+              if (a != b) bm[(size_t)blk_tag[a] * nt + blk_tag[b]] = 1;
+        DevBuf<uint8_t> tmp;
+        tmp.alloc(bm.size());
+        tmp.upload(bm.data(), bm.size(), stream);
+        NCCL_CHECK(ncclAllReduce(tmp.p, tmp.p, bm.size(), ncclUint8, ncclMax, comm, stream));
+        HIP_CHECK(hipMemcpyAsync(bm.data(), tmp.p, bm.size(), hipMemcpyDeviceToHost, stream));
+        HIP_CHECK(hipStreamSynchronize(stream));
+        for (int a = 0; a < nt; ++a)
+          for (int b = 0; b < nt; ++b)
+            if (bm[(size_t)a * nt + b]) adj[a].push_back(b);
+      } else {
+        for (int c = 0; c < nc; ++c)
+          for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a)
+            for (int b = cap_blk_start[c]; b < cap_blk_start[c + 1]; ++b)
+              if (a != b) adj[blk_tag[a]].push_back(blk_tag[b]);
+        for (auto &v : adj) {
+          std::sort(v.begin(), v.end());
+          v.erase(std::unique(v.begin(), v.end()), v.end());
+        }
+      }
+      order = arslam::rcm_order(nt, adj);
+    }
+    for (int p = 0; p < nt; ++p) {
+      pos_tag[p] = order[p];
+      tag_pos[order[p]] = p;
+    }
+  }
+  if (has_f) {
+    N = round_up(nF + 1, arslam::kTile);
+    const int T = (int)(N / arslam::kTile);
+    std::vector<uint8_t> pattern((size_t)T * T, 0);
+    if (!sparse) {
+      for (int i = 0; i < T; ++i)
+        for (int j = 0; j <= i; ++j) pattern[(size_t)i * T + j] = 1;
+    } else {
+      auto mark_set = [&](std::vector<int> &ts) {
+        std::sort(ts.begin(), ts.end());
+        ts.erase(std::unique(ts.begin(), ts.end()), ts.end());
+        for (size_t a = 0; a < ts.size(); ++a)
+          for (size_t b = 0; b <= a; ++b) pattern[(size_t)ts[a] * T + ts[b]] = 1;
+      };
+      std::vector<int> ts;
+      const int cam0 = (int)((6L * nt) / arslam::kTile), cam1 = (int)((6L * nt + 2) / arslam::kTile);
+      for (int c = 0; c < nc; ++c) {
+        ts.assign({cam0, cam1});
+        for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a) {
+          const long f0 = 6L * tag_pos[blk_tag[a]];
+          ts.push_back((int)(f0 / arslam::kTile));
+          ts.push_back((int)((f0 + 5) / arslam::kTile));
+        }
+        mark_set(ts);
+      }
+      const int rhs = (int)(nF / arslam::kTile);
+      for (int j = 0; j <= rhs; ++j) pattern[(size_t)rhs * T + j] = 1;
+      for (int j = 0; j <= cam1; ++j) pattern[(size_t)cam1 * T + j] = 1;   // camera border (camera free)
+      if (nranks > 1) {
+        DevBuf<uint8_t> tmp;
+        tmp.alloc(pattern.size());
+        tmp.upload(pattern.data(), pattern.size(), stream);
+        NCCL_CHECK(ncclAllReduce(tmp.p, tmp.p, pattern.size(), ncclUint8, ncclMax, comm, stream));
+        HIP_CHECK(hipMemcpyAsync(pattern.data(), tmp.p, pattern.size(), hipMemcpyDeviceToHost, stream));
+        HIP_CHECK(hipStreamSynchronize(stream));
+      }
+    }
+    arslam::llt_plan_build(plan, T, N, pattern, stream);
+  }
+
   // ---- device upload ----
   d_cap_start.alloc(nc + 1); d_cap_start.upload(cap_start.data(), nc + 1, stream);
   d_obs_tag.alloc(nb); d_obs_tag.upload(obs_tag.data(), nb, stream);
@@ -324,8 +407,9 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_red.alloc(16);
   d_norms.alloc(8);
   d_flag.alloc(1);
+  d_tag_pos.alloc(tag_pos.size()); d_tag_pos.upload(tag_pos.data(), tag_pos.size(), stream);
+  d_pos_tag.alloc(pos_tag.size()); d_pos_tag.upload(pos_tag.data(), pos_tag.size(), stream);
   if (has_f) {
-    N = round_up(nF + 1, arslam::kTile);
     d_S.alloc((size_t)N * N);
     HIP_CHECK(hipMemsetAsync(d_S.p, 0, (size_t)N * N * sizeof(double), stream));
     d_z.alloc(N);
@@ -345,6 +429,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   P.cap_blk_start = d_cap_blk_start.p; P.blk_tag = d_blk_tag.p;
   P.obs_active = d_obs_active.p; P.slot_free = d_slot_free.p;
   P.tag_start = d_tag_start.p; P.tag_obs = d_tag_obs.p; P.corners = d_corners.p;
+  P.tag_pos = d_tag_pos.p; P.pos_tag = d_pos_tag.p;
   HIP_CHECK(hipStreamSynchronize(stream));
   loaded = true;
 }
@@ -500,18 +585,17 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     HIP_CHECK(hipMemsetAsync(d_flag.p, 0, sizeof(int), stream));
     if (has_f) {
       timers[PH_SCHUR].start(stream);
-      arslam::launch_zero_lower(d_S.p, N, N, nullptr, stream);
+      arslam::launch_zero_tiles(plan, d_S.p, stream);
       arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream);
       if (nranks > 1) allreduce(d_S.p, (size_t)N * N, ncclSum);
       arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
       timing_begin();
-      arslam::launch_dense_llt(d_S.p, N, N, d_flag.p, nullptr, stream,
-                               opt.kernel_timing ? &upd_timing : nullptr);
+      arslam::launch_dense_llt(plan, d_S.p, d_flag.p, stream, opt.kernel_timing ? &upd_timing : nullptr);
       timers[PH_CHOL].stop(stream);
       timers[PH_SOLVE].start(stream);
-      arslam::launch_dense_back_solve(d_S.p, N, N, nF, d_z.p, d_yF.p, d_flag.p, nullptr, stream);
+      arslam::launch_dense_back_solve(plan, d_S.p, nF, d_z.p, d_yF.p, d_flag.p, stream);
       timers[PH_SOLVE].stop(stream);
     }
     timers[PH_BACK].start(stream);
@@ -621,6 +705,9 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->t_dominant_ms = dom_ms;
   s->dominant_flops = dom_flops;
   s->n_dominant_launches = dom_launches;
+  s->n_factor_tiles = plan.n_tiles;
+  s->n_update_tiles = plan.total_upd_tiles;
+  s->factor_update_flops = plan.total_upd_flops;
 }
 
 // ===========================================================================

@@ -96,6 +96,8 @@ class Summary(C.Structure):
                 ("t_backsub_ms", C.c_double), ("t_cost_ms", C.c_double),
                 ("t_dominant_ms", C.c_double), ("dominant_flops", C.c_double),
                 ("n_dominant_launches", C.c_long),
+                ("n_factor_tiles", C.c_long), ("n_update_tiles", C.c_long),
+                ("factor_update_flops", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 
     def to_dict(self):

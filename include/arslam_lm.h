@@ -113,6 +113,10 @@ typedef struct {
   double t_dominant_ms;         /* sum of its launch durations */
   double dominant_flops;        /* algorithmic flops of those launches */
   long n_dominant_launches;
+  /* reduced-system tile plan (per factorization) */
+  long n_factor_tiles;          /* 64x64 tiles of the factor that exist */
+  long n_update_tiles;          /* tile updates (MFMA work items) */
+  double factor_update_flops;   /* useful flops of the trailing updates */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
 } arslam_lm_summary;

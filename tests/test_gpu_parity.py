@@ -156,3 +156,27 @@ def test_resident_problem_resolves_identically(lm):
     s2 = rp.solve()
     assert [i["cost"] for i in s1["iterations"]] == pytest.approx([i["cost"] for i in s2["iterations"]], rel=1e-12)
     np.testing.assert_allclose(rp.cap, c1, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["small", "medium", "cfg2"])
+def test_sparse_tile_plan_matches_oracle(lm, oracle, name):
+    """RCM-ordered reduced system with structurally-zero tiles skipped: same LM."""
+    g = synth.config_graph(name)
+    ref = oracle.solve_graph(g)
+    ours = lm.solve_graph(g, cholesky_skip_zero_tiles=1)
+    _compare_solves(g, ours, ref)
+    if name == "cfg2":
+        s = ours[3]
+        T = (6 * g.n_tag + 3 + 1 + 63) // 64
+        assert s["n_factor_tiles"] < T * (T + 1) // 2
+
+
+def test_sparse_plan_equals_dense_plan_on_same_order(lm):
+    """Skipping zero tiles changes nothing but the work: the trace matches the dense plan."""
+    g = synth.config_graph("cfg2")
+    dense = lm.solve_graph(g)
+    sparse = lm.solve_graph(g, cholesky_skip_zero_tiles=1)
+    cd = [it["cost"] for it in dense[3]["iterations"]]
+    cs = [it["cost"] for it in sparse[3]["iterations"]]
+    assert len(cd) == len(cs)
+    np.testing.assert_allclose(cs, cd, rtol=1e-10)
