@@ -79,6 +79,7 @@ extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double
   }
   arslam::launch_dense_llt(plan, d_S, d_flag, 0);
   arslam::launch_dense_back_solve(plan, d_S, n, d_z, d_y, d_flag, 0);
+  arslam::launch_scatter_diag(plan, d_S, 0);
   DBG_CHECK(hipGetLastError());
   DBG_CHECK(hipDeviceSynchronize());
   DBG_CHECK(hipMemcpy(h.data(), d_S, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost));

@@ -22,7 +22,6 @@
 #include "lm_internal.h"
 
 #include <cmath>
-#include <cstdlib>
 
 namespace arslam {
 
@@ -122,14 +121,13 @@ __device__ __forceinline__ void wave_gemm16_sub(double *C, const double *A, cons
 // 16 columns: unblocked 16x16 factor (16 lanes of wave 0), row solve of the
 // panel below (16 lanes per wave), MFMA rank-16 update of the trailing tile.
 // Returns false (uniformly) if a pivot is not positive; inv[c] = 1 / L_cc.
-template <int AB>
 __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, int tid) {
   const int w = tid >> 6, lane = tid & 63;
   if (tid == 0) *bad = 0;
   __syncthreads();
   for (int p = 0; p < 4; ++p) {
     const int b0 = 16 * p;
-    if (w == 0 && !(AB & 1)) {
+    if (w == 0) {
       // 16x16 diagonal block, lane i < 16 owns row b0+i in registers.  LDL^T
       // form: a_ic -= (a_ij / a_jj) a_cj, so only a reciprocal sits on the
       // pivot chain (the square roots are taken once at the end); the pivot
@@ -187,7 +185,7 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
     // rows below the diagonal block: X L_pp^T = A_panel
     {
       const int i = b0 + 16 + w * 16 + lane;
-      if (lane < 16 && i < 64 && !(AB & 2)) {
+      if (lane < 16 && i < 64) {
         double x[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) x[c] = D[i * LQ + b0 + c];
@@ -205,7 +203,7 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
     __syncthreads();
     // trailing update of blocks p+1..3 (lower tiles I >= C) with the panel
     const int m = 3 - p;
-    const int ntl = (AB & 4) ? 0 : m * (m + 1) / 2;
+    const int ntl = m * (m + 1) / 2;
     for (int t = w; t < ntl; t += 4) {
       int I = 0;
       while ((I + 1) * (I + 2) / 2 <= t) ++I;
@@ -220,16 +218,15 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
 
 // In-LDS blocked solve X L^T = A for a 64x64 tile X (256 threads), L from
 // blocked_potrf64 (lower part of D, inv = 1 / diag).
-template <int AB>
 __device__ void blocked_trsm64(double *X, const double *D, const double *inv, const double *LTd,
                                int tid) {
   const int w = tid >> 6, lane = tid & 63;
   for (int p = 0; p < 4; ++p) {
     const int b0 = 16 * p;
-    if (p > 0 && !(AB & 8))   // X[:, b0:b0+16] -= X[:, 0:b0] L[b0:b0+16, 0:b0]^T  (wave w: rows 16w..)
+    if (p > 0)   // X[:, b0:b0+16] -= X[:, 0:b0] L[b0:b0+16, 0:b0]^T  (wave w: rows 16w..)
       wave_gemm16_sub(X + 16 * w * LQ + b0, X + 16 * w * LQ, D + b0 * LQ, b0, lane);
     __syncthreads();
-    if (lane < 16 && !(AB & 16)) {
+    if (lane < 16) {
       const int r = 16 * w + lane;
       double x[16];
 #pragma unroll
@@ -248,12 +245,14 @@ __device__ void blocked_trsm64(double *X, const double *D, const double *inv, co
   }
 }
 
-// Panel of step k: workgroup 0 factors the diagonal tile (k,k) and stores
-// L_kk; workgroup b > 0 factors it redundantly (no extra launch on the
-// critical path) and solves tile (rows[b-1], k).
-template <int AB>
-__global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda, int k,
-                                               const int *__restrict__ rows,
+// Panel tasks of one level: task (i,k) factors the diagonal tile (k,k) (every
+// task of column k does so redundantly, keeping the level to one launch) and
+// either stores L_kk (i == k) or solves tile (i,k) against it.  L_kk goes to
+// its own buffer Ld (64x64 per tile column), never over A_kk in S: the other
+// tasks of the column may still be reading A_kk.
+__global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
+                                               double *__restrict__ Ld,
+                                               const int2 *__restrict__ tasks,
                                                int *__restrict__ flag) {
   __shared__ __attribute__((aligned(16))) double D[T64 * LQ];
   __shared__ __attribute__((aligned(16))) double X[T64 * LQ];
@@ -261,57 +260,46 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
   __shared__ __attribute__((aligned(16))) double LTd[32 + 4 * 256];   // column scratch + transposed diagonal blocks
   __shared__ int bad;
   if (*flag) return;
-  const int tid = threadIdx.x, b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int2 t = tasks[blockIdx.x];
+  const int ti = t.x, k = t.y;
   const double *dk = S + (long)k * T64 * lda + (long)k * T64;
-  double *xt = b > 0 ? S + (long)rows[b - 1] * T64 * lda + (long)k * T64 : nullptr;
+  double *xt = S + (long)ti * T64 * lda + (long)k * T64;
   load_tile_wg(dk, lda, D, tid);
-  if (b > 0) load_tile_wg(xt, lda, X, tid);
+  if (ti != k) load_tile_wg(xt, lda, X, tid);
   __syncthreads();
-  const bool ok = blocked_potrf64<AB>(D, inv, LTd, &bad, tid) || AB != 0;
+  const bool ok = blocked_potrf64(D, inv, LTd, &bad, tid);
   if (!ok) {
-    if (b == 0 && tid == 0) {
+    if (ti == k && tid == 0) {
       int first = 0;
       while (first < T64 && D[first * LQ + first] > 0.0) ++first;
       atomicCAS(flag, 0, 1 + k * T64 + first);
     }
     return;
   }
-  if (b == 0) {
-    store_tile_wg(const_cast<double *>(dk), lda, D, tid, true);
+  if (ti == k) {
+    store_tile_wg(Ld + (long)k * T64 * T64, T64, D, tid, true);
     return;
   }
-  blocked_trsm64<AB>(X, D, inv, LTd, tid);
+  blocked_trsm64(X, D, inv, LTd, tid);
   store_tile_wg(xt, lda, X, tid, false);
 }
 
-// A_ij -= L_ik L_jk^T for the (i,j) tile pairs listed for step k.
-__global__ __launch_bounds__(256) void k_update(double *__restrict__ S, long lda, int k,
-                                                const int2 *__restrict__ pairs,
+// Update targets of one level: tile (i,j) -= sum over the level's columns k
+// of L_ik L_jk^T.  One workgroup per target (no two workgroups write the same
+// tile); 4 waves x 32x32 on v_mfma_f64_16x16x4_f64, K = 64 per column.
+__global__ __launch_bounds__(256) void k_update(double *__restrict__ S, long lda,
+                                                const int2 *__restrict__ targets,
+                                                const int *__restrict__ kstart,
+                                                const int *__restrict__ ks,
                                                 const int *__restrict__ flag) {
   __shared__ __attribute__((aligned(16))) double sA[T64 * LM];
   __shared__ __attribute__((aligned(16))) double sB[T64 * LM];
   if (*flag) return;
-  const int2 pr = pairs[blockIdx.x];
+  const int2 pr = targets[blockIdx.x];
   const int ti = pr.x, tj = pr.y;
+  const int q0 = kstart[blockIdx.x], q1 = kstart[blockIdx.x + 1];
   const int tid = threadIdx.x;
-  const double *Ai = S + (long)ti * T64 * lda + (long)k * T64;
-  const double *Bj = S + (long)tj * T64 * lda + (long)k * T64;
-  {
-    dbl2 va[8], vb[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
-      va[q] = *reinterpret_cast<const dbl2 *>(Ai + (long)r * lda + c2);
-      vb[q] = *reinterpret_cast<const dbl2 *>(Bj + (long)r * lda + c2);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
-      *reinterpret_cast<dbl2 *>(&sA[r * LM + c2]) = va[q];
-      *reinterpret_cast<dbl2 *>(&sB[r * LM + c2]) = vb[q];
-    }
-  }
-  __syncthreads();
   const int w = tid >> 6, lane = tid & 63;
   const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
   const int li = lane & 15, lk = lane >> 4;
@@ -324,17 +312,37 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, long lda
     for (int reg = 0; reg < 4; ++reg) cval[4 * q + reg] = C[(long)(rb + lk + 4 * reg) * lda + cb + li];
   }
   dbl4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
+  for (int q = q0; q < q1; ++q) {
+    const int k = ks[q];
+    const double *Ai = S + (long)ti * T64 * lda + (long)k * T64;
+    const double *Bj = S + (long)tj * T64 * lda + (long)k * T64;
+    dbl2 va[8], vb[8];
+#pragma unroll
+    for (int e8 = 0; e8 < 8; ++e8) {
+      const int e = e8 * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
+      va[e8] = *reinterpret_cast<const dbl2 *>(Ai + (long)r * lda + c2);
+      vb[e8] = *reinterpret_cast<const dbl2 *>(Bj + (long)r * lda + c2);
+    }
+    if (q > q0) __syncthreads();   // previous column's fragments consumed
+#pragma unroll
+    for (int e8 = 0; e8 < 8; ++e8) {
+      const int e = e8 * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
+      *reinterpret_cast<dbl2 *>(&sA[r * LM + c2]) = va[e8];
+      *reinterpret_cast<dbl2 *>(&sB[r * LM + c2]) = vb[e8];
+    }
+    __syncthreads();
 #pragma unroll 4
-  for (int kk = 0; kk < T64 / 4; ++kk) {
-    const int kc = kk * 4 + lk;
-    const double a0 = sA[(r0 + li) * LM + kc];
-    const double a1 = sA[(r0 + 16 + li) * LM + kc];
-    const double b0 = sB[(c0 + li) * LM + kc];
-    const double b1 = sB[(c0 + 16 + li) * LM + kc];
-    acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
-    acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
-    acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
-    acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+    for (int kk = 0; kk < T64 / 4; ++kk) {
+      const int kc = kk * 4 + lk;
+      const double a0 = sA[(r0 + li) * LM + kc];
+      const double a1 = sA[(r0 + 16 + li) * LM + kc];
+      const double b0 = sB[(c0 + li) * LM + kc];
+      const double b1 = sB[(c0 + 16 + li) * LM + kc];
+      acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+    }
   }
   // f64 MFMA C/D layout: col = lane & 15, row = (lane >> 4) + 4 * reg
   const dbl4 accs[4] = {acc00, acc01, acc10, acc11};
@@ -349,34 +357,61 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, long lda
   }
 }
 
-// z[j] = S[nF][j] (the forward-substituted right-hand side)
-__global__ void k_init_z(const double *__restrict__ S, long lda, long nF, long N,
-                         double *__restrict__ z) {
+// z[j] = L[nR][j], the forward-substituted right-hand side: from S for the
+// tiles left of the rhs row's own tile, from that tile's diagonal factor in Ld.
+__global__ void k_init_z(const double *__restrict__ S, long lda, const double *__restrict__ Ld,
+                         long nR, long N, double *__restrict__ z) {
   const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < N) z[j] = j < nF ? S[nF * lda + j] : 0.0;
+  if (j >= N) return;
+  const long kr = nR / T64;
+  double v = 0.0;
+  if (j < nR) {
+    if (j >= kr * T64) v = Ld[kr * T64 * T64 + (nR - kr * T64) * T64 + (j - kr * T64)];
+    else v = S[nR * lda + j];
+  }
+  z[j] = v;
 }
 
-// One tile row k of L^T y = z.  Every workgroup solves the 64x64 diagonal
-// block (redundantly; lane r owns z_r, blocked by 16 with scalar broadcasts),
-// then z_j -= L_kj^T y_k over its listed tile column.  Workgroup 0 writes y_k.
-__global__ __launch_bounds__(64) void k_back_solve(const double *__restrict__ S, long lda, long nF,
-                                                   int k, const int *__restrict__ cols,
-                                                   double *__restrict__ z, double *__restrict__ yF,
-                                                   const int *__restrict__ flag) {
+// Backward solve L^T y = z for the columns of one level (root level first).
+// Column k gathers z_k -= sum_i L_ik^T y_i over its tile rows i > k (all of
+// them ancestors, solved by earlier launches), then solves the 64x64 block
+// L_kk^T y_k = z_k with lane r owning z_r and scalar broadcasts of y.
+__global__ __launch_bounds__(256) void k_back_solve(const double *__restrict__ S, long lda,
+                                                    const double *__restrict__ Ld, long nR,
+                                                    const int *__restrict__ cols,
+                                                    const int *__restrict__ gstart,
+                                                    const int *__restrict__ grows,
+                                                    const double *__restrict__ z,
+                                                    double *__restrict__ yF,
+                                                    const int *__restrict__ flag) {
   __shared__ double Lk[T64 * LP];
+  __shared__ double part[4][T64];
   __shared__ double y[T64];
   if (*flag) return;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int k = cols[blockIdx.x];
   const long row0 = (long)k * T64;
-  const double *lk = S + row0 * lda + row0;
-  double zr = (row0 + lane < nF) ? z[row0 + lane] : 0.0;
-  load_tile64(lk, lda, Lk, lane);
+  const int g0 = gstart[blockIdx.x], g1 = gstart[blockIdx.x + 1];
+  // gather: wave w takes rows r = w, w+4, ... of every gathered tile
+  double acc = 0.0;
+  for (int g = g0; g < g1; ++g) {
+    const long ri = (long)grows[g] * T64;
+    const double *Lik = S + ri * lda + row0;
+#pragma unroll 4
+    for (int r = w; r < T64; r += 4) {
+      const double yv = (ri + r < nR) ? yF[ri + r] : 0.0;
+      acc += Lik[(long)r * lda + lane] * yv;
+    }
+  }
+  part[w][lane] = acc;
+  if (w == 0) load_tile64(Ld + (long)k * T64 * T64, T64, Lk, lane);
   __syncthreads();
-  const double my_inv = (row0 + lane < nF) ? 1.0 / Lk[lane * LP + lane] : 0.0;   // y = 0 past nF
+  if (w != 0) return;
+  double zr = (row0 + lane < nR) ? z[row0 + lane] - (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) : 0.0;
+  const double my_inv = (row0 + lane < nR) ? 1.0 / Lk[lane * LP + lane] : 0.0;   // y = 0 past nR
   double yv_own = 0.0;
   for (int p = 3; p >= 0; --p) {
     const int b0 = 16 * p;
-    // 16x16 diagonal block: sequential over rows, scalar broadcast of y
     for (int rr = 15; rr >= 0; --rr) {
       const int r = b0 + rr;
       const double yv = readlane_d(zr * my_inv, r);
@@ -384,30 +419,17 @@ __global__ __launch_bounds__(64) void k_back_solve(const double *__restrict__ S,
       if (lane >= b0 && lane < r) zr -= Lk[r * LP + lane] * yv;
     }
     y[lane] = yv_own;
-    __syncthreads();
-    // rows above the block: z_i -= sum_r L[b0+r][i] y[b0+r]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane < b0) {
-      double acc = 0.0;
+      double a2 = 0.0;
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) acc += Lk[(b0 + rr) * LP + lane] * y[b0 + rr];
-      zr -= acc;
+      for (int rr = 0; rr < 16; ++rr) a2 += Lk[(b0 + rr) * LP + lane] * y[b0 + rr];
+      zr -= a2;
     }
-    __syncthreads();
   }
-  y[lane] = yv_own;
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    if (row0 + lane < nF) yF[row0 + lane] = yv_own;
-    return;
-  }
-  const long j = (long)cols[blockIdx.x - 1] * T64 + lane;
-  double s0 = 0.0, s1 = 0.0;
-#pragma unroll 8
-  for (int r = 0; r < T64; r += 2) {
-    s0 += S[(row0 + r) * lda + j] * y[r];
-    s1 += S[(row0 + r + 1) * lda + j] * y[r + 1];
-  }
-  z[j] -= s0 + s1;
+  if (row0 + lane < nR) yF[row0 + lane] = yv_own;
 }
 
 __global__ void k_zero_tiles(double *__restrict__ S, long lda, const int2 *__restrict__ tiles) {
@@ -421,12 +443,14 @@ __global__ void k_zero_tiles(double *__restrict__ S, long lda, const int2 *__res
 
 }  // namespace
 
-static int panel_ablation() {
-  static const int v = [] {
-    const char *e = std::getenv("ARSLAM_PANEL_ABLATION");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
+__global__ void k_scatter_diag(double *__restrict__ S, long lda, const double *__restrict__ Ld) {
+  const int k = blockIdx.x;
+  for (int e = threadIdx.x; e < T64 * T64; e += blockDim.x)
+    S[((long)k * T64 + e / T64) * lda + (long)k * T64 + e % T64] = Ld[(long)k * T64 * T64 + e];
+}
+
+void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s) {
+  hipLaunchKernelGGL(k_scatter_diag, dim3((unsigned)P.T), dim3(256), 0, s, S, P.lda, P.ldiag);
 }
 
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s) {
@@ -435,43 +459,34 @@ void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s) {
 }
 
 void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, LaunchTiming *timing) {
-  const int T = P.T;
-  for (int k = 0; k < T; ++k) {
-    const int nr = P.h_trsm_off[k + 1] - P.h_trsm_off[k];
-    const dim3 g((unsigned)(nr + 1));
-    const int *rows = P.trsm_rows + P.h_trsm_off[k];
-    switch (panel_ablation()) {   // timing-only ablations (ARSLAM_PANEL_ABLATION), 0 = real kernel
-      case 1: hipLaunchKernelGGL(k_panel<1>, g, dim3(256), 0, s, S, P.lda, k, rows, flag); break;
-      case 2: hipLaunchKernelGGL(k_panel<2>, g, dim3(256), 0, s, S, P.lda, k, rows, flag); break;
-      case 4: hipLaunchKernelGGL(k_panel<4>, g, dim3(256), 0, s, S, P.lda, k, rows, flag); break;
-      case 8: hipLaunchKernelGGL(k_panel<8>, g, dim3(256), 0, s, S, P.lda, k, rows, flag); break;
-      case 16: hipLaunchKernelGGL(k_panel<16>, g, dim3(256), 0, s, S, P.lda, k, rows, flag); break;
-      case 31: hipLaunchKernelGGL(k_panel<31>, g, dim3(256), 0, s, S, P.lda, k, rows, flag); break;
-      default: hipLaunchKernelGGL(k_panel<0>, g, dim3(256), 0, s, S, P.lda, k, rows, flag); break;
-    }
-    const long nu = P.h_upd_off[k + 1] - P.h_upd_off[k];
+  for (int l = 0; l < P.nlev; ++l) {
+    const int np = P.h_panel_off[l + 1] - P.h_panel_off[l];
+    hipLaunchKernelGGL(k_panel, dim3((unsigned)np), dim3(256), 0, s, S, P.lda, P.ldiag,
+                       P.panel + P.h_panel_off[l], flag);
+    const int nu = P.h_upd_off[l + 1] - P.h_upd_off[l];
     if (nu > 0) {
       const bool rec = timing && timing->used < timing->cap;
       if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
-      hipLaunchKernelGGL(k_update, dim3((unsigned)nu), dim3(256), 0, s, S, P.lda, k,
-                         P.upd_pairs + P.h_upd_off[k], flag);
+      hipLaunchKernelGGL(k_update, dim3((unsigned)nu), dim3(256), 0, s, S, P.lda,
+                         P.upd_targets + P.h_upd_off[l], P.upd_kstart + P.h_upd_off[l], P.upd_ks, flag);
       if (rec) {
         (void)hipEventRecord(timing->ev[2 * timing->used + 1], s);
         timing->used++;
-        timing->flops += P.h_upd_flops[k];
+        timing->flops += P.h_upd_flops[l];
       }
     }
   }
 }
 
-void launch_dense_back_solve(const LltPlan &P, const double *S, long nF, double *z, double *yF,
+void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s) {
   const long N = (long)P.T * T64;
-  hipLaunchKernelGGL(k_init_z, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, S, P.lda, nF, N, z);
-  for (int k = P.T - 1; k >= 0; --k) {
-    const int nc = P.h_bs_off[k + 1] - P.h_bs_off[k];
-    hipLaunchKernelGGL(k_back_solve, dim3((unsigned)(nc + 1)), dim3(64), 0, s, S, P.lda, nF, k,
-                       P.bs_cols + P.h_bs_off[k], z, yF, flag);
+  hipLaunchKernelGGL(k_init_z, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, S, P.lda, P.ldiag, nR, N,
+                     z);
+  for (int l = 0; l < P.nlev; ++l) {
+    const int b0 = P.h_bs_off[l], nc = P.h_bs_off[l + 1] - b0;
+    hipLaunchKernelGGL(k_back_solve, dim3((unsigned)nc), dim3(256), 0, s, S, P.lda, P.ldiag, nR, P.bs_cols + b0,
+                       P.bs_gstart + b0, P.bs_grows, z, yF, flag);
   }
 }
 

@@ -1,7 +1,14 @@
-// llt_plan.cpp -- host-side symbolic analysis for the reduced-system Cholesky:
-// reverse Cuthill-McKee ordering of the tag co-visibility graph and the
-// tile-level symbolic factorization (fill) that decides which tiles of the
-// factor exist.  Built once per problem structure; the LM steps replay it.
+// llt_plan.cpp -- host-side symbolic analysis of the reduced (tag + camera)
+// system, built once per problem structure and replayed by every LM step:
+//
+//  1. ordering of the tags: natural, reverse Cuthill-McKee (band), or nested
+//     dissection (recursive BFS-level vertex separators, each part aligned to
+//     a 64-row tile so the tile elimination tree mirrors the dissection tree);
+//  2. tile pattern of the reduced matrix (co-visible tags + the camera border
+//     + the right-hand-side row) and its symbolic Cholesky fill;
+//  3. a level schedule of the tile elimination tree: tile columns of equal
+//     height are independent and are factored in one launch, their updates
+//     applied in one launch; the backward solve walks the levels in reverse.
 #include "lm_internal.h"
 
 #include <algorithm>
@@ -26,46 +33,121 @@ T *upload(const std::vector<T> &h, hipStream_t s) {
   return d;
 }
 
-// BFS levels from `start` within unvisited nodes; returns the last level's min-degree node
-int bfs_far(int start, const std::vector<std::vector<int>> &adj, const std::vector<char> &done,
-            int *depth) {
-  std::vector<int> lev(adj.size(), -1);
-  std::deque<int> q{start};
+// BFS over `mark == tag` nodes from start; fills level of each visited node
+// (-1 unvisited) and returns the visit order.
+std::vector<int> bfs(int start, const std::vector<std::vector<int>> &adj, const std::vector<int> &mark,
+                     int tag, std::vector<int> &lev) {
+  std::vector<int> order{start};
   lev[start] = 0;
-  int last = start;
-  while (!q.empty()) {
-    const int u = q.front();
-    q.pop_front();
-    if (lev[u] > lev[last] || (lev[u] == lev[last] && adj[u].size() < adj[last].size())) last = u;
+  for (size_t h = 0; h < order.size(); ++h) {
+    const int u = order[h];
     for (int v : adj[u])
-      if (!done[v] && lev[v] < 0) { lev[v] = lev[u] + 1; q.push_back(v); }
+      if (mark[v] == tag && lev[v] < 0) {
+        lev[v] = lev[u] + 1;
+        order.push_back(v);
+      }
   }
-  *depth = lev[last];
-  return last;
+  return order;
 }
+
+// pseudo-peripheral node of the component of `start` (George-Liu)
+int peripheral(int start, const std::vector<std::vector<int>> &adj, const std::vector<int> &mark,
+               int tag, std::vector<int> &lev) {
+  int best = start, depth = -1;
+  for (int it = 0; it < 6; ++it) {
+    const std::vector<int> ord = bfs(best, adj, mark, tag, lev);
+    const int d = lev[ord.back()];
+    int far = ord.back();
+    for (int u : ord)   // among the last level, the one of least degree
+      if (lev[u] == d && adj[u].size() < adj[far].size()) far = u;
+    for (int u : ord) lev[u] = -1;
+    if (d <= depth) break;
+    depth = d;
+    best = far;
+  }
+  return best;
+}
+
+struct Dissector {
+  const std::vector<std::vector<int>> &adj;
+  int leaf;
+  std::vector<int> mark, lev;
+  int next_tag = 1;
+  std::vector<std::vector<int>> parts;   // elimination order
+
+  Dissector(const std::vector<std::vector<int>> &a, int leaf_size)
+      : adj(a), leaf(leaf_size), mark(a.size(), 0), lev(a.size(), -1) {}
+
+  // nodes: all with mark == tag
+  void run(std::vector<int> nodes, int tag) {
+    if (nodes.empty()) return;
+    // split into connected components
+    std::vector<std::vector<int>> comps;
+    for (int u : nodes) {
+      if (lev[u] >= 0) continue;
+      std::vector<int> c = bfs(u, adj, mark, tag, lev);
+      comps.push_back(std::move(c));
+    }
+    for (int u : nodes) lev[u] = -1;
+    for (auto &c : comps) dissect(c, tag);
+  }
+
+  void dissect(std::vector<int> &comp, int tag) {
+    if ((int)comp.size() <= leaf) {
+      leaf_part(comp, tag);
+      return;
+    }
+    const int s = peripheral(comp[0], adj, mark, tag, lev);
+    std::vector<int> ord = bfs(s, adj, mark, tag, lev);
+    const int depth = lev[ord.back()];
+    if (depth < 2) {
+      for (int u : ord) lev[u] = -1;
+      leaf_part(comp, tag);
+      return;
+    }
+    std::vector<int> cnt(depth + 1, 0);
+    for (int u : ord) cnt[lev[u]]++;
+    // separator level: balances the two sides, never the first or last level
+    int sep = 1, acc = cnt[0];
+    const int half = (int)ord.size() / 2;
+    while (sep < depth - 1 && acc + cnt[sep] / 2 < half) acc += cnt[sep++];
+    std::vector<int> A, B, S;
+    for (int u : ord) {
+      if (lev[u] < sep) A.push_back(u);
+      else if (lev[u] > sep) B.push_back(u);
+      else S.push_back(u);
+    }
+    for (int u : ord) lev[u] = -1;
+    const int ta = ++next_tag, tb = ++next_tag, ts = ++next_tag;
+    for (int u : A) mark[u] = ta;
+    for (int u : B) mark[u] = tb;
+    for (int u : S) mark[u] = ts;
+    run(A, ta);
+    run(B, tb);
+    parts.push_back(S);
+  }
+
+  void leaf_part(std::vector<int> &comp, int tag) {
+    // within a leaf keep BFS order (locality)
+    std::vector<int> ord = bfs(comp[0], adj, mark, tag, lev);
+    for (int u : ord) lev[u] = -1;
+    parts.push_back(ord);
+  }
+};
 
 }  // namespace
 
 std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj) {
   std::vector<int> order;
   order.reserve(n);
+  std::vector<int> mark(n, 0), lev(n, -1);
   std::vector<char> done(n, 0);
   for (;;) {
     int start = -1;
     for (int v = 0; v < n; ++v)
       if (!done[v] && (start < 0 || adj[v].size() < adj[start].size())) start = v;
     if (start < 0) break;
-    // pseudo-peripheral start node (George-Liu): walk to the far end until depth stops growing
-    int depth = 0, far = bfs_far(start, adj, done, &depth);
-    for (int it = 0; it < 8; ++it) {
-      int d2 = 0;
-      const int f2 = bfs_far(far, adj, done, &d2);
-      if (d2 <= depth) break;
-      depth = d2;
-      start = far;
-      far = f2;
-    }
-    start = far;
+    start = peripheral(start, adj, mark, 0, lev);
     std::deque<int> q{start};
     done[start] = 1;
     while (!q.empty()) {
@@ -84,11 +166,19 @@ std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj) {
   return order;
 }
 
+std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf) {
+  Dissector d(adj, leaf);
+  std::vector<int> all(n);
+  for (int i = 0; i < n; ++i) all[i] = i;
+  d.run(all, 0);
+  return d.parts;
+}
+
 void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hipStream_t s) {
   llt_plan_free(plan);
   plan.T = T;
   plan.lda = lda;
-  // symbolic factorization at tile level: column k's rows fill every pair
+  // symbolic factorization at tile level
   std::vector<int> rows;
   for (int k = 0; k < T; ++k) {
     P[(long)k * T + k] = 1;
@@ -98,50 +188,102 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
     for (size_t a = 0; a < rows.size(); ++a)
       for (size_t b = 0; b <= a; ++b) P[(long)rows[a] * T + rows[b]] = 1;
   }
-  std::vector<int> trsm_rows, bs_cols;
-  std::vector<int2> pairs, tiles;
-  plan.h_trsm_off.assign(1, 0);
+  // tile elimination tree and heights
+  std::vector<int> parent(T, -1), height(T, 0);
+  for (int k = 0; k < T; ++k)
+    for (int i = k + 1; i < T; ++i)
+      if (P[(long)i * T + k]) { parent[k] = i; break; }
+  for (int k = 0; k < T; ++k)
+    if (parent[k] >= 0) height[parent[k]] = std::max(height[parent[k]], height[k] + 1);
+  int nlev = 0;
+  for (int k = 0; k < T; ++k) nlev = std::max(nlev, height[k] + 1);
+  std::vector<std::vector<int>> levcols(nlev);
+  for (int k = 0; k < T; ++k) levcols[height[k]].push_back(k);
+  plan.nlev = nlev;
+
+  std::vector<int2> panel, targets, tiles;
+  std::vector<int> kstart{0}, ks, bcols, gstart{0}, grows;
+  plan.h_panel_off.assign(1, 0);
   plan.h_upd_off.assign(1, 0);
   plan.h_bs_off.assign(1, 0);
   plan.h_upd_flops.clear();
+  plan.total_upd_flops = 0.0;
+  plan.total_upd_tiles = 0;
   const double t3 = 64.0 * 64.0 * 64.0;
-  for (int k = 0; k < T; ++k) {
-    rows.clear();
-    for (int i = k + 1; i < T; ++i)
-      if (P[(long)i * T + k]) rows.push_back(i);
-    double fl = 0.0;
-    for (size_t a = 0; a < rows.size(); ++a) {
-      trsm_rows.push_back(rows[a]);
-      for (size_t b = 0; b <= a; ++b) {
-        pairs.push_back(make_int2(rows[a], rows[b]));
-        // useful flops: off-diagonal tile 2*64^3, diagonal tile lower incl. diagonal 64*65*64
-        fl += (a == b) ? 64.0 * 65.0 * 64.0 : 2.0 * t3;
-      }
+  std::vector<int> tgt_id((size_t)T * T, -1);
+  for (int l = 0; l < nlev; ++l) {
+    // panel tasks
+    for (int k : levcols[l]) {
+      panel.push_back(make_int2(k, k));
+      for (int i = k + 1; i < T; ++i)
+        if (P[(long)i * T + k]) panel.push_back(make_int2(i, k));
     }
-    plan.h_trsm_off.push_back((int)trsm_rows.size());
-    plan.h_upd_off.push_back((long)pairs.size());
+    plan.h_panel_off.push_back((int)panel.size());
+    // update targets of this level: (i,j), j <= i, both in some column k of the level
+    std::vector<int2> lt;
+    std::vector<std::vector<int>> lks;
+    double fl = 0.0;
+    for (int k : levcols[l]) {
+      rows.clear();
+      for (int i = k + 1; i < T; ++i)
+        if (P[(long)i * T + k]) rows.push_back(i);
+      for (size_t a = 0; a < rows.size(); ++a)
+        for (size_t b = 0; b <= a; ++b) {
+          const long key = (long)rows[a] * T + rows[b];
+          int id = tgt_id[key];
+          if (id < 0) {
+            id = (int)lt.size();
+            tgt_id[key] = id;
+            lt.push_back(make_int2(rows[a], rows[b]));
+            lks.emplace_back();
+          }
+          lks[id].push_back(k);
+          fl += (a == b) ? 64.0 * 65.0 * 64.0 : 2.0 * t3;
+          plan.total_upd_tiles++;
+        }
+    }
+    for (size_t t = 0; t < lt.size(); ++t) {
+      tgt_id[(long)lt[t].x * T + lt[t].y] = -1;
+      targets.push_back(lt[t]);
+      ks.insert(ks.end(), lks[t].begin(), lks[t].end());
+      kstart.push_back((int)ks.size());
+    }
+    plan.h_upd_off.push_back((int)targets.size());
     plan.h_upd_flops.push_back(fl);
     plan.total_upd_flops += fl;
-    for (int j = 0; j < k; ++j)
-      if (P[(long)k * T + j]) bs_cols.push_back(j);
-    plan.h_bs_off.push_back((int)bs_cols.size());
-    for (int j = 0; j <= k; ++j)
-      if (P[(long)k * T + j]) tiles.push_back(make_int2(k, j));
   }
-  plan.total_upd_tiles = (long)pairs.size();
+  // backward solve: levels from the root down; each column gathers from its
+  // tile rows below the diagonal (ancestors, solved in earlier launches)
+  for (int l = nlev - 1; l >= 0; --l) {
+    for (int k : levcols[l]) {
+      bcols.push_back(k);
+      for (int i = k + 1; i < T; ++i)
+        if (P[(long)i * T + k]) grows.push_back(i);
+      gstart.push_back((int)grows.size());
+    }
+    plan.h_bs_off.push_back((int)bcols.size());
+  }
+  for (int i = 0; i < T; ++i)
+    for (int j = 0; j <= i; ++j)
+      if (P[(long)i * T + j]) tiles.push_back(make_int2(i, j));
   plan.n_tiles = (long)tiles.size();
-  plan.trsm_rows = upload(trsm_rows, s);
-  plan.upd_pairs = upload(pairs, s);
-  plan.bs_cols = upload(bs_cols, s);
+  plan.panel = upload(panel, s);
+  plan.upd_targets = upload(targets, s);
+  plan.upd_kstart = upload(kstart, s);
+  plan.upd_ks = upload(ks, s);
+  plan.bs_cols = upload(bcols, s);
+  plan.bs_gstart = upload(gstart, s);
+  plan.bs_grows = upload(grows, s);
   plan.tiles = upload(tiles, s);
+  check(hipMalloc(&plan.ldiag, (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
   check(hipStreamSynchronize(s), "plan sync");
 }
 
 void llt_plan_free(LltPlan &plan) {
-  if (plan.trsm_rows) (void)hipFree(plan.trsm_rows);
-  if (plan.upd_pairs) (void)hipFree(plan.upd_pairs);
-  if (plan.bs_cols) (void)hipFree(plan.bs_cols);
-  if (plan.tiles) (void)hipFree(plan.tiles);
+  for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
+                  (void *)plan.upd_ks, (void *)plan.bs_cols, (void *)plan.bs_gstart,
+                  (void *)plan.bs_grows, (void *)plan.tiles, (void *)plan.ldiag})
+    if (p) (void)hipFree(p);
   plan = LltPlan{};
 }
 

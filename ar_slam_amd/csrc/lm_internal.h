@@ -6,8 +6,9 @@
 //   [0,3)                camera  f, l1, l2
 //   [3 + 6c, 9 + 6c)     capture c inv_pose  t_c, w_c
 //   [3 + 6Nc + 6t, ...)  tag t pose  t_t, w_t
-// Reduced (f-side) index: tag t -> 6t + a, camera -> 6Nt + b (camera last, so
-// the dense system is an arrow-head: banded tag block + one border).
+// Reduced (f-side) rows: tag t -> tag_row[t] + a, camera -> cam_row + b, in an
+// ordering chosen on the host (llt_plan.cpp); the camera comes last, so the
+// reduced matrix is an arrow-head (sparse tag block + one dense border).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -36,10 +37,11 @@ enum PartIdx {
 struct DevProblem {
   int nc, nt, nb;
   long n;              // number of parameter slots 3 + 6nc + 6nt
-  long nF;             // reduced size 6nt + 3
-  long N;              // padded reduced size (multiple of kTile, > nF: row nF holds the rhs)
+  long nR;             // rows of the reduced system (tags + camera + alignment padding); row nR = rhs
+  long N;              // padded matrix size (multiple of kTile, > nR)
   long lda;            // leading dimension of S
   int max_obs_per_cap;
+  int cam_row;               // first reduced row of the camera block, -1 if the camera is not free
   const int *cap_start;      // [nc+1]  CSR of observations by capture
   const int *obs_tag;        // [nb]
   const int *obs_lblk;       // [nb]    local f-block (1..) of the observation's tag in its capture
@@ -50,31 +52,30 @@ struct DevProblem {
   const int *tag_start;      // [nt+1]  CSR of observations by tag (capture-major order inside)
   const int *tag_obs;        // [nb]
   const double *corners;     // [nb*8]
-  const int *tag_pos;        // [nt]    position of tag t in the reduced ordering (F index 6*pos)
-  const int *pos_tag;        // [nt]    inverse
+  const int *tag_row;        // [nt]    first reduced row of tag t (6 rows), -1 if not free
+  const int *row_slot;       // [nR]    parameter slot of a reduced row, -1 for padding rows
 };
 
-// reduced index of parameter j (0..5) of tag t, and the slot of reduced index i
-__device__ inline long fidx_tag(const DevProblem &P, int t, int j) { return 6L * P.tag_pos[t] + j; }
-__device__ inline long fslot(const DevProblem &P, long i) {
-  return i < 6L * P.nt ? 3 + 6L * P.nc + 6L * P.pos_tag[i / 6] + i % 6 : i - 6L * P.nt;
-}
-
-// Tile plan of the reduced-system Cholesky (see dense_llt.hip).  Per step k:
-// the tile rows i > k of column k (TRSM), the (i,j) pairs it updates, and the
-// tile columns of row k (backward solve).  Device arrays, host offsets.
+// Tile plan of the reduced-system Cholesky (dense_llt.hip), level-scheduled
+// over the tile elimination tree.  Device arrays, host per-level offsets.
 struct LltPlan {
   int T = 0;
   long lda = 0;
-  int *trsm_rows = nullptr;
-  int2 *upd_pairs = nullptr;
-  int *bs_cols = nullptr;
-  int2 *tiles = nullptr;     // every tile of the factor (zeroed before assembly)
+  int nlev = 0;
+  int2 *panel = nullptr;        // (i,k) factor tasks; i == k is the diagonal tile
+  int2 *upd_targets = nullptr;  // (i,j) tiles updated by a level
+  int *upd_kstart = nullptr;    // CSR over targets of the contributing columns k
+  int *upd_ks = nullptr;
+  int *bs_cols = nullptr;       // backward-solve columns, root level first
+  int *bs_gstart = nullptr;     // CSR over bs_cols of the tile rows gathered
+  int *bs_grows = nullptr;
+  int2 *tiles = nullptr;        // every tile of the factor (zeroed before assembly)
   long n_tiles = 0;
-  std::vector<int> h_trsm_off;
-  std::vector<long> h_upd_off;
-  std::vector<int> h_bs_off;
-  std::vector<double> h_upd_flops;   // useful flops of each step's update
+  double *ldiag = nullptr;      // T x 64 x 64 diagonal factors L_kk (row-major, ld 64)
+  std::vector<int> h_panel_off;     // [nlev+1]
+  std::vector<int> h_upd_off;       // [nlev+1]
+  std::vector<int> h_bs_off;        // [nlev+1], in backward (root-first) order
+  std::vector<double> h_upd_flops;  // useful flops of each level's update
   double total_upd_flops = 0.0;
   long total_upd_tiles = 0;
 };
@@ -84,6 +85,8 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &patter
 void llt_plan_free(LltPlan &plan);
 // Reverse Cuthill-McKee order of an undirected graph (adjacency lists).
 std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj);
+// Nested-dissection parts (leaves and separators) in elimination order.
+std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf);
 
 // ---- lm_kernels.hip ----
 void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
@@ -123,13 +126,15 @@ struct LaunchTiming {
 
 // ---- dense_llt.hip ----
 // Cholesky of the lower triangle of S (row-major, lda) over the plan's tiles,
-// in place.  Row nF carries the right-hand side, so on exit row nF =
+// in place.  Row nR carries the right-hand side, so on exit row nR =
 // (L^{-1} b)^T.  *flag is set non-zero if a pivot is not positive.  Then
-// y = L^{-T} z into yF[0..nF).
+// y = L^{-T} z into yF[0..nR).
 void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
                       LaunchTiming *timing = nullptr);
-void launch_dense_back_solve(const LltPlan &P, const double *S, long nF, double *z, double *yF,
+void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s);
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s);
+// copy the diagonal factors L_kk into S (tests only: S then holds the whole factor)
+void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s);
 
 }  // namespace arslam

@@ -437,8 +437,12 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
 
   for (int q = lane; q < k; q += kWave) lblk[q] = P.obs_lblk[o0 + q];
   for (int p = lane; p < m; p += kWave) {
-    if (p == 0) gidx[p] = 6L * P.nt;
-    else gidx[p] = fidx_tag(P, P.blk_tag[b0 + (p - 1) / 6], (p - 1) % 6);
+    if (p == 0) {
+      gidx[p] = P.cam_row;   // f; -1 when the camera is held constant
+    } else {
+      const int tr = P.tag_row[P.blk_tag[b0 + (p - 1) / 6]];
+      gidx[p] = tr < 0 ? -1 : tr + (p - 1) % 6;
+    }
   }
   fill_rows(P, x, scale, c, o0, nrows, rows);
   __syncthreads();
@@ -490,9 +494,10 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   }
   __syncthreads();
   const long lda = P.lda;
-  double *rhs = S + P.nF * lda;
+  double *rhs = S + P.nR * lda;
   // reduced rhs: F'r - W' Ui E'r
   for (int p = lane; p < m; p += kWave) {
+    if (gidx[p] < 0) continue;
     double s = 0.0;
 #pragma unroll
     for (int a = 0; a < 6; ++a) s += W[a * m + p] * UiE[a];
@@ -517,21 +522,25 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
 #pragma unroll
     for (int a = 0; a < 6; ++a) wz += W[a * m + p] * Z[a * m + q];
     const long gi = gidx[p], gj = gidx[q];
+    if (gi < 0 || gj < 0) continue;
     const long hi = gi > gj ? gi : gj, lo = gi > gj ? gj : gi;
     atomicAdd(S + hi * lda + lo, ff - wz);
   }
 }
 
-// S[i][i] += D_f^2 for the reduced (tag + camera) index; padding rows become
-// identity rows; the rhs row gets a pivot large enough to stay positive.
+// S[i][i] += D_f^2 for the reduced (tag + camera) rows; alignment padding and
+// the rows past the rhs become identity rows; the rhs row gets a pivot large
+// enough to stay positive (its factor row is L^{-1} b, its pivot unused).
 __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, double radius,
                                double *__restrict__ S) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.N) return;
   double *d = S + i * P.lda + i;
-  if (i < P.nF) {
-    *d += lm_d2(diag, fslot(P, i), radius);
-  } else if (i == P.nF) {
+  if (i < P.nR) {
+    const int slot = P.row_slot[i];
+    if (slot >= 0) *d += lm_d2(diag, slot, radius);
+    else *d = 1.0;
+  } else if (i == P.nR) {
     *d = 1e300;
   } else {
     *d = 1.0;
@@ -568,13 +577,15 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   double *yc = v + 8;                             // 8
   fill_rows(P, x, scale, c, o0, nrows, rows);
   __syncthreads();
-  const double yf = yF[6L * P.nt];
+  const double yf = P.cam_row >= 0 ? yF[P.cam_row] : 0.0;
   for (int row = lane; row < nrows; row += kWave) {
     const double *rr = rows + (long)row * kRowStride;
-    const long tb = fidx_tag(P, P.obs_tag[o0 + (row >> 3)], 0);
+    const int tr = P.tag_row[P.obs_tag[o0 + (row >> 3)]];
     double q = rr[0] * yf;
+    if (tr >= 0) {
 #pragma unroll
-    for (int j = 0; j < 6; ++j) q += rr[7 + j] * yF[tb + j];
+      for (int j = 0; j < 6; ++j) q += rr[7 + j] * yF[tr + j];
+    }
     qv[row] = q;
   }
   __syncthreads();
@@ -647,8 +658,8 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
   __shared__ double red[2][256];
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0;
-  if (i < P.nF) {
-    const long slot = fslot(P, i);
+  const long slot = i < P.nR ? P.row_slot[i] : -1;
+  if (slot >= 0) {
     const double yv = yF[i];
     const double xo = x[slot];
     const double xn = xo + (-yv * scale[slot]);
@@ -875,8 +886,8 @@ void launch_backsub(const DevProblem &P, const double *x, const double *scale, c
 
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,
                      double *xc, double *fparts, hipStream_t s) {
-  if (P.nF == 0) return;
-  hipLaunchKernelGGL(k_update_f, dim3((unsigned)((P.nF + 255) / 256)), dim3(256), 0, s, P, x, scale, yF,
+  if (P.nR == 0) return;
+  hipLaunchKernelGGL(k_update_f, dim3((unsigned)((P.nR + 255) / 256)), dim3(256), 0, s, P, x, scale, yF,
                      xc, fparts);
 }
 

@@ -119,7 +119,7 @@ struct arslam_lm {
   bool loaded = false;
   arslam_soa_problem soa{};
   int nc = 0, nt = 0, nb = 0;
-  long n = 0, nF = 0, N = 0;
+  long n = 0, nR = 0, N = 0;
   bool has_f = false;
   std::vector<unsigned char> slot_free;
   std::vector<double> x0;   // initial slots
@@ -131,7 +131,7 @@ struct arslam_lm {
   DevBuf<unsigned char> d_obs_active, d_slot_free;
   DevBuf<double> d_corners, d_x0, d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_norms, d_S, d_z, d_yF;
-  DevBuf<int> d_flag, d_tag_pos, d_pos_tag;
+  DevBuf<int> d_flag, d_tag_row, d_row_slot;
   arslam::LltPlan plan;
   double *x = nullptr, *xc = nullptr;
   int n_fparts = 0;
@@ -144,7 +144,7 @@ struct arslam_lm {
 
   void timing_begin() {
     if (!opt.kernel_timing || !has_f) return;
-    const int need = plan.T + 1;
+    const int need = plan.nlev + 1;
     if ((int)upd_events.size() < 2 * need) {
       for (auto e : upd_events) (void)hipEventDestroy(e);
       upd_events.assign(2 * need, nullptr);
@@ -221,7 +221,6 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   nt = p->n_tag;
   nb = p->n_obs;
   n = 3 + 6L * nc + 6L * nt;
-  nF = 6L * nt + 3;
 
   // capture-major observation order (stable)
   std::vector<int> cap_start(nc + 1, 0);
@@ -289,11 +288,9 @@ void arslam_lm::load(const arslam_soa_problem *p) {
     const bool f = cap_start[c + 1] > cap_start[c] && !(p->cap_const && p->cap_const[c]);
     for (int j = 0; j < 6; ++j) slot_free[3 + 6L * c + j] = f;
   }
-  has_f = cam_free;
   for (int t = 0; t < nt; ++t) {
     const bool f = tag_deg[t] > 0 && !(p->tag_const && p->tag_const[t]);
     for (int j = 0; j < 6; ++j) slot_free[3 + 6L * nc + 6L * t + j] = f;
-    has_f = has_f || f;
   }
   std::vector<unsigned char> obs_active(nb);
   for (int q = 0; q < nb; ++q) {
@@ -306,15 +303,22 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   if (nt) std::memcpy(x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
 
   // ---- reduced-system ordering and tile plan ----
-  std::vector<int> tag_pos(std::max(nt, 1)), pos_tag(std::max(nt, 1));
+  // Rows exist only for free tags and a free camera (constant / unused blocks
+  // are not parameters).  Tags are ordered natural, RCM or by nested
+  // dissection; with ND every part starts on a tile boundary so the tile
+  // elimination tree follows the dissection tree.
+  std::vector<int> tag_row(std::max(nt, 1), -1);
+  std::vector<int> row_slot;
+  int cam_row = -1;
   const bool sparse = opt.cholesky_skip_zero_tiles != 0;
+  const int ordering = opt.reduced_ordering;
   {
-    std::vector<int> order(nt);
-    for (int t = 0; t < nt; ++t) order[t] = t;
-    if (sparse && nt > 1) {
-      std::vector<std::vector<int>> adj(nt);
+    std::vector<char> tfree(nt, 0);
+    for (int t = 0; t < nt; ++t) tfree[t] = slot_free[3 + 6L * nc + 6L * t];
+    std::vector<std::vector<int>> adj(nt);
+    if (ordering != 0 && nt > 1) {
       if (nranks > 1) {
-        fail_if(nt > 16384, ARSLAM_E_UNSUPPORTED, "sparse multi-GPU plan limited to 16384 tags");
+        fail_if(nt > 16384, ARSLAM_E_UNSUPPORTED, "multi-GPU reduced ordering limited to 16384 tags");
         std::vector<uint8_t> bm((size_t)nt * nt, 0);
         for (int c = 0; c < nc; ++c)
           for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a)
@@ -328,52 +332,85 @@ void arslam_lm::load(const arslam_soa_problem *p) {
         HIP_CHECK(hipStreamSynchronize(stream));
         for (int a = 0; a < nt; ++a)
           for (int b = 0; b < nt; ++b)
-            if (bm[(size_t)a * nt + b]) adj[a].push_back(b);
+            if (bm[(size_t)a * nt + b] && tfree[a] && tfree[b]) adj[a].push_back(b);
       } else {
         for (int c = 0; c < nc; ++c)
           for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a)
             for (int b = cap_blk_start[c]; b < cap_blk_start[c + 1]; ++b)
-              if (a != b) adj[blk_tag[a]].push_back(blk_tag[b]);
+              if (a != b && tfree[blk_tag[a]] && tfree[blk_tag[b]]) adj[blk_tag[a]].push_back(blk_tag[b]);
         for (auto &v : adj) {
           std::sort(v.begin(), v.end());
           v.erase(std::unique(v.begin(), v.end()), v.end());
         }
       }
-      order = arslam::rcm_order(nt, adj);
     }
-    for (int p = 0; p < nt; ++p) {
-      pos_tag[p] = order[p];
-      tag_pos[order[p]] = p;
+    std::vector<std::vector<int>> parts;
+    if (ordering == 2 && nt > 1) {
+      parts = arslam::nd_parts(nt, adj, 10);
+    } else {
+      std::vector<int> order;
+      if (ordering == 1 && nt > 1) order = arslam::rcm_order(nt, adj);
+      else for (int t = 0; t < nt; ++t) order.push_back(t);
+      parts.push_back(order);
     }
+    long row = 0;
+    for (auto &part : parts) {
+      bool any = false;
+      for (int t : part) any = any || tfree[t];
+      if (!any) continue;
+      if (ordering == 2) row = round_up(row, arslam::kTile);
+      for (int t : part) {
+        if (!tfree[t]) continue;
+        tag_row[t] = (int)row;
+        for (int j = 0; j < 6; ++j) row_slot.push_back(3 + 6 * nc + 6 * t + j);
+        row += 6;
+      }
+      while ((long)row_slot.size() < row) row_slot.push_back(-1);
+    }
+    // alignment padding rows inside the tag block
+    {
+      std::vector<int> rs(row, -1);
+      for (int t = 0; t < nt; ++t)
+        if (tag_row[t] >= 0)
+          for (int j = 0; j < 6; ++j) rs[tag_row[t] + j] = 3 + 6 * nc + 6 * t + j;
+      row_slot = rs;
+    }
+    if (slot_free[0]) {
+      cam_row = (int)row;
+      for (int j = 0; j < 3; ++j) row_slot.push_back(j);
+      row += 3;
+    }
+    nR = row;
   }
+  has_f = nR > 0;
   if (has_f) {
-    N = round_up(nF + 1, arslam::kTile);
+    N = round_up(nR + 1, arslam::kTile);
     const int T = (int)(N / arslam::kTile);
     std::vector<uint8_t> pattern((size_t)T * T, 0);
     if (!sparse) {
       for (int i = 0; i < T; ++i)
         for (int j = 0; j <= i; ++j) pattern[(size_t)i * T + j] = 1;
     } else {
-      auto mark_set = [&](std::vector<int> &ts) {
+      std::vector<int> ts;
+      for (int c = 0; c < nc; ++c) {
+        ts.clear();
+        if (cam_row >= 0) {
+          ts.push_back(cam_row / arslam::kTile);
+          ts.push_back((cam_row + 2) / arslam::kTile);
+        }
+        for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a) {
+          const int r0 = tag_row[blk_tag[a]];
+          if (r0 < 0) continue;
+          ts.push_back(r0 / arslam::kTile);
+          ts.push_back((r0 + 5) / arslam::kTile);
+        }
         std::sort(ts.begin(), ts.end());
         ts.erase(std::unique(ts.begin(), ts.end()), ts.end());
         for (size_t a = 0; a < ts.size(); ++a)
           for (size_t b = 0; b <= a; ++b) pattern[(size_t)ts[a] * T + ts[b]] = 1;
-      };
-      std::vector<int> ts;
-      const int cam0 = (int)((6L * nt) / arslam::kTile), cam1 = (int)((6L * nt + 2) / arslam::kTile);
-      for (int c = 0; c < nc; ++c) {
-        ts.assign({cam0, cam1});
-        for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a) {
-          const long f0 = 6L * tag_pos[blk_tag[a]];
-          ts.push_back((int)(f0 / arslam::kTile));
-          ts.push_back((int)((f0 + 5) / arslam::kTile));
-        }
-        mark_set(ts);
       }
-      const int rhs = (int)(nF / arslam::kTile);
+      const int rhs = (int)(nR / arslam::kTile);
       for (int j = 0; j <= rhs; ++j) pattern[(size_t)rhs * T + j] = 1;
-      for (int j = 0; j <= cam1; ++j) pattern[(size_t)cam1 * T + j] = 1;   // camera border (camera free)
       if (nranks > 1) {
         DevBuf<uint8_t> tmp;
         tmp.alloc(pattern.size());
@@ -384,6 +421,9 @@ void arslam_lm::load(const arslam_soa_problem *p) {
       }
     }
     arslam::llt_plan_build(plan, T, N, pattern, stream);
+  } else {
+    N = 0;
+    arslam::llt_plan_free(plan);
   }
 
   // ---- device upload ----
@@ -402,34 +442,32 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_g.alloc(n); d_colnorm.alloc(n); d_scale.alloc(n); d_diag.alloc(n);
   d_obs_tg.alloc(std::max(12L * nb, 1L));
   d_parts.alloc((size_t)arslam::NPART * std::max(nc, 1));
-  n_fparts = (int)((nF + 255) / 256);
+  n_fparts = (int)((std::max(nR, 1L) + 255) / 256);
   d_fparts.alloc(2L * std::max(n_fparts, 1));
   d_red.alloc(16);
   d_norms.alloc(8);
   d_flag.alloc(1);
-  d_tag_pos.alloc(tag_pos.size()); d_tag_pos.upload(tag_pos.data(), tag_pos.size(), stream);
-  d_pos_tag.alloc(pos_tag.size()); d_pos_tag.upload(pos_tag.data(), pos_tag.size(), stream);
+  d_tag_row.alloc(tag_row.size()); d_tag_row.upload(tag_row.data(), tag_row.size(), stream);
+  d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
   if (has_f) {
     d_S.alloc((size_t)N * N);
     HIP_CHECK(hipMemsetAsync(d_S.p, 0, (size_t)N * N * sizeof(double), stream));
     d_z.alloc(N);
     d_yF.alloc(N);
   } else {
-    N = 0;
     d_S.release();
     d_z.release();
-    d_yF.alloc(nF);
-    HIP_CHECK(hipMemsetAsync(d_yF.p, 0, nF * sizeof(double), stream));
+    d_yF.alloc(1);
   }
   HIP_CHECK(hipMemsetAsync(d_parts.p, 0, d_parts.n * sizeof(double), stream));
 
-  P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nF = nF; P.N = N; P.lda = N;
+  P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nR = nR; P.N = N; P.lda = N; P.cam_row = cam_row;
   P.max_obs_per_cap = std::max(maxk, 1);
   P.cap_start = d_cap_start.p; P.obs_tag = d_obs_tag.p; P.obs_lblk = d_obs_lblk.p;
   P.cap_blk_start = d_cap_blk_start.p; P.blk_tag = d_blk_tag.p;
   P.obs_active = d_obs_active.p; P.slot_free = d_slot_free.p;
   P.tag_start = d_tag_start.p; P.tag_obs = d_tag_obs.p; P.corners = d_corners.p;
-  P.tag_pos = d_tag_pos.p; P.pos_tag = d_pos_tag.p;
+  P.tag_row = d_tag_row.p; P.row_slot = d_row_slot.p;
   HIP_CHECK(hipStreamSynchronize(stream));
   loaded = true;
 }
@@ -509,7 +547,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   dom_ms = dom_flops = 0.0;
   dom_launches = 0;
   s->n_obs = nb;
-  s->n_reduced = has_f ? (int)nF : 0;
+  s->n_reduced = has_f ? (int)nR : 0;
   x = d_xa.p;
   xc = d_xb.p;
   HIP_CHECK(hipMemcpyAsync(x, d_x0.p, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
@@ -595,10 +633,11 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       arslam::launch_dense_llt(plan, d_S.p, d_flag.p, stream, opt.kernel_timing ? &upd_timing : nullptr);
       timers[PH_CHOL].stop(stream);
       timers[PH_SOLVE].start(stream);
-      arslam::launch_dense_back_solve(plan, d_S.p, nF, d_z.p, d_yF.p, d_flag.p, stream);
+      arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
       timers[PH_SOLVE].stop(stream);
     }
     timers[PH_BACK].start(stream);
+    HIP_CHECK(hipMemcpyAsync(xc, x, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
     arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream);
     arslam::launch_update_f(P, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
     timers[PH_BACK].stop(stream);
@@ -706,6 +745,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->dominant_flops = dom_flops;
   s->n_dominant_launches = dom_launches;
   s->n_factor_tiles = plan.n_tiles;
+  s->n_levels = plan.nlev;
   s->n_update_tiles = plan.total_upd_tiles;
   s->factor_update_flops = plan.total_upd_flops;
 }
@@ -759,7 +799,8 @@ int arslam_lm_options_init(arslam_lm_options *o) {
   o->minimizer_progress_to_stdout = 0;
   o->update_state_every_iteration = 0;
   o->device = -1;
-  o->cholesky_skip_zero_tiles = 0;
+  o->cholesky_skip_zero_tiles = 1;
+  o->reduced_ordering = 2;
   o->kernel_timing = 0;
   return ARSLAM_OK;
 }

@@ -69,7 +69,7 @@ class Options(C.Structure):
                 ("minimizer_progress_to_stdout", C.c_int),
                 ("update_state_every_iteration", C.c_int),
                 ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int),
-                ("kernel_timing", C.c_int)]
+                ("reduced_ordering", C.c_int), ("kernel_timing", C.c_int)]
 
 
 class Iteration(C.Structure):
@@ -96,7 +96,7 @@ class Summary(C.Structure):
                 ("t_backsub_ms", C.c_double), ("t_cost_ms", C.c_double),
                 ("t_dominant_ms", C.c_double), ("dominant_flops", C.c_double),
                 ("n_dominant_launches", C.c_long),
-                ("n_factor_tiles", C.c_long), ("n_update_tiles", C.c_long),
+                ("n_factor_tiles", C.c_long), ("n_levels", C.c_int), ("n_update_tiles", C.c_long),
                 ("factor_update_flops", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 

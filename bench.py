@@ -86,7 +86,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--skip-zero-tiles", type=int, default=0)
+    ap.add_argument("--skip-zero-tiles", type=int, default=1)
+    ap.add_argument("--ordering", type=int, default=2, help="0 natural, 1 RCM, 2 nested dissection")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,7 +111,8 @@ def main():
         comm = (rank, world, obj[0])
     rp = lm.ResidentProblem(**part, comm=comm, device=local_rank,
                             kernel_timing=0 if args.no_kernel_timing else 1,
-                            cholesky_skip_zero_tiles=args.skip_zero_tiles)
+                            cholesky_skip_zero_tiles=args.skip_zero_tiles,
+                            reduced_ordering=args.ordering)
 
     def barrier():
         if world > 1:
@@ -171,6 +173,10 @@ def main():
             "final_rms_px": last["final_rms_px"],
             "termination": f"{last['termination']} ({last['rule']})",
             "lm_iterations_per_solve": last["num_linear_solves"],
+            "reduced_system": {"rows": int(last["n_reduced"]), "factor_tiles": int(last["n_factor_tiles"]),
+                               "etree_levels": int(last["n_levels"]),
+                               "ordering": ["natural", "RCM", "nested dissection"][args.ordering],
+                               "skip_zero_tiles": bool(args.skip_zero_tiles)},
             "phase_ms_per_solve": {k: last[f"t_{k}_ms"] for k in
                                    ("linearize", "schur", "cholesky", "solve", "backsub", "cost")},
             "roofline": roofline,

@@ -83,6 +83,8 @@ typedef struct {
   int update_state_every_iteration;  /* write improving iterates back */
   int device;                        /* HIP device ordinal, -1 = current */
   int cholesky_skip_zero_tiles;      /* 1: skip structurally-zero tiles of the reduced system */
+  int reduced_ordering;              /* tags in the reduced system: 0 natural, 1 reverse
+                                        Cuthill-McKee, 2 nested dissection (default) */
   int kernel_timing;                 /* 1: HIP events around every launch of the dominant kernel */
 } arslam_lm_options;
 
@@ -115,6 +117,7 @@ typedef struct {
   long n_dominant_launches;
   /* reduced-system tile plan (per factorization) */
   long n_factor_tiles;          /* 64x64 tiles of the factor that exist */
+  int n_levels;                 /* levels of the tile elimination tree (launch pairs) */
   long n_update_tiles;          /* tile updates (MFMA work items) */
   double factor_update_flops;   /* useful flops of the trailing updates */
   int n_iters;                  /* entries in iters[], iteration 0 included */

@@ -158,24 +158,29 @@ def test_resident_problem_resolves_identically(lm):
     np.testing.assert_allclose(rp.cap, c1, rtol=1e-9, atol=1e-12)
 
 
-@pytest.mark.parametrize("name", ["small", "medium", "cfg2"])
-def test_sparse_tile_plan_matches_oracle(lm, oracle, name):
-    """RCM-ordered reduced system with structurally-zero tiles skipped: same LM."""
+@pytest.mark.parametrize("ordering", [0, 1, 2])
+@pytest.mark.parametrize("skip", [0, 1])
+@pytest.mark.parametrize("name", ["small", "cfg2"])
+def test_reduced_orderings_match_oracle(lm, oracle, name, skip, ordering):
+    """Natural / RCM / nested-dissection reduced orderings, dense or zero-tile-skipping plans."""
     g = synth.config_graph(name)
     ref = oracle.solve_graph(g)
-    ours = lm.solve_graph(g, cholesky_skip_zero_tiles=1)
+    ours = lm.solve_graph(g, cholesky_skip_zero_tiles=skip, reduced_ordering=ordering)
     _compare_solves(g, ours, ref)
-    if name == "cfg2":
+    if name == "cfg2" and skip:
         s = ours[3]
-        T = (6 * g.n_tag + 3 + 1 + 63) // 64
+        T = (s["n_reduced"] + 1 + 63) // 64
         assert s["n_factor_tiles"] < T * (T + 1) // 2
+    if ordering == 2 and skip and name == "cfg2":
+        # nested dissection: the tile elimination tree is much shallower than the chain
+        assert ours[3]["n_levels"] < (ours[3]["n_reduced"] + 64) // 64 // 2
 
 
 def test_sparse_plan_equals_dense_plan_on_same_order(lm):
     """Skipping zero tiles changes nothing but the work: the trace matches the dense plan."""
     g = synth.config_graph("cfg2")
-    dense = lm.solve_graph(g)
-    sparse = lm.solve_graph(g, cholesky_skip_zero_tiles=1)
+    dense = lm.solve_graph(g, cholesky_skip_zero_tiles=0, reduced_ordering=1)
+    sparse = lm.solve_graph(g, cholesky_skip_zero_tiles=1, reduced_ordering=1)
     cd = [it["cost"] for it in dense[3]["iterations"]]
     cs = [it["cost"] for it in sparse[3]["iterations"]]
     assert len(cd) == len(cs)

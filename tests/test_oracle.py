@@ -1,0 +1,210 @@
+"""CPU tests of the oracle (the parity checker), pinned against independent references.
+
+The reference's only test (ar_slam/test/util_test.cpp) checks a filename
+helper, so nothing in the reference pins the LM path.
+The oracle is therefore pinned by:
+  * torch fp64 autograd of the reference's residual (the analogue of Ceres'
+    Jet autodiff) and central differences -> analytic Jacobian;
+  * scipy.optimize.least_squares -> converged cost;
+  * noise-free graphs -> the truth, modulo the 6-DoF gauge;
+  * the full normal-equation solve -> the Schur-complement step;
+  * committed golden fixtures (tests/golden, made by make_golden.py) -> regressions.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ar_slam_amd import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+EPS = np.finfo(float).eps
+
+
+def _torch_residual():
+    torch = pytest.importorskip("torch")
+
+    def rot(w, x):
+        th2 = (w * w).sum()
+        if th2.item() > EPS:   # ceres::AngleAxisRotatePoint branch
+            th = torch.sqrt(th2)
+            c, s = torch.cos(th), torch.sin(th)
+            u = w * (1.0 / th)
+            cr = torch.stack([u[1] * x[2] - u[2] * x[1], u[2] * x[0] - u[0] * x[2], u[0] * x[1] - u[1] * x[0]])
+            return x * c + cr * s + u * ((u * x).sum() * (1.0 - c))
+        cr = torch.stack([w[1] * x[2] - w[2] * x[1], w[2] * x[0] - w[0] * x[2], w[0] * x[1] - w[1] * x[0]])
+        return x + cr
+
+    def res(p, corners):
+        cam, cap, tag = p[:3], p[3:9], p[9:15]
+        out = []
+        for i, (dx, dy) in enumerate(synth.ARUCO_DIRECTIONS):
+            c = torch.tensor([0.5 * synth.ARUCO_SIZE * dx, 0.5 * synth.ARUCO_SIZE * dy, 0.0], dtype=torch.float64)
+            a = rot(tag[3:], c) + tag[:3]
+            b = a + cap[:3]
+            q = rot(cap[3:], b)
+            out += [cam[0] * (q[0] / q[2]) - corners[2 * i], cam[0] * (q[1] / q[2]) - corners[2 * i + 1]]
+        return torch.stack(out)
+    return torch, res
+
+
+def test_residual_matches_numpy_model(oracle):
+    g = synth.config_graph("small")
+    pred = synth.project_corners(g.camera, g.cap[g.obs_cap], g.tag[g.obs_tag]) - g.corners
+    for b in range(0, g.n_obs, 7):
+        r = oracle.residual(g.camera, g.cap[g.obs_cap[b]], g.tag[g.obs_tag[b]], g.corners[b])
+        np.testing.assert_allclose(r, pred[b], rtol=1e-12, atol=1e-9)
+
+
+def test_jacobian_vs_torch_autograd(oracle):
+    """Analytic Jacobian == autodiff of the reference formula (Jet analogue), 1e-12."""
+    torch, res = _torch_residual()
+    kat = np.load(os.path.join(GOLDEN, "jacobian_kat.npz"))
+    for i in range(kat["cam"].shape[0]):
+        wn = np.linalg.norm(kat["cap"][i, 3:])
+        if 1e-9 < wn < 1e-6:
+            continue   # autodiff through w/|w| loses precision near sqrt(eps): see the FD test
+        p = torch.tensor(np.concatenate([kat["cam"][i], kat["cap"][i], kat["tag"][i]]))
+        c = torch.tensor(kat["corners"][i])
+        Jt = torch.autograd.functional.jacobian(lambda q: res(q, c), p).numpy()
+        r, J = oracle.residual_jacobian(kat["cam"][i], kat["cap"][i], kat["tag"][i], kat["corners"][i])
+        scale = np.abs(Jt).max(axis=1, keepdims=True)
+        assert np.max(np.abs(J - Jt) / scale) < 1e-12, i
+        np.testing.assert_allclose(r, res(p, c).detach().numpy(), rtol=1e-13, atol=1e-9)
+
+
+def test_jacobian_vs_central_differences(oracle):
+    """Near the small-angle threshold (|w|^2 ~ DBL_EPSILON) the analytic form is checked by FD."""
+    kat = np.load(os.path.join(GOLDEN, "jacobian_kat.npz"))
+    for i in list(range(3, 64, 8)) + [0, 1, 2, 5, 6]:
+        x0 = np.concatenate([kat["cam"][i], kat["cap"][i], kat["tag"][i]])
+        _, J = oracle.residual_jacobian(x0[:3], x0[3:9], x0[9:], kat["corners"][i])
+        Jfd = np.zeros_like(J)
+        for j in range(15):
+            h = 1e-6 * max(1.0, abs(x0[j]))
+            xp, xm = x0.copy(), x0.copy()
+            xp[j] += h
+            xm[j] -= h
+            rp = oracle.residual(xp[:3], xp[3:9], xp[9:], kat["corners"][i])
+            rm = oracle.residual(xm[:3], xm[3:9], xm[9:], kat["corners"][i])
+            Jfd[:, j] = (rp - rm) / (2 * h)
+        scale = np.abs(J).max(axis=1, keepdims=True)
+        assert np.max(np.abs(J - Jfd) / scale) < 1e-6, i
+
+
+def test_golden_jacobian_table(oracle):
+    kat = np.load(os.path.join(GOLDEN, "jacobian_kat.npz"))
+    for i in range(0, kat["cam"].shape[0], 5):
+        r, J = oracle.residual_jacobian(kat["cam"][i], kat["cap"][i], kat["tag"][i], kat["corners"][i])
+        np.testing.assert_array_equal(r, kat["r"][i])
+        np.testing.assert_array_equal(J, kat["J"][i])
+
+
+@pytest.mark.parametrize("name", ["tiny", "small", "medium"])
+def test_golden_lm_traces(oracle, name):
+    with open(os.path.join(GOLDEN, f"lm_{name}.json")) as f:
+        gold = json.load(f)
+    g = synth.config_graph(name)
+    cam, cap, tag, s = oracle.solve_graph(g)
+    assert s["termination"] == gold["termination"] and s["rule"] == gold["rule"]
+    np.testing.assert_allclose([it["cost"] for it in s["iterations"]], gold["cost"], rtol=1e-12)
+    np.testing.assert_allclose([it["trust_region_radius"] for it in s["iterations"]],
+                               gold["trust_region_radius"], rtol=1e-12)
+    assert cam[0] == pytest.approx(gold["final_focal"], rel=1e-12)
+
+
+@pytest.mark.parametrize("name", ["tiny", "small"])
+def test_schur_step_equals_full_normal_equations(oracle, name):
+    """Eliminating captures (DENSE_SCHUR) gives the LM step of the full system."""
+    g = synth.config_graph(name)
+    _, _, _, s1 = oracle.solve_graph(g, elimination=0)
+    _, _, _, s2 = oracle.solve_graph(g, elimination=1)
+    assert s1["termination"] == s2["termination"]
+    c1 = [it["cost"] for it in s1["iterations"]]
+    c2 = [it["cost"] for it in s2["iterations"]]
+    assert len(c1) == len(c2)
+    np.testing.assert_allclose(c1, c2, rtol=1e-10)
+
+
+def test_converged_cost_matches_scipy_least_squares(oracle):
+    """Same local minimum as scipy's trust-region reflective solver."""
+    scipy_opt = pytest.importorskip("scipy.optimize")
+    g = synth.config_graph("tiny")
+    cam, cap, tag, s = oracle.solve_graph(g, function_tolerance=1e-12, parameter_tolerance=1e-14,
+                                          max_num_iterations=200)
+    nc, nt = g.n_cap, g.n_tag
+
+    def unpack(x):
+        return x[:3], x[3:3 + 6 * nc].reshape(nc, 6), x[3 + 6 * nc:].reshape(nt, 6)
+
+    def fun(x):
+        c, cp, tg = unpack(x)
+        return np.concatenate([oracle.residual(c, cp[g.obs_cap[b]], tg[g.obs_tag[b]], g.corners[b])
+                               for b in range(g.n_obs)])
+
+    def jac(x):
+        c, cp, tg = unpack(x)
+        J = np.zeros((8 * g.n_obs, x.size))
+        for b in range(g.n_obs):
+            _, Jb = oracle.residual_jacobian(c, cp[g.obs_cap[b]], tg[g.obs_tag[b]], g.corners[b])
+            J[8 * b:8 * b + 8, 0:3] = Jb[:, 0:3]
+            J[8 * b:8 * b + 8, 3 + 6 * g.obs_cap[b]:9 + 6 * g.obs_cap[b]] = Jb[:, 3:9]
+            J[8 * b:8 * b + 8, 3 + 6 * nc + 6 * g.obs_tag[b]:9 + 6 * nc + 6 * g.obs_tag[b]] = Jb[:, 9:15]
+        return J
+
+    x0 = np.concatenate([g.camera, g.cap.ravel(), g.tag.ravel()])
+    sol = scipy_opt.least_squares(fun, x0, jac=jac, method="trf", xtol=1e-15, ftol=1e-15, gtol=1e-15,
+                                  max_nfev=500)
+    assert s["final_cost"] == pytest.approx(sol.cost, rel=1e-9)
+
+
+def test_noise_free_graph_recovers_truth(oracle):
+    """Zero pixel noise: RMS -> 0, focal -> f_true, tag layout -> truth (gauge-aligned)."""
+    g = synth.make_graph(30, 5, 4, seed=21, noise_px=0.0, name="noisefree")
+    cam, cap, tag, s = oracle.solve_graph(g, max_num_iterations=100)
+    assert s["termination"] == "CONVERGENCE"
+    assert synth.rms_px(s["final_cost"], g.n_obs) < 1e-6
+    assert cam[0] == pytest.approx(synth.F_TRUE, rel=1e-7)
+    used = np.unique(g.obs_tag)
+    P, Q = tag[used, :3], g.tag_true[used, :3]
+    pc, qc = P.mean(0), Q.mean(0)
+    U, _, Vt = np.linalg.svd((P - pc).T @ (Q - qc))
+    d = np.sign(np.linalg.det(Vt.T @ U.T))
+    R = Vt.T @ np.diag([1, 1, d]) @ U.T
+    assert np.abs((R @ (P - pc).T).T + qc - Q).max() < 1e-6
+
+
+def test_constant_blocks_and_localize(oracle):
+    """SetParameterBlockConstant semantics (ar_slam_util.cpp:965,972): constant blocks untouched."""
+    g = synth.config_graph("small")
+    tag_const = np.ones(g.n_tag, np.uint8)
+    cam, cap, tag, s = oracle.solve(g.camera_true, g.cap, g.tag_true, g.obs_cap, g.obs_tag, g.corners,
+                                    camera_const=True, tag_const=tag_const)
+    assert s["termination"] == "CONVERGENCE"
+    np.testing.assert_array_equal(tag, g.tag_true)
+    np.testing.assert_array_equal(cam, g.camera_true)
+    # localized captures land near the truth (poses fixed by the map, no gauge freedom)
+    assert np.abs(cap[:, :3] - g.cap_true[:, :3]).max() < 0.05
+
+
+def test_all_constant_is_fixed_cost(oracle):
+    """Residual blocks whose parameters are all constant count as fixed cost only."""
+    g = synth.config_graph("tiny")
+    kw = dict(camera_const=True, cap_const=np.ones(g.n_cap, np.uint8), tag_const=np.ones(g.n_tag, np.uint8))
+    cam, cap, tag, s = oracle.solve(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, **kw)
+    assert s["fixed_cost"] == pytest.approx(oracle.cost(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners))
+    assert s["initial_cost"] == pytest.approx(s["fixed_cost"])
+    np.testing.assert_array_equal(cap, g.cap)
+
+
+def test_dense_llt_matches_numpy(oracle):
+    rng = np.random.default_rng(3)
+    n = 300
+    B = rng.normal(size=(n, n))
+    A = B @ B.T + n * np.eye(n)
+    L = A.copy()
+    assert oracle.llt_lower(L) == 0
+    np.testing.assert_allclose(np.tril(L), np.linalg.cholesky(A), rtol=1e-10, atol=1e-10)
+    A[5, 5] = -1.0
+    assert oracle.llt_lower(A.copy()) == 6
