@@ -31,6 +31,20 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 constexpr int T64 = kTile;
+
+#ifdef ARSLAM_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define STAMP(id)                                                                       \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long _t;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");        \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[id] = _t;                         \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+  } while (0)
+#else
+#define STAMP(id) do {} while (0)
+#endif
 constexpr int LP = 65;   // LDS row pitch (doubles) for row-per-lane tiles
 constexpr int LM = 66;   // LDS row pitch for MFMA operand tiles (conflict-free ds_read_b64)
 
@@ -117,6 +131,24 @@ __device__ __forceinline__ void wave_gemm16_sub(double *C, const double *A, cons
   for (int reg = 0; reg < 4; ++reg) C[(lk + 4 * reg) * LQ + li] -= acc[reg];
 }
 
+constexpr int LI = 18;   // LDS pitch of the 16x16 inverse diagonal blocks (conflict-free fragments)
+
+// One wave: C(16x16) <- C Linv^T in place (the 16-column triangular solve
+// X L^T = C as an MFMA product with the explicit inverse of the 16x16 block).
+__device__ __forceinline__ void wave_apply_inv16(double *C, const double *Linv, int lane) {
+  const int li = lane & 15, lk = lane >> 4;
+  double a[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = C[li * LQ + 4 * q + lk];
+  __builtin_amdgcn_wave_barrier();
+  dbl4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], Linv[li * LI + 4 * q + lk], acc, 0, 0, 0);
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) C[(lk + 4 * reg) * LQ + li] = acc[reg];
+}
+
 // In-LDS blocked Cholesky of the 64x64 tile D (256 threads).  Sub-panels of
 // 16 columns: unblocked 16x16 factor (16 lanes of wave 0), row solve of the
 // panel below (16 lanes per wave), MFMA rank-16 update of the trailing tile.
@@ -127,33 +159,26 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
   __syncthreads();
   for (int p = 0; p < 4; ++p) {
     const int b0 = 16 * p;
+    STAMP(10 + 4 * p);
     if (w == 0) {
       // 16x16 diagonal block, lane i < 16 owns row b0+i in registers.  LDL^T
       // form: a_ic -= (a_ij / a_jj) a_cj, so only a reciprocal sits on the
-      // pivot chain (the square roots are taken once at the end); the pivot
-      // is broadcast with v_readlane, the column through LDS.
+      // pivot chain (square roots are taken once at the end); every broadcast
+      // is a v_readlane from the owning lane -- no LDS round trip per pivot.
       double x[16];
-      double *cb = LTd;   // scratch column buffer (16 doubles)
       const int li = lane & 15;
       const int i = b0 + li;
 #pragma unroll
       for (int c = 0; c < 16; ++c) x[c] = D[i * LQ + b0 + c];
 #pragma unroll
       for (int jj = 0; jj < 16; ++jj) {
-        if (lane < 16) cb[lane] = x[jj];
         const double ajj = readlane_d(x[jj], jj);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double r = __builtin_amdgcn_rcp(ajj);
         r = r * (2.0 - ajj * r);                    // Newton refinement of v_rcp_f64
         r = r * (2.0 - ajj * r);
-        const double f = (lane > jj) ? x[jj] * r : 0.0;
+        const double f = (li > jj) ? x[jj] * r : 0.0;
 #pragma unroll
-        for (int c = jj + 1; c < 16; ++c) x[c] -= f * cb[c];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int c = jj + 1; c < 16; ++c) x[c] -= f * readlane_d(x[jj], c);
       }
       // pivots are x_i[i]; L_ic = x_i[c] / sqrt(piv_c), L_ii = sqrt(piv_i)
       double piv = 0.0;
@@ -161,46 +186,43 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
       for (int c = 0; c < 16; ++c) piv = (c == li) ? x[c] : piv;
       if (!(piv > 0.0) && lane < 16) *bad = 1;
       const double d = sqrt(piv), rd = 1.0 / d;
-      if (lane < 16) { cb[16 + lane] = rd; inv[i] = rd; }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (lane < 16) {
+        inv[i] = rd;
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
-          const double l = (c < li) ? x[c] * cb[16 + c] : (c == li ? d : 0.0);
+          const double l = (c < li) ? x[c] * readlane_d(rd, c) : (c == li ? d : 0.0);
           D[i * LQ + b0 + c] = l;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // transposed copy of the diagonal block for the row solves: LTd[p][j][c] = L[b0+c][b0+j]
-      if (lane < 16) {
+      // explicit inverse of the 16x16 diagonal block: lane c < 16 forward-
+      // substitutes column c of L_pp^{-1} (right-looking, so only one multiply
+      // and one FMA per step sit on the dependency chain)
+      {
+        double v[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) LTd[32 + p * 256 + lane * 16 + c] = D[(b0 + c) * LQ + b0 + lane];
-      }
-    }
-    __syncthreads();
-    // rows below the diagonal block: X L_pp^T = A_panel
-    {
-      const int i = b0 + 16 + w * 16 + lane;
-      if (lane < 16 && i < 64) {
-        double x[16];
+        for (int r = 0; r < 16; ++r) v[r] = (r == li) ? 1.0 : 0.0;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) x[c] = D[i * LQ + b0 + c];
-        const double *lt = LTd + 32 + p * 256;
+        for (int k = 0; k < 16; ++k) {
+          v[k] *= inv[b0 + k];
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-          x[jj] *= inv[b0 + jj];
-#pragma unroll
-          for (int c = jj + 1; c < 16; ++c) x[c] -= x[jj] * lt[jj * 16 + c];
+          for (int r = k + 1; r < 16; ++r) v[r] -= D[(b0 + r) * LQ + b0 + k] * v[k];
         }
+        double *Li = LTd + p * 16 * LI;
+        if (lane < 16) {
 #pragma unroll
-        for (int c = 0; c < 16; ++c) D[i * LQ + b0 + c] = x[c];
+          for (int r = 0; r < 16; ++r) Li[r * LI + li] = v[r];
+        }
       }
     }
     __syncthreads();
+    STAMP(11 + 4 * p);
+    // rows below the diagonal block: X L_pp^T = A_panel  ->  X = A_panel L_pp^{-T}
+    if (w < 3 - p) wave_apply_inv16(D + (b0 + 16 + 16 * w) * LQ + b0, LTd + p * 16 * LI, lane);
+    __syncthreads();
+    STAMP(12 + 4 * p);
     // trailing update of blocks p+1..3 (lower tiles I >= C) with the panel
     const int m = 3 - p;
     const int ntl = m * (m + 1) / 2;
@@ -212,6 +234,7 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
       wave_gemm16_sub(D + bi * LQ + bc, D + bi * LQ + b0, D + bc * LQ + b0, 16, lane);
     }
     __syncthreads();
+    STAMP(13 + 4 * p);
   }
   return *bad == 0;
 }
@@ -226,21 +249,7 @@ __device__ void blocked_trsm64(double *X, const double *D, const double *inv, co
     if (p > 0)   // X[:, b0:b0+16] -= X[:, 0:b0] L[b0:b0+16, 0:b0]^T  (wave w: rows 16w..)
       wave_gemm16_sub(X + 16 * w * LQ + b0, X + 16 * w * LQ, D + b0 * LQ, b0, lane);
     __syncthreads();
-    if (lane < 16) {
-      const int r = 16 * w + lane;
-      double x[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) x[c] = X[r * LQ + b0 + c];
-      const double *lt = LTd + 32 + p * 256;
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) {
-        x[jj] *= inv[b0 + jj];
-#pragma unroll
-        for (int c = jj + 1; c < 16; ++c) x[c] -= x[jj] * lt[jj * 16 + c];
-      }
-#pragma unroll
-      for (int c = 0; c < 16; ++c) X[r * LQ + b0 + c] = x[c];
-    }
+    wave_apply_inv16(X + 16 * w * LQ + b0, LTd + p * 16 * LI, lane);
     __syncthreads();
   }
 }
@@ -257,8 +266,9 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
   __shared__ __attribute__((aligned(16))) double D[T64 * LQ];
   __shared__ __attribute__((aligned(16))) double X[T64 * LQ];
   __shared__ double inv[T64];
-  __shared__ __attribute__((aligned(16))) double LTd[32 + 4 * 256];   // column scratch + transposed diagonal blocks
+  __shared__ __attribute__((aligned(16))) double LTd[4 * 16 * LI];   // inverses of the 16x16 diagonal blocks
   __shared__ int bad;
+  STAMP(0);
   if (*flag) return;
   const int tid = threadIdx.x;
   const int2 t = tasks[blockIdx.x];
@@ -268,6 +278,7 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
   load_tile_wg(dk, lda, D, tid);
   if (ti != k) load_tile_wg(xt, lda, X, tid);
   __syncthreads();
+  STAMP(1);
   const bool ok = blocked_potrf64(D, inv, LTd, &bad, tid);
   if (!ok) {
     if (ti == k && tid == 0) {
@@ -281,8 +292,11 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
     store_tile_wg(Ld + (long)k * T64 * T64, T64, D, tid, true);
     return;
   }
+  STAMP(2);
   blocked_trsm64(X, D, inv, LTd, tid);
+  STAMP(3);
   store_tile_wg(xt, lda, X, tid, false);
+  STAMP(4);
 }
 
 // Update targets of one level: tile (i,j) -= sum over the level's columns k
@@ -372,42 +386,50 @@ __global__ void k_init_z(const double *__restrict__ S, long lda, const double *_
   z[j] = v;
 }
 
-// Backward solve L^T y = z for the columns of one level (root level first).
-// Column k gathers z_k -= sum_i L_ik^T y_i over its tile rows i > k (all of
-// them ancestors, solved by earlier launches), then solves the 64x64 block
-// L_kk^T y_k = z_k with lane r owning z_r and scalar broadcasts of y.
-__global__ __launch_bounds__(256) void k_back_solve(const double *__restrict__ S, long lda,
-                                                    const double *__restrict__ Ld, long nR,
-                                                    const int *__restrict__ cols,
-                                                    const int *__restrict__ gstart,
-                                                    const int *__restrict__ grows,
-                                                    const double *__restrict__ z,
-                                                    double *__restrict__ yF,
-                                                    const int *__restrict__ flag) {
-  __shared__ double Lk[T64 * LP];
+// Backward solve L^T y = z, level by level from the root.  For a level:
+//   k_bs_gather: one workgroup per gathered tile (i,k) (i > k, an ancestor
+//     already solved): zacc_k += L_ik^T y_i, 64 atomic adds per workgroup;
+//   k_bs_solve:  one workgroup per column k: solve L_kk^T y_k = z_k - zacc_k
+//     (lane r owns row r, 16-row blocks, scalar broadcasts of y).
+__global__ __launch_bounds__(256) void k_bs_gather(const double *__restrict__ S, long lda, long nR,
+                                                   const int2 *__restrict__ tasks,
+                                                   const double *__restrict__ yF,
+                                                   double *__restrict__ zacc,
+                                                   const int *__restrict__ flag) {
   __shared__ double part[4][T64];
-  __shared__ double y[T64];
   if (*flag) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int2 t = tasks[blockIdx.x];
+  const long ri = (long)t.x * T64, ck = (long)t.y * T64;
+  const double *Lik = S + ri * lda + ck;
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int r = w; r < T64; r += 8) {
+    const double y0 = (ri + r < nR) ? yF[ri + r] : 0.0;
+    const double y1 = (ri + r + 4 < nR) ? yF[ri + r + 4] : 0.0;
+    a0 += Lik[(long)r * lda + lane] * y0;
+    a1 += Lik[(long)(r + 4) * lda + lane] * y1;
+  }
+  part[w][lane] = a0 + a1;
+  __syncthreads();
+  if (w == 0) atomicAdd(zacc + ck + lane, part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
+}
+
+__global__ __launch_bounds__(64) void k_bs_solve(const double *__restrict__ Ld, long nR,
+                                                 const int *__restrict__ cols,
+                                                 const double *__restrict__ z,
+                                                 const double *__restrict__ zacc,
+                                                 double *__restrict__ yF,
+                                                 const int *__restrict__ flag) {
+  __shared__ double Lk[T64 * LP];
+  __shared__ double y[T64];
+  if (*flag) return;
+  const int lane = threadIdx.x;
   const int k = cols[blockIdx.x];
   const long row0 = (long)k * T64;
-  const int g0 = gstart[blockIdx.x], g1 = gstart[blockIdx.x + 1];
-  // gather: wave w takes rows r = w, w+4, ... of every gathered tile
-  double acc = 0.0;
-  for (int g = g0; g < g1; ++g) {
-    const long ri = (long)grows[g] * T64;
-    const double *Lik = S + ri * lda + row0;
-#pragma unroll 4
-    for (int r = w; r < T64; r += 4) {
-      const double yv = (ri + r < nR) ? yF[ri + r] : 0.0;
-      acc += Lik[(long)r * lda + lane] * yv;
-    }
-  }
-  part[w][lane] = acc;
-  if (w == 0) load_tile64(Ld + (long)k * T64 * T64, T64, Lk, lane);
+  double zr = (row0 + lane < nR) ? z[row0 + lane] - zacc[row0 + lane] : 0.0;
+  load_tile64(Ld + (long)k * T64 * T64, T64, Lk, lane);
   __syncthreads();
-  if (w != 0) return;
-  double zr = (row0 + lane < nR) ? z[row0 + lane] - (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) : 0.0;
   const double my_inv = (row0 + lane < nR) ? 1.0 / Lk[lane * LP + lane] : 0.0;   // y = 0 past nR
   double yv_own = 0.0;
   for (int p = 3; p >= 0; --p) {
@@ -481,12 +503,18 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s) {
   const long N = (long)P.T * T64;
+  double *zacc = z + N;   // z buffer holds 2N: z, then the gathered partial sums
+  (void)hipMemsetAsync(zacc, 0, N * sizeof(double), s);
   hipLaunchKernelGGL(k_init_z, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, S, P.lda, P.ldiag, nR, N,
                      z);
   for (int l = 0; l < P.nlev; ++l) {
+    const int g0 = P.h_bsg_off[l], ng = P.h_bsg_off[l + 1] - g0;
+    if (ng > 0)
+      hipLaunchKernelGGL(k_bs_gather, dim3((unsigned)ng), dim3(256), 0, s, S, P.lda, nR, P.bs_gather + g0, yF,
+                         zacc, flag);
     const int b0 = P.h_bs_off[l], nc = P.h_bs_off[l + 1] - b0;
-    hipLaunchKernelGGL(k_back_solve, dim3((unsigned)nc), dim3(256), 0, s, S, P.lda, P.ldiag, nR, P.bs_cols + b0,
-                       P.bs_gstart + b0, P.bs_grows, z, yF, flag);
+    hipLaunchKernelGGL(k_bs_solve, dim3((unsigned)nc), dim3(64), 0, s, P.ldiag, nR, P.bs_cols + b0, z, zacc,
+                       yF, flag);
   }
 }
 

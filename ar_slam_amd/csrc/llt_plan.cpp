@@ -202,10 +202,12 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   plan.nlev = nlev;
 
   std::vector<int2> panel, targets, tiles;
-  std::vector<int> kstart{0}, ks, bcols, gstart{0}, grows;
+  std::vector<int> kstart{0}, ks, bcols;
+  std::vector<int2> gather;
   plan.h_panel_off.assign(1, 0);
   plan.h_upd_off.assign(1, 0);
   plan.h_bs_off.assign(1, 0);
+  plan.h_bsg_off.assign(1, 0);
   plan.h_upd_flops.clear();
   plan.total_upd_flops = 0.0;
   plan.total_upd_tiles = 0;
@@ -258,10 +260,10 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
     for (int k : levcols[l]) {
       bcols.push_back(k);
       for (int i = k + 1; i < T; ++i)
-        if (P[(long)i * T + k]) grows.push_back(i);
-      gstart.push_back((int)grows.size());
+        if (P[(long)i * T + k]) gather.push_back(make_int2(i, k));
     }
     plan.h_bs_off.push_back((int)bcols.size());
+    plan.h_bsg_off.push_back((int)gather.size());
   }
   for (int i = 0; i < T; ++i)
     for (int j = 0; j <= i; ++j)
@@ -272,8 +274,7 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   plan.upd_kstart = upload(kstart, s);
   plan.upd_ks = upload(ks, s);
   plan.bs_cols = upload(bcols, s);
-  plan.bs_gstart = upload(gstart, s);
-  plan.bs_grows = upload(grows, s);
+  plan.bs_gather = upload(gather, s);
   plan.tiles = upload(tiles, s);
   check(hipMalloc(&plan.ldiag, (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
   check(hipStreamSynchronize(s), "plan sync");
@@ -281,8 +282,8 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
 
 void llt_plan_free(LltPlan &plan) {
   for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
-                  (void *)plan.upd_ks, (void *)plan.bs_cols, (void *)plan.bs_gstart,
-                  (void *)plan.bs_grows, (void *)plan.tiles, (void *)plan.ldiag})
+                  (void *)plan.upd_ks, (void *)plan.bs_cols, (void *)plan.bs_gather,
+                  (void *)plan.tiles, (void *)plan.ldiag})
     if (p) (void)hipFree(p);
   plan = LltPlan{};
 }

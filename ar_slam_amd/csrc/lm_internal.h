@@ -67,14 +67,14 @@ struct LltPlan {
   int *upd_kstart = nullptr;    // CSR over targets of the contributing columns k
   int *upd_ks = nullptr;
   int *bs_cols = nullptr;       // backward-solve columns, root level first
-  int *bs_gstart = nullptr;     // CSR over bs_cols of the tile rows gathered
-  int *bs_grows = nullptr;
+  int2 *bs_gather = nullptr;    // (i,k) tiles gathered by each backward level, root level first
   int2 *tiles = nullptr;        // every tile of the factor (zeroed before assembly)
   long n_tiles = 0;
   double *ldiag = nullptr;      // T x 64 x 64 diagonal factors L_kk (row-major, ld 64)
   std::vector<int> h_panel_off;     // [nlev+1]
   std::vector<int> h_upd_off;       // [nlev+1]
   std::vector<int> h_bs_off;        // [nlev+1], in backward (root-first) order
+  std::vector<int> h_bsg_off;       // [nlev+1], gather tasks per backward level
   std::vector<double> h_upd_flops;  // useful flops of each level's update
   double total_upd_flops = 0.0;
   long total_upd_tiles = 0;

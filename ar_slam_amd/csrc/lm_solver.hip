@@ -452,7 +452,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   if (has_f) {
     d_S.alloc((size_t)N * N);
     HIP_CHECK(hipMemsetAsync(d_S.p, 0, (size_t)N * N * sizeof(double), stream));
-    d_z.alloc(N);
+    d_z.alloc(2 * N);
     d_yF.alloc(N);
   } else {
     d_S.release();
