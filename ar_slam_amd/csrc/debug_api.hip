@@ -53,21 +53,14 @@ extern "C" int arslam_debug_residual_jacobian(int n, const double *cam, const do
 extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double *y, int *info) {
   if (n <= 0 || !A || !b || !y || !info) return ARSLAM_E_INVALID_ARG;
   const long N = (n + 1 + arslam::kTile - 1) / arslam::kTile * arslam::kTile;
+  const int T = (int)(N / arslam::kTile);
+  // dense lower matrix with the rhs as row n and identity padding, then compact tiles
   std::vector<double> h((size_t)N * N, 0.0);
   for (long i = 0; i < n; ++i)
     for (long j = 0; j <= i; ++j) h[i * N + j] = A[i * n + j];
   for (long j = 0; j < n; ++j) h[n * N + j] = b[j];
   h[n * N + n] = 1e300;
   for (long i = n + 1; i < N; ++i) h[i * N + i] = 1.0;
-  double *d_S = nullptr, *d_z = nullptr, *d_y = nullptr;
-  int *d_flag = nullptr;
-  DBG_CHECK(hipMalloc(&d_S, (size_t)N * N * sizeof(double)));
-  DBG_CHECK(hipMalloc(&d_z, 2 * N * sizeof(double)));
-  DBG_CHECK(hipMalloc(&d_y, N * sizeof(double)));
-  DBG_CHECK(hipMalloc(&d_flag, sizeof(int)));
-  DBG_CHECK(hipMemcpy(d_S, h.data(), (size_t)N * N * sizeof(double), hipMemcpyHostToDevice));
-  DBG_CHECK(hipMemset(d_flag, 0, sizeof(int)));
-  const int T = (int)(N / arslam::kTile);
   std::vector<uint8_t> pattern((size_t)T * T, 0);
   for (int i = 0; i < T; ++i)
     for (int j = 0; j <= i; ++j) pattern[(size_t)i * T + j] = 1;
@@ -77,16 +70,34 @@ extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double
   } catch (...) {
     return ARSLAM_E_HIP;
   }
+  std::vector<double> tiles((size_t)plan.n_tiles * 4096, 0.0);
+  for (int ti = 0; ti < T; ++ti)
+    for (int tj = 0; tj <= ti; ++tj) {
+      double *t = tiles.data() + (size_t)plan.h_tile_id[(size_t)ti * T + tj] * 4096;
+      for (int r = 0; r < 64; ++r)
+        for (int c = 0; c < 64; ++c) t[r * 64 + c] = h[(ti * 64 + r) * N + tj * 64 + c];
+    }
+  double *d_S = nullptr, *d_z = nullptr, *d_y = nullptr;
+  int *d_flag = nullptr;
+  DBG_CHECK(hipMalloc(&d_S, tiles.size() * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_z, 2 * N * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_y, N * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_flag, sizeof(int)));
+  DBG_CHECK(hipMemcpy(d_S, tiles.data(), tiles.size() * sizeof(double), hipMemcpyHostToDevice));
+  DBG_CHECK(hipMemset(d_flag, 0, sizeof(int)));
   arslam::launch_dense_llt(plan, d_S, d_flag, 0);
   arslam::launch_dense_back_solve(plan, d_S, n, d_z, d_y, d_flag, 0);
   arslam::launch_scatter_diag(plan, d_S, 0);
   DBG_CHECK(hipGetLastError());
   DBG_CHECK(hipDeviceSynchronize());
-  DBG_CHECK(hipMemcpy(h.data(), d_S, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost));
+  DBG_CHECK(hipMemcpy(tiles.data(), d_S, tiles.size() * sizeof(double), hipMemcpyDeviceToHost));
   DBG_CHECK(hipMemcpy(y, d_y, n * sizeof(double), hipMemcpyDeviceToHost));
   DBG_CHECK(hipMemcpy(info, d_flag, sizeof(int), hipMemcpyDeviceToHost));
   for (long i = 0; i < n; ++i)
-    for (long j = 0; j < n; ++j) A[i * n + j] = j <= i ? h[i * N + j] : 0.0;
+    for (long j = 0; j < n; ++j) {
+      const double *t = tiles.data() + (size_t)plan.h_tile_id[(size_t)(i / 64) * T + (j <= i ? j / 64 : 0)] * 4096;
+      A[i * n + j] = j <= i ? t[(i % 64) * 64 + (j % 64)] : 0.0;
+    }
   arslam::llt_plan_free(plan);
   (void)hipFree(d_S);
   (void)hipFree(d_z);

@@ -2,7 +2,9 @@
 // replacing the Eigen::LLT that Ceres' DenseSchurComplementSolver runs on one
 // CPU thread.
 //
-// Storage: dense row-major N x N (lower triangle used), 64 x 64 fp64 tiles.
+// Storage: compact 64 x 64 fp64 tiles (only the tiles of the factor exist;
+// tile (i,j) at S + tile_id[i*T+j] * 4096, assembled tiles first so the
+// multi-GPU all-reduce of the Schur sums covers one contiguous prefix).
 // Right-looking tiled factorization driven by a tile plan (LltPlan):
 //   for k:  POTRF(k,k)            one wavefront, lane r owns row r in VGPRs
 //           TRSM (i,k)            one wavefront per tile, rows in VGPRs,
@@ -47,6 +49,15 @@ __device__ unsigned long long g_stamps[64];
 #endif
 constexpr int LP = 65;   // LDS row pitch (doubles) for row-per-lane tiles
 constexpr int LM = 66;   // LDS row pitch for MFMA operand tiles (conflict-free ds_read_b64)
+
+// Compact tile storage: tile (i,j) of the factor is a contiguous 64x64
+// row-major block at S + tid[i*T + j] * 4096 (tid = -1: structurally zero).
+__device__ __forceinline__ double *tile_ptr(double *S, const int *tid, int T, int i, int j) {
+  return S + (long)tid[(long)i * T + j] * (T64 * T64);
+}
+__device__ __forceinline__ const double *tile_ptr(const double *S, const int *tid, int T, int i, int j) {
+  return S + (long)tid[(long)i * T + j] * (T64 * T64);
+}
 
 // Load a 64x64 tile (row-major, lda) into LDS with pitch LP using 64 lanes:
 // 32 independent 16-byte loads per lane are issued before any LDS store.
@@ -259,8 +270,8 @@ __device__ void blocked_trsm64(double *X, const double *D, const double *inv, co
 // either stores L_kk (i == k) or solves tile (i,k) against it.  L_kk goes to
 // its own buffer Ld (64x64 per tile column), never over A_kk in S: the other
 // tasks of the column may still be reading A_kk.
-__global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
-                                               double *__restrict__ Ld,
+__global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, const int *__restrict__ tid_map,
+                                               int T, double *__restrict__ Ld,
                                                const int2 *__restrict__ tasks,
                                                int *__restrict__ flag) {
   __shared__ __attribute__((aligned(16))) double D[T64 * LQ];
@@ -273,10 +284,10 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
   const int tid = threadIdx.x;
   const int2 t = tasks[blockIdx.x];
   const int ti = t.x, k = t.y;
-  const double *dk = S + (long)k * T64 * lda + (long)k * T64;
-  double *xt = S + (long)ti * T64 * lda + (long)k * T64;
-  load_tile_wg(dk, lda, D, tid);
-  if (ti != k) load_tile_wg(xt, lda, X, tid);
+  const double *dk = tile_ptr(S, tid_map, T, k, k);
+  double *xt = tile_ptr(S, tid_map, T, ti, k);
+  load_tile_wg(dk, T64, D, tid);
+  if (ti != k) load_tile_wg(xt, T64, X, tid);
   __syncthreads();
   STAMP(1);
   const bool ok = blocked_potrf64(D, inv, LTd, &bad, tid);
@@ -295,15 +306,15 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long lda,
   STAMP(2);
   blocked_trsm64(X, D, inv, LTd, tid);
   STAMP(3);
-  store_tile_wg(xt, lda, X, tid, false);
+  store_tile_wg(xt, T64, X, tid, false);
   STAMP(4);
 }
 
 // Update targets of one level: tile (i,j) -= sum over the level's columns k
 // of L_ik L_jk^T.  One workgroup per target (no two workgroups write the same
 // tile); 4 waves x 32x32 on v_mfma_f64_16x16x4_f64, K = 64 per column.
-__global__ __launch_bounds__(256) void k_update(double *__restrict__ S, long lda,
-                                                const int2 *__restrict__ targets,
+__global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const int *__restrict__ tid_map,
+                                                int T, const int2 *__restrict__ targets,
                                                 const int *__restrict__ kstart,
                                                 const int *__restrict__ ks,
                                                 const int *__restrict__ flag) {
@@ -317,25 +328,25 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, long lda
   const int w = tid >> 6, lane = tid & 63;
   const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
   const int li = lane & 15, lk = lane >> 4;
-  double *C = S + (long)ti * T64 * lda + (long)tj * T64;
+  double *C = tile_ptr(S, tid_map, T, ti, tj);
   double cval[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) cval[4 * q + reg] = C[(long)(rb + lk + 4 * reg) * lda + cb + li];
+    for (int reg = 0; reg < 4; ++reg) cval[4 * q + reg] = C[(rb + lk + 4 * reg) * T64 + cb + li];
   }
   dbl4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
   for (int q = q0; q < q1; ++q) {
     const int k = ks[q];
-    const double *Ai = S + (long)ti * T64 * lda + (long)k * T64;
-    const double *Bj = S + (long)tj * T64 * lda + (long)k * T64;
+    const double *Ai = tile_ptr(S, tid_map, T, ti, k);
+    const double *Bj = tile_ptr(S, tid_map, T, tj, k);
     dbl2 va[8], vb[8];
 #pragma unroll
     for (int e8 = 0; e8 < 8; ++e8) {
       const int e = e8 * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
-      va[e8] = *reinterpret_cast<const dbl2 *>(Ai + (long)r * lda + c2);
-      vb[e8] = *reinterpret_cast<const dbl2 *>(Bj + (long)r * lda + c2);
+      va[e8] = *reinterpret_cast<const dbl2 *>(Ai + r * T64 + c2);
+      vb[e8] = *reinterpret_cast<const dbl2 *>(Bj + r * T64 + c2);
     }
     if (q > q0) __syncthreads();   // previous column's fragments consumed
 #pragma unroll
@@ -366,22 +377,22 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, long lda
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int row = rb + lk + 4 * reg, col = cb + li;
-      C[(long)row * lda + col] = cval[4 * q + reg] - accs[q][reg];
+      C[row * T64 + col] = cval[4 * q + reg] - accs[q][reg];
     }
   }
 }
 
 // z[j] = L[nR][j], the forward-substituted right-hand side: from S for the
 // tiles left of the rhs row's own tile, from that tile's diagonal factor in Ld.
-__global__ void k_init_z(const double *__restrict__ S, long lda, const double *__restrict__ Ld,
-                         long nR, long N, double *__restrict__ z) {
+__global__ void k_init_z(const double *__restrict__ S, const int *__restrict__ tid_map, int T,
+                         const double *__restrict__ Ld, long nR, long N, double *__restrict__ z) {
   const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= N) return;
   const long kr = nR / T64;
   double v = 0.0;
   if (j < nR) {
     if (j >= kr * T64) v = Ld[kr * T64 * T64 + (nR - kr * T64) * T64 + (j - kr * T64)];
-    else v = S[nR * lda + j];
+    else v = tile_ptr(S, tid_map, T, (int)kr, (int)(j / T64))[(nR - kr * T64) * T64 + (j % T64)];
   }
   z[j] = v;
 }
@@ -391,7 +402,8 @@ __global__ void k_init_z(const double *__restrict__ S, long lda, const double *_
 //     already solved): zacc_k += L_ik^T y_i, 64 atomic adds per workgroup;
 //   k_bs_solve:  one workgroup per column k: solve L_kk^T y_k = z_k - zacc_k
 //     (lane r owns row r, 16-row blocks, scalar broadcasts of y).
-__global__ __launch_bounds__(256) void k_bs_gather(const double *__restrict__ S, long lda, long nR,
+__global__ __launch_bounds__(256) void k_bs_gather(const double *__restrict__ S,
+                                                   const int *__restrict__ tid_map, int T, long nR,
                                                    const int2 *__restrict__ tasks,
                                                    const double *__restrict__ yF,
                                                    double *__restrict__ zacc,
@@ -401,14 +413,14 @@ __global__ __launch_bounds__(256) void k_bs_gather(const double *__restrict__ S,
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int2 t = tasks[blockIdx.x];
   const long ri = (long)t.x * T64, ck = (long)t.y * T64;
-  const double *Lik = S + ri * lda + ck;
+  const double *Lik = tile_ptr(S, tid_map, T, t.x, t.y);
   double a0 = 0.0, a1 = 0.0;
 #pragma unroll
   for (int r = w; r < T64; r += 8) {
     const double y0 = (ri + r < nR) ? yF[ri + r] : 0.0;
     const double y1 = (ri + r + 4 < nR) ? yF[ri + r + 4] : 0.0;
-    a0 += Lik[(long)r * lda + lane] * y0;
-    a1 += Lik[(long)(r + 4) * lda + lane] * y1;
+    a0 += Lik[r * T64 + lane] * y0;
+    a1 += Lik[(r + 4) * T64 + lane] * y1;
   }
   part[w][lane] = a0 + a1;
   __syncthreads();
@@ -454,42 +466,34 @@ __global__ __launch_bounds__(64) void k_bs_solve(const double *__restrict__ Ld, 
   if (row0 + lane < nR) yF[row0 + lane] = yv_own;
 }
 
-__global__ void k_zero_tiles(double *__restrict__ S, long lda, const int2 *__restrict__ tiles) {
-  const int2 t = tiles[blockIdx.x];
-  double *p = S + (long)t.x * T64 * lda + (long)t.y * T64;
-  for (int e = threadIdx.x; e < T64 * 32; e += blockDim.x) {
-    const int r = e >> 5, c2 = (e & 31) * 2;
-    *reinterpret_cast<dbl2 *>(p + (long)r * lda + c2) = dbl2{0.0, 0.0};
-  }
+// tests only: copy the diagonal factors L_kk into their S tiles
+__global__ void k_scatter_diag(double *__restrict__ S, const int *__restrict__ tid_map, int T,
+                               const double *__restrict__ Ld) {
+  const int k = blockIdx.x;
+  double *t = tile_ptr(S, tid_map, T, k, k);
+  for (int e = threadIdx.x; e < T64 * T64; e += blockDim.x) t[e] = Ld[(long)k * T64 * T64 + e];
 }
 
 }  // namespace
 
-__global__ void k_scatter_diag(double *__restrict__ S, long lda, const double *__restrict__ Ld) {
-  const int k = blockIdx.x;
-  for (int e = threadIdx.x; e < T64 * T64; e += blockDim.x)
-    S[((long)k * T64 + e / T64) * lda + (long)k * T64 + e % T64] = Ld[(long)k * T64 * T64 + e];
-}
-
 void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s) {
-  hipLaunchKernelGGL(k_scatter_diag, dim3((unsigned)P.T), dim3(256), 0, s, S, P.lda, P.ldiag);
+  hipLaunchKernelGGL(k_scatter_diag, dim3((unsigned)P.T), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag);
 }
 
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s) {
-  if (P.n_tiles == 0) return;
-  hipLaunchKernelGGL(k_zero_tiles, dim3((unsigned)P.n_tiles), dim3(256), 0, s, S, P.lda, P.tiles);
+  if (P.n_tiles) (void)hipMemsetAsync(S, 0, (size_t)P.n_tiles * T64 * T64 * sizeof(double), s);
 }
 
 void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, LaunchTiming *timing) {
   for (int l = 0; l < P.nlev; ++l) {
     const int np = P.h_panel_off[l + 1] - P.h_panel_off[l];
-    hipLaunchKernelGGL(k_panel, dim3((unsigned)np), dim3(256), 0, s, S, P.lda, P.ldiag,
+    hipLaunchKernelGGL(k_panel, dim3((unsigned)np), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag,
                        P.panel + P.h_panel_off[l], flag);
     const int nu = P.h_upd_off[l + 1] - P.h_upd_off[l];
     if (nu > 0) {
       const bool rec = timing && timing->used < timing->cap;
       if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
-      hipLaunchKernelGGL(k_update, dim3((unsigned)nu), dim3(256), 0, s, S, P.lda,
+      hipLaunchKernelGGL(k_update, dim3((unsigned)nu), dim3(256), 0, s, S, P.tile_id, P.T,
                          P.upd_targets + P.h_upd_off[l], P.upd_kstart + P.h_upd_off[l], P.upd_ks, flag);
       if (rec) {
         (void)hipEventRecord(timing->ev[2 * timing->used + 1], s);
@@ -505,12 +509,12 @@ void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double 
   const long N = (long)P.T * T64;
   double *zacc = z + N;   // z buffer holds 2N: z, then the gathered partial sums
   (void)hipMemsetAsync(zacc, 0, N * sizeof(double), s);
-  hipLaunchKernelGGL(k_init_z, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, S, P.lda, P.ldiag, nR, N,
-                     z);
+  hipLaunchKernelGGL(k_init_z, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag,
+                     nR, N, z);
   for (int l = 0; l < P.nlev; ++l) {
     const int g0 = P.h_bsg_off[l], ng = P.h_bsg_off[l + 1] - g0;
     if (ng > 0)
-      hipLaunchKernelGGL(k_bs_gather, dim3((unsigned)ng), dim3(256), 0, s, S, P.lda, nR, P.bs_gather + g0, yF,
+      hipLaunchKernelGGL(k_bs_gather, dim3((unsigned)ng), dim3(256), 0, s, S, P.tile_id, P.T, nR, P.bs_gather + g0, yF,
                          zacc, flag);
     const int b0 = P.h_bs_off[l], nc = P.h_bs_off[l + 1] - b0;
     hipLaunchKernelGGL(k_bs_solve, dim3((unsigned)nc), dim3(64), 0, s, P.ldiag, nR, P.bs_cols + b0, z, zacc,

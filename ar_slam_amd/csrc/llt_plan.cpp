@@ -178,6 +178,13 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   llt_plan_free(plan);
   plan.T = T;
   plan.lda = lda;
+  // compact tile numbering: assembled tiles (the input pattern + diagonal) first
+  plan.h_tile_id.assign((size_t)T * T, -1);
+  long nid = 0;
+  for (int i = 0; i < T; ++i)
+    for (int j = 0; j <= i; ++j)
+      if (P[(long)i * T + j] || i == j) plan.h_tile_id[(long)i * T + j] = (int)nid++;
+  plan.n_assembled = nid;
   // symbolic factorization at tile level
   std::vector<int> rows;
   for (int k = 0; k < T; ++k) {
@@ -201,7 +208,7 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   for (int k = 0; k < T; ++k) levcols[height[k]].push_back(k);
   plan.nlev = nlev;
 
-  std::vector<int2> panel, targets, tiles;
+  std::vector<int2> panel, targets;
   std::vector<int> kstart{0}, ks, bcols;
   std::vector<int2> gather;
   plan.h_panel_off.assign(1, 0);
@@ -265,17 +272,17 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
     plan.h_bs_off.push_back((int)bcols.size());
     plan.h_bsg_off.push_back((int)gather.size());
   }
-  for (int i = 0; i < T; ++i)
+  for (int i = 0; i < T; ++i)   // fill tiles numbered after the assembled ones
     for (int j = 0; j <= i; ++j)
-      if (P[(long)i * T + j]) tiles.push_back(make_int2(i, j));
-  plan.n_tiles = (long)tiles.size();
+      if (P[(long)i * T + j] && plan.h_tile_id[(long)i * T + j] < 0) plan.h_tile_id[(long)i * T + j] = (int)nid++;
+  plan.n_tiles = nid;
   plan.panel = upload(panel, s);
   plan.upd_targets = upload(targets, s);
   plan.upd_kstart = upload(kstart, s);
   plan.upd_ks = upload(ks, s);
   plan.bs_cols = upload(bcols, s);
   plan.bs_gather = upload(gather, s);
-  plan.tiles = upload(tiles, s);
+  plan.tile_id = upload(plan.h_tile_id, s);
   check(hipMalloc(&plan.ldiag, (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
   check(hipStreamSynchronize(s), "plan sync");
 }
@@ -283,7 +290,7 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
 void llt_plan_free(LltPlan &plan) {
   for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
                   (void *)plan.upd_ks, (void *)plan.bs_cols, (void *)plan.bs_gather,
-                  (void *)plan.tiles, (void *)plan.ldiag})
+                  (void *)plan.tile_id, (void *)plan.ldiag})
     if (p) (void)hipFree(p);
   plan = LltPlan{};
 }

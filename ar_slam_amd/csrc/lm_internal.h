@@ -54,7 +54,14 @@ struct DevProblem {
   const double *corners;     // [nb*8]
   const int *tag_row;        // [nt]    first reduced row of tag t (6 rows), -1 if not free
   const int *row_slot;       // [nR]    parameter slot of a reduced row, -1 for padding rows
+  const int *tile_id;        // [T*T]   compact tile index of the reduced system (see LltPlan)
+  int T;                     // tiles per side
 };
+
+// element (r, c), r >= c, of the compact-tiled reduced system
+__device__ inline double *reduced_elem(double *S, const DevProblem &P, long r, long c) {
+  return S + (long)P.tile_id[(r >> 6) * P.T + (c >> 6)] * 4096 + (r & 63) * 64 + (c & 63);
+}
 
 // Tile plan of the reduced-system Cholesky (dense_llt.hip), level-scheduled
 // over the tile elimination tree.  Device arrays, host per-level offsets.
@@ -68,8 +75,10 @@ struct LltPlan {
   int *upd_ks = nullptr;
   int *bs_cols = nullptr;       // backward-solve columns, root level first
   int2 *bs_gather = nullptr;    // (i,k) tiles gathered by each backward level, root level first
-  int2 *tiles = nullptr;        // every tile of the factor (zeroed before assembly)
-  long n_tiles = 0;
+  int *tile_id = nullptr;       // [T*T] compact index of tile (i,j), -1 if structurally zero
+  std::vector<int> h_tile_id;
+  long n_tiles = 0;             // tiles of the factor (compact storage = n_tiles * 4096 doubles)
+  long n_assembled = 0;         // tiles the Schur assembly writes (numbered first)
   double *ldiag = nullptr;      // T x 64 x 64 diagonal factors L_kk (row-major, ld 64)
   std::vector<int> h_panel_off;     // [nlev+1]
   std::vector<int> h_upd_off;       // [nlev+1]

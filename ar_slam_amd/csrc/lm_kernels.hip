@@ -411,8 +411,8 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
   diag[i] = fmin(fmax(d, dmin), dmax);
 }
 
-// Schur elimination of capture c into the dense reduced system S (lower,
-// row-major, lda); row nF of S accumulates the reduced right-hand side.
+// Schur elimination of capture c into the reduced system S (compact tiles,
+// lower triangle); row nR of S accumulates the reduced right-hand side.
 __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ x,
                                                  const double *__restrict__ scale,
                                                  const double *__restrict__ diag, double radius,
@@ -493,15 +493,13 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
     }
   }
   __syncthreads();
-  const long lda = P.lda;
-  double *rhs = S + P.nR * lda;
-  // reduced rhs: F'r - W' Ui E'r
+  // reduced rhs (row nR): F'r - W' Ui E'r
   for (int p = lane; p < m; p += kWave) {
     if (gidx[p] < 0) continue;
     double s = 0.0;
 #pragma unroll
     for (int a = 0; a < 6; ++a) s += W[a * m + p] * UiE[a];
-    atomicAdd(rhs + gidx[p], Ftr[p] - s);
+    atomicAdd(reduced_elem(S, P, P.nR, gidx[p]), Ftr[p] - s);
   }
   // reduced matrix: F'F - W' Ui W, local pairs p >= q
   const int npairs = m * (m + 1) / 2;
@@ -524,7 +522,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
     const long gi = gidx[p], gj = gidx[q];
     if (gi < 0 || gj < 0) continue;
     const long hi = gi > gj ? gi : gj, lo = gi > gj ? gj : gi;
-    atomicAdd(S + hi * lda + lo, ff - wz);
+    atomicAdd(reduced_elem(S, P, hi, lo), ff - wz);
   }
 }
 
@@ -535,7 +533,7 @@ __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, do
                                double *__restrict__ S) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.N) return;
-  double *d = S + i * P.lda + i;
+  double *d = reduced_elem(S, P, i, i);
   if (i < P.nR) {
     const int slot = P.row_slot[i];
     if (slot >= 0) *d += lm_d2(diag, slot, radius);

@@ -450,8 +450,8 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_tag_row.alloc(tag_row.size()); d_tag_row.upload(tag_row.data(), tag_row.size(), stream);
   d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
   if (has_f) {
-    d_S.alloc((size_t)N * N);
-    HIP_CHECK(hipMemsetAsync(d_S.p, 0, (size_t)N * N * sizeof(double), stream));
+    d_S.alloc((size_t)plan.n_tiles * 4096);
+    HIP_CHECK(hipMemsetAsync(d_S.p, 0, d_S.n * sizeof(double), stream));
     d_z.alloc(2 * N);
     d_yF.alloc(N);
   } else {
@@ -468,6 +468,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   P.obs_active = d_obs_active.p; P.slot_free = d_slot_free.p;
   P.tag_start = d_tag_start.p; P.tag_obs = d_tag_obs.p; P.corners = d_corners.p;
   P.tag_row = d_tag_row.p; P.row_slot = d_row_slot.p;
+  P.tile_id = plan.tile_id; P.T = plan.T;
   HIP_CHECK(hipStreamSynchronize(stream));
   loaded = true;
 }
@@ -625,7 +626,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       timers[PH_SCHUR].start(stream);
       arslam::launch_zero_tiles(plan, d_S.p, stream);
       arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream);
-      if (nranks > 1) allreduce(d_S.p, (size_t)N * N, ncclSum);
+      if (nranks > 1) allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ncclSum);
       arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
