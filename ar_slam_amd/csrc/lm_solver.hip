@@ -822,6 +822,26 @@ int arslam_lm_create(arslam_lm **out, const arslam_lm_options *opt) {
 
 void arslam_lm_destroy(arslam_lm *h) { delete h; }
 
+int arslam_lm_set_options(arslam_lm *h, const arslam_lm_options *opt) {
+  if (!h || !opt) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    fail_if(opt->elimination != ARSLAM_ELIM_AUTO && opt->elimination != ARSLAM_ELIM_CAPTURES,
+            ARSLAM_E_UNSUPPORTED, "only capture elimination is implemented");
+    fail_if(opt->max_num_iterations < 0 || opt->max_num_iterations > ARSLAM_LM_MAX_ITERS,
+            ARSLAM_E_INVALID_ARG, "max_num_iterations out of range");
+    if (opt->device != h->opt.device || opt->reduced_ordering != h->opt.reduced_ordering ||
+        opt->cholesky_skip_zero_tiles != h->opt.cholesky_skip_zero_tiles)
+      h->loaded = false;
+    h->opt = *opt;
+  });
+}
+
+int arslam_lm_get_options(const arslam_lm *h, arslam_lm_options *opt) {
+  if (!h || !opt) return ARSLAM_E_INVALID_ARG;
+  *opt = h->opt;
+  return ARSLAM_OK;
+}
+
 int arslam_lm_add_residual_block(arslam_lm *h, const double corners[8], double *camera,
                                  double *capture, double *tag) {
   if (!h || !corners || !camera || !capture || !tag) return ARSLAM_E_INVALID_ARG;

@@ -37,6 +37,7 @@ ERRORS = {-1: "INVALID_ARG", -2: "UNSUPPORTED", -3: "NO_DEVICE", -4: "HIP", -5: 
 
 # Every symbol include/arslam_lm.h declares (checked by the CPU tests).
 EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
+           "arslam_lm_set_options", "arslam_lm_get_options",
            "arslam_lm_add_residual_block", "arslam_lm_set_parameter_block_constant",
            "arslam_lm_set_parameter_block_variable", "arslam_lm_solve", "arslam_lm_reset",
            "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
@@ -135,6 +136,8 @@ def lib():
     L = C.CDLL(LIB_PATH)
     L.arslam_lm_options_init.argtypes = [C.POINTER(Options)]
     L.arslam_lm_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
+    L.arslam_lm_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
+    L.arslam_lm_get_options.argtypes = [C.c_void_p, C.POINTER(Options)]
     L.arslam_lm_destroy.argtypes = [C.c_void_p]
     L.arslam_lm_destroy.restype = None
     L.arslam_lm_add_residual_block.argtypes = [C.c_void_p, _dp, _dp, _dp, _dp]
@@ -229,6 +232,14 @@ class _Handle:
             self.close()
         except Exception:
             pass
+
+    def set_options(self, **opts):
+        _check(lib().arslam_lm_set_options(self._h, C.byref(make_options(**opts))))
+
+    def get_options(self) -> Options:
+        o = Options()
+        _check(lib().arslam_lm_get_options(self._h, C.byref(o)))
+        return o
 
     def set_comm(self, rank, nranks, uid: bytes):
         _check(lib().arslam_lm_set_comm(self._h, rank, nranks, uid))

@@ -147,6 +147,13 @@ int arslam_lm_options_init(arslam_lm_options *opt);
 int arslam_lm_create(arslam_lm **out, const arslam_lm_options *opt);
 void arslam_lm_destroy(arslam_lm *h);
 
+/* Per-solve options (the Solver::Options ArSlamSolver::optimize builds on
+ * every call, ar_slam_util.cpp:1003-1012).  Changing device, reduced_ordering
+ * or cholesky_skip_zero_tiles drops a problem loaded by arslam_lm_load_soa
+ * (load again); the pointer-keyed problem is unaffected. */
+int arslam_lm_set_options(arslam_lm *h, const arslam_lm_options *opt);
+int arslam_lm_get_options(const arslam_lm *h, arslam_lm_options *opt);
+
 /* problem_.AddResidualBlock(new AutoDiffCostFunction<ArucoReprojectionError,
  * 8,3,6,6>(new ArucoReprojectionError(rect)), nullptr, camera, capture, tag)
  * -- ar_slam_util.cpp:720-727.  corners = ArucoRect x0,y0,..,x3,y3. */

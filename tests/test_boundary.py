@@ -91,3 +91,17 @@ def test_solve_without_gpu_fails_loudly(L):
 def test_empty_problem_converges_immediately(L):
     s = L.Problem().solve()
     assert s["termination"] == "CONVERGENCE" and s["num_linear_solves"] == 0
+
+
+def test_set_and_get_options_roundtrip(L):
+    """Per-solve options (ArSlamSolver::optimize builds Solver::Options per call, ar_slam_util.cpp:1003-1012)."""
+    prob = L.Problem()
+    prob.set_options(max_num_iterations=7, minimizer_progress_to_stdout=1, function_tolerance=1e-9)
+    o = prob.get_options()
+    assert o.max_num_iterations == 7 and o.minimizer_progress_to_stdout == 1
+    assert o.function_tolerance == 1e-9
+    with pytest.raises(L.LMError):
+        prob.set_options(max_num_iterations=-1)
+    with pytest.raises(L.LMError):
+        prob.set_options(elimination=5)
+    assert prob.get_options().max_num_iterations == 7   # a rejected call leaves the options unchanged
