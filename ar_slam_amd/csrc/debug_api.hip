@@ -80,7 +80,7 @@ extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double
   double *d_S = nullptr, *d_z = nullptr, *d_y = nullptr;
   int *d_flag = nullptr;
   DBG_CHECK(hipMalloc(&d_S, tiles.size() * sizeof(double)));
-  DBG_CHECK(hipMalloc(&d_z, 2 * N * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_z, N * sizeof(double)));
   DBG_CHECK(hipMalloc(&d_y, N * sizeof(double)));
   DBG_CHECK(hipMalloc(&d_flag, sizeof(int)));
   DBG_CHECK(hipMemcpy(d_S, tiles.data(), tiles.size() * sizeof(double), hipMemcpyHostToDevice));

@@ -399,20 +399,22 @@ __global__ void k_init_z(const double *__restrict__ S, const int *__restrict__ t
 
 // Backward solve L^T y = z, level by level from the root.  For a level:
 //   k_bs_gather: one workgroup per gathered tile (i,k) (i > k, an ancestor
-//     already solved): zacc_k += L_ik^T y_i, 64 atomic adds per workgroup;
-//   k_bs_solve:  one workgroup per column k: solve L_kk^T y_k = z_k - zacc_k
-//     (lane r owns row r, 16-row blocks, scalar broadcasts of y).
+//     already solved): part_g = L_ik^T y_i, stored to its own slot;
+//   k_bs_solve:  one workgroup per column k: sums its gathers' partials in
+//     plan order (deterministic: every rank of a sharded solve computes the
+//     same bits), then solves L_kk^T y_k = z_k - sum (lane r owns row r,
+//     16-row blocks, scalar broadcasts of y).
 __global__ __launch_bounds__(256) void k_bs_gather(const double *__restrict__ S,
                                                    const int *__restrict__ tid_map, int T, long nR,
                                                    const int2 *__restrict__ tasks,
                                                    const double *__restrict__ yF,
-                                                   double *__restrict__ zacc,
+                                                   double *__restrict__ part_out,
                                                    const int *__restrict__ flag) {
   __shared__ double part[4][T64];
   if (*flag) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int2 t = tasks[blockIdx.x];
-  const long ri = (long)t.x * T64, ck = (long)t.y * T64;
+  const long ri = (long)t.x * T64;
   const double *Lik = tile_ptr(S, tid_map, T, t.x, t.y);
   double a0 = 0.0, a1 = 0.0;
 #pragma unroll
@@ -424,13 +426,14 @@ __global__ __launch_bounds__(256) void k_bs_gather(const double *__restrict__ S,
   }
   part[w][lane] = a0 + a1;
   __syncthreads();
-  if (w == 0) atomicAdd(zacc + ck + lane, part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
+  if (w == 0) part_out[(long)blockIdx.x * T64 + lane] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
 }
 
 __global__ __launch_bounds__(64) void k_bs_solve(const double *__restrict__ Ld, long nR,
                                                  const int *__restrict__ cols,
+                                                 const int *__restrict__ gbeg,
                                                  const double *__restrict__ z,
-                                                 const double *__restrict__ zacc,
+                                                 const double *__restrict__ part,
                                                  double *__restrict__ yF,
                                                  const int *__restrict__ flag) {
   __shared__ double Lk[T64 * LP];
@@ -439,8 +442,10 @@ __global__ __launch_bounds__(64) void k_bs_solve(const double *__restrict__ Ld, 
   const int lane = threadIdx.x;
   const int k = cols[blockIdx.x];
   const long row0 = (long)k * T64;
-  double zr = (row0 + lane < nR) ? z[row0 + lane] - zacc[row0 + lane] : 0.0;
   load_tile64(Ld + (long)k * T64 * T64, T64, Lk, lane);
+  double acc = 0.0;
+  for (int g = gbeg[blockIdx.x]; g < gbeg[blockIdx.x + 1]; ++g) acc += part[(long)g * T64 + lane];
+  double zr = (row0 + lane < nR) ? z[row0 + lane] - acc : 0.0;
   __syncthreads();
   const double my_inv = (row0 + lane < nR) ? 1.0 / Lk[lane * LP + lane] : 0.0;   // y = 0 past nR
   double yv_own = 0.0;
@@ -507,18 +512,16 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s) {
   const long N = (long)P.T * T64;
-  double *zacc = z + N;   // z buffer holds 2N: z, then the gathered partial sums
-  (void)hipMemsetAsync(zacc, 0, N * sizeof(double), s);
   hipLaunchKernelGGL(k_init_z, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag,
                      nR, N, z);
   for (int l = 0; l < P.nlev; ++l) {
     const int g0 = P.h_bsg_off[l], ng = P.h_bsg_off[l + 1] - g0;
     if (ng > 0)
       hipLaunchKernelGGL(k_bs_gather, dim3((unsigned)ng), dim3(256), 0, s, S, P.tile_id, P.T, nR, P.bs_gather + g0, yF,
-                         zacc, flag);
+                         P.bs_part + (long)g0 * T64, flag);
     const int b0 = P.h_bs_off[l], nc = P.h_bs_off[l + 1] - b0;
-    hipLaunchKernelGGL(k_bs_solve, dim3((unsigned)nc), dim3(64), 0, s, P.ldiag, nR, P.bs_cols + b0, z, zacc,
-                       yF, flag);
+    hipLaunchKernelGGL(k_bs_solve, dim3((unsigned)nc), dim3(64), 0, s, P.ldiag, nR, P.bs_cols + b0,
+                       P.bs_gbeg + b0, z, P.bs_part, yF, flag);
   }
 }
 

@@ -209,7 +209,7 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   plan.nlev = nlev;
 
   std::vector<int2> panel, targets;
-  std::vector<int> kstart{0}, ks, bcols;
+  std::vector<int> kstart{0}, ks, bcols, gbeg{0};
   std::vector<int2> gather;
   plan.h_panel_off.assign(1, 0);
   plan.h_upd_off.assign(1, 0);
@@ -268,6 +268,7 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
       bcols.push_back(k);
       for (int i = k + 1; i < T; ++i)
         if (P[(long)i * T + k]) gather.push_back(make_int2(i, k));
+      gbeg.push_back((int)gather.size());   // column's gathers: [gbeg[b], gbeg[b+1])
     }
     plan.h_bs_off.push_back((int)bcols.size());
     plan.h_bsg_off.push_back((int)gather.size());
@@ -282,6 +283,8 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   plan.upd_ks = upload(ks, s);
   plan.bs_cols = upload(bcols, s);
   plan.bs_gather = upload(gather, s);
+  plan.bs_gbeg = upload(gbeg, s);
+  check(hipMalloc(&plan.bs_part, std::max<size_t>(gather.size(), 1) * 64 * sizeof(double)), "hipMalloc(bs_part)");
   plan.tile_id = upload(plan.h_tile_id, s);
   check(hipMalloc(&plan.ldiag, (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
   check(hipStreamSynchronize(s), "plan sync");
@@ -290,7 +293,7 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
 void llt_plan_free(LltPlan &plan) {
   for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
                   (void *)plan.upd_ks, (void *)plan.bs_cols, (void *)plan.bs_gather,
-                  (void *)plan.tile_id, (void *)plan.ldiag})
+                  (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.tile_id, (void *)plan.ldiag})
     if (p) (void)hipFree(p);
   plan = LltPlan{};
 }

@@ -75,6 +75,8 @@ struct LltPlan {
   int *upd_ks = nullptr;
   int *bs_cols = nullptr;       // backward-solve columns, root level first
   int2 *bs_gather = nullptr;    // (i,k) tiles gathered by each backward level, root level first
+  int *bs_gbeg = nullptr;       // [ncols+1] gather range of each backward column (bs_cols order)
+  double *bs_part = nullptr;    // [n_gather*64] per-gather partial sums L_ik^T y_i (summed in order)
   int *tile_id = nullptr;       // [T*T] compact index of tile (i,j), -1 if structurally zero
   std::vector<int> h_tile_id;
   long n_tiles = 0;             // tiles of the factor (compact storage = n_tiles * 4096 doubles)

@@ -47,6 +47,10 @@ struct Error : std::runtime_error {
       throw Error(ARSLAM_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(_r));       \
   } while (0)
 
+void fail_if(bool cond, int code, const std::string &msg) {
+  if (cond) throw Error(code, msg);
+}
+
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -180,10 +184,31 @@ struct arslam_lm {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
-  void allreduce(double *buf, size_t count, ncclRedOp_t op) {
-    if (!comm || nranks <= 1 || count == 0) return;
-    NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclDouble, op, comm, stream));
+  // host-callback transport (arslam_lm_set_comm_callback): stage through host memory
+  arslam_allreduce_fn comm_cb = nullptr;
+  void *comm_cb_ctx = nullptr;
+  std::vector<unsigned char> comm_stage;
+
+  // In-place all-reduce of a device buffer over the ranks (RCCL, or the
+  // caller's callback).  Every rank issues the same sequence of calls.
+  void allreduce_any(void *buf, size_t count, int dtype, int op) {
+    if (nranks <= 1 || count == 0) return;
+    const size_t bytes = count * (dtype == ARSLAM_DT_F64 ? sizeof(double) : 1);
+    if (comm_cb) {
+      comm_stage.resize(bytes);
+      HIP_CHECK(hipMemcpyAsync(comm_stage.data(), buf, bytes, hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+      fail_if(comm_cb(comm_cb_ctx, comm_stage.data(), count, dtype, op) != 0, ARSLAM_E_COMM,
+              "all-reduce callback failed");
+      HIP_CHECK(hipMemcpyAsync(buf, comm_stage.data(), bytes, hipMemcpyHostToDevice, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+      return;
+    }
+    fail_if(!comm, ARSLAM_E_STATE, "nranks > 1 without a communicator");
+    NCCL_CHECK(ncclAllReduce(buf, buf, count, dtype == ARSLAM_DT_F64 ? ncclDouble : ncclUint8,
+                             op == ARSLAM_OP_SUM ? ncclSum : ncclMax, comm, stream));
   }
+  void allreduce(double *buf, size_t count, int op) { allreduce_any(buf, count, ARSLAM_DT_F64, op); }
 
   void ensure_stream() {
     if (opt.device >= 0) HIP_CHECK(hipSetDevice(opt.device));
@@ -199,10 +224,6 @@ struct arslam_lm {
 };
 
 namespace {
-
-void fail_if(bool cond, int code, const std::string &msg) {
-  if (cond) throw Error(code, msg);
-}
 
 long round_up(long v, long m) { return (v + m - 1) / m * m; }
 
@@ -273,11 +294,11 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   std::vector<double> tag_deg(nt + 1, 0.0);
   for (int q = 0; q < nb; ++q) tag_deg[obs_tag[q]] += 1.0;
   tag_deg[nt] = nb;
-  if (comm && nranks > 1) {
+  if (nranks > 1) {
     DevBuf<double> tmp;
     tmp.alloc(nt + 1);
     tmp.upload(tag_deg.data(), nt + 1, stream);
-    allreduce(tmp.p, nt + 1, ncclSum);
+    allreduce(tmp.p, nt + 1, ARSLAM_OP_SUM);
     HIP_CHECK(hipMemcpyAsync(tag_deg.data(), tmp.p, (nt + 1) * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
   }
@@ -327,7 +348,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
         DevBuf<uint8_t> tmp;
         tmp.alloc(bm.size());
         tmp.upload(bm.data(), bm.size(), stream);
-        NCCL_CHECK(ncclAllReduce(tmp.p, tmp.p, bm.size(), ncclUint8, ncclMax, comm, stream));
+        allreduce_any(tmp.p, bm.size(), ARSLAM_DT_U8, ARSLAM_OP_MAX);
         HIP_CHECK(hipMemcpyAsync(bm.data(), tmp.p, bm.size(), hipMemcpyDeviceToHost, stream));
         HIP_CHECK(hipStreamSynchronize(stream));
         for (int a = 0; a < nt; ++a)
@@ -415,7 +436,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
         DevBuf<uint8_t> tmp;
         tmp.alloc(pattern.size());
         tmp.upload(pattern.data(), pattern.size(), stream);
-        NCCL_CHECK(ncclAllReduce(tmp.p, tmp.p, pattern.size(), ncclUint8, ncclMax, comm, stream));
+        allreduce_any(tmp.p, pattern.size(), ARSLAM_DT_U8, ARSLAM_OP_MAX);
         HIP_CHECK(hipMemcpyAsync(pattern.data(), tmp.p, pattern.size(), hipMemcpyDeviceToHost, stream));
         HIP_CHECK(hipStreamSynchronize(stream));
       }
@@ -452,7 +473,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   if (has_f) {
     d_S.alloc((size_t)plan.n_tiles * 4096);
     HIP_CHECK(hipMemsetAsync(d_S.p, 0, d_S.n * sizeof(double), stream));
-    d_z.alloc(2 * N);
+    d_z.alloc(N);
     d_yF.alloc(N);
   } else {
     d_S.release();
@@ -483,9 +504,9 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
   arslam::launch_reduce_parts(d_parts.p, nc, nullptr, 0, d_red.p, stream);
   if (nranks > 1) {
     const long t0 = 3 + 6L * nc;
-    allreduce(d_g.p + t0, n - t0, ncclSum);
-    allreduce(d_colnorm.p + t0, n - t0, ncclSum);
-    allreduce(d_red.p, 4, ncclSum);   // cost, fixed, g_f, col_f
+    allreduce(d_g.p + t0, n - t0, ARSLAM_OP_SUM);
+    allreduce(d_colnorm.p + t0, n - t0, ARSLAM_OP_SUM);
+    allreduce(d_red.p, 4, ARSLAM_OP_SUM);   // cost, fixed, g_f, col_f
   }
   arslam::launch_camera_slots(P, d_red.p, d_g.p, d_colnorm.p, stream);
   arslam::launch_slot_norms(P, d_g.p, x, d_norms.p, stream);
@@ -501,8 +522,8 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
     DevBuf<double> tmp;
     tmp.alloc(3);
     tmp.upload(cap_part, 3, stream);
-    allreduce(tmp.p, 1, ncclMax);
-    allreduce(tmp.p + 1, 2, ncclSum);
+    allreduce(tmp.p, 1, ARSLAM_OP_MAX);
+    allreduce(tmp.p + 1, 2, ARSLAM_OP_SUM);
     HIP_CHECK(hipMemcpyAsync(cap_part, tmp.p, 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
     norms[0] = cap_part[0]; norms[1] = cap_part[1]; norms[2] = cap_part[2];
@@ -626,7 +647,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       timers[PH_SCHUR].start(stream);
       arslam::launch_zero_tiles(plan, d_S.p, stream);
       arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream);
-      if (nranks > 1) allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ncclSum);
+      if (nranks > 1) allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ARSLAM_OP_SUM);
       arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
@@ -647,9 +668,9 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream);
     if (nranks > 1) {
       // model change, capture step^2, candidate cost, fixed; flags by max
-      allreduce(d_red.p + arslam::P_COST, 2, ncclSum);
-      allreduce(d_red.p + arslam::P_MODEL, 2, ncclSum);
-      allreduce(d_red.p + arslam::P_YBAD, 2, ncclMax);
+      allreduce(d_red.p + arslam::P_COST, 2, ARSLAM_OP_SUM);
+      allreduce(d_red.p + arslam::P_MODEL, 2, ARSLAM_OP_SUM);
+      allreduce(d_red.p + arslam::P_YBAD, 2, ARSLAM_OP_MAX);
     }
     timers[PH_COST].stop(stream);
     double red[16];
@@ -729,7 +750,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     DevBuf<double> tmp;
     tmp.alloc(1);
     tmp.upload(&v, 1, stream);
-    allreduce(tmp.p, 1, ncclSum);
+    allreduce(tmp.p, 1, ARSLAM_OP_SUM);
     HIP_CHECK(hipMemcpyAsync(&v, tmp.p, sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
     nb_all = (long)v;
@@ -978,13 +999,27 @@ int arslam_comm_unique_id(unsigned char id[ARSLAM_COMM_ID_BYTES]) {
   });
 }
 
+int arslam_lm_set_comm_callback(arslam_lm *h, int rank, int nranks, arslam_allreduce_fn fn, void *ctx) {
+  if (!h || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    if (h->comm) { (void)ncclCommDestroy(h->comm); h->comm = nullptr; }
+    h->rank = rank;
+    h->nranks = nranks;
+    h->comm_cb = nranks > 1 ? fn : nullptr;
+    h->comm_cb_ctx = ctx;
+    h->loaded = false;
+  });
+}
+
 int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks, const unsigned char id[ARSLAM_COMM_ID_BYTES]) {
   if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks) return ARSLAM_E_INVALID_ARG;
   return guarded([&] {
     h->ensure_stream();
     if (h->comm) { (void)ncclCommDestroy(h->comm); h->comm = nullptr; }
+    h->comm_cb = nullptr;
     h->rank = rank;
     h->nranks = nranks;
+    h->loaded = false;
     if (nranks > 1) {
       ncclUniqueId u;
       std::memcpy(&u, id, sizeof(u));

@@ -41,11 +41,12 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_add_residual_block", "arslam_lm_set_parameter_block_constant",
            "arslam_lm_set_parameter_block_variable", "arslam_lm_solve", "arslam_lm_reset",
            "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
-           "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm",
+           "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm", "arslam_lm_set_comm_callback",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt"]
 
 _dp = C.POINTER(C.c_double)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
 _ip = C.POINTER(C.c_int)
 _up = C.POINTER(C.c_ubyte)
 
@@ -136,6 +137,7 @@ def lib():
     L = C.CDLL(LIB_PATH)
     L.arslam_lm_options_init.argtypes = [C.POINTER(Options)]
     L.arslam_lm_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
+    L.arslam_lm_set_comm_callback.argtypes = [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, C.c_void_p]
     L.arslam_lm_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
     L.arslam_lm_get_options.argtypes = [C.c_void_p, C.POINTER(Options)]
     L.arslam_lm_destroy.argtypes = [C.c_void_p]
@@ -241,8 +243,25 @@ class _Handle:
         _check(lib().arslam_lm_get_options(self._h, C.byref(o)))
         return o
 
-    def set_comm(self, rank, nranks, uid: bytes):
-        _check(lib().arslam_lm_set_comm(self._h, rank, nranks, uid))
+    def set_comm(self, rank, nranks, uid):
+        """Join the ranks' exchange: ``uid`` is an RCCL unique id (bytes, one GPU per
+        rank) or a host all-reduce ``fn(array, op)`` reducing a numpy array in place
+        (op "sum" or "max"), e.g. over torch.distributed gloo."""
+        if callable(uid):
+            fn = uid
+
+            def tramp(ctx, buf, count, dtype, op):
+                try:
+                    ct = C.c_double if dtype == 0 else C.c_ubyte
+                    arr = np.ctypeslib.as_array(C.cast(buf, C.POINTER(ct)), shape=(count,))
+                    fn(arr, "sum" if op == 0 else "max")
+                    return 0
+                except Exception:   # noqa: BLE001 -- reported to the solver as a comm failure
+                    return 1
+            self._comm_cb = ALLREDUCE_FN(tramp)
+            _check(lib().arslam_lm_set_comm_callback(self._h, rank, nranks, self._comm_cb, None))
+        else:
+            _check(lib().arslam_lm_set_comm(self._h, rank, nranks, uid))
 
 
 def comm_unique_id() -> bytes:

@@ -189,6 +189,17 @@ int arslam_comm_unique_id(unsigned char id[ARSLAM_COMM_ID_BYTES]);
 int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks,
                        const unsigned char id[ARSLAM_COMM_ID_BYTES]);
 
+/* The same exchange through a caller-supplied host all-reduce (MPI, gloo,
+ * ...): the solver stages each device buffer to host memory, calls
+ * fn(ctx, buf, count, dtype, op) -- reduce `count` elements of `buf` in
+ * place over all ranks, return 0 on success -- and copies the result back.
+ * For ranks that share one GPU (RCCL needs one GPU per rank) and for tests.
+ * Like arslam_lm_set_comm, this drops a loaded problem (load again). */
+enum { ARSLAM_DT_F64 = 0, ARSLAM_DT_U8 = 1 };
+enum { ARSLAM_OP_SUM = 0, ARSLAM_OP_MAX = 1 };
+typedef int (*arslam_allreduce_fn)(void *ctx, void *buf, size_t count, int dtype, int op);
+int arslam_lm_set_comm_callback(arslam_lm *h, int rank, int nranks, arslam_allreduce_fn fn, void *ctx);
+
 /* Diagnostics */
 int arslam_device_count(void);
 const char *arslam_lm_last_error(void);

@@ -185,3 +185,24 @@ def test_sparse_plan_equals_dense_plan_on_same_order(lm):
     cs = [it["cost"] for it in sparse[3]["iterations"]]
     assert len(cd) == len(cs)
     np.testing.assert_allclose(cs, cd, rtol=1e-10)
+
+
+def test_cfg3_matches_golden_oracle_trace(lm):
+    """The headline workload (10k captures / 2k tags) against the oracle's committed trace
+    (tests/golden/lm_cfg3.json, made by make_golden.py; the oracle takes minutes here)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lm_cfg3.json")) as f:
+        gold = json.load(f)
+    g = synth.config_graph("cfg3")
+    cam, _, _, s = lm.solve_graph(g)
+    assert s["termination"] == gold["termination"] and s["rule"] == gold["rule"]
+    assert abs(s["num_linear_solves"] - gold["num_linear_solves"]) <= 1
+    costs = [it["cost"] for it in s["iterations"]]
+    for a, b in list(zip(costs, gold["cost"]))[:5]:
+        assert abs(a - b) <= 1e-9 * abs(b), (costs, gold["cost"])
+    np.testing.assert_allclose([it["trust_region_radius"] for it in s["iterations"]][:5],
+                               gold["trust_region_radius"][:5], rtol=1e-12)
+    assert abs(s["final_cost"] - gold["final_cost"]) <= 1e-8 * gold["final_cost"]
+    assert abs(cam[0] - gold["final_focal"]) <= 1e-8 * gold["final_focal"]
+    assert abs(s["final_rms_px"] - gold["final_rms_px"]) <= 1e-8 * gold["final_rms_px"]
