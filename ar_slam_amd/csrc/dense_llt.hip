@@ -310,44 +310,47 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, const int
   STAMP(4);
 }
 
-// Update targets of one level: tile (i,j) -= sum over the level's columns k
-// of L_ik L_jk^T.  One workgroup per target (no two workgroups write the same
-// tile); 4 waves x 32x32 on v_mfma_f64_16x16x4_f64, K = 64 per column.
+// Update items of one level: tile (i,j) -= sum over the item's columns k of
+// L_ik L_jk^T.  An unsplit target is one item (one workgroup writes the
+// tile); a split target's chunks each store their partial product to a slot
+// of `part`, and the chunk that arrives last sums the partials in chunk order
+// and writes the tile (agent-scope release / acquire hand-off: correct for
+// any placement of the chunks over XCDs).  4 waves x 32x32 on
+// v_mfma_f64_16x16x4_f64, K = 64 per column; the next column's operand
+// tiles are in flight while the current column's MFMAs run.
 __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const int *__restrict__ tid_map,
                                                 int T, const int2 *__restrict__ targets,
-                                                const int *__restrict__ kstart,
+                                                const int4 *__restrict__ items,
                                                 const int *__restrict__ ks,
+                                                const int2 *__restrict__ split,
+                                                double *__restrict__ part, int *__restrict__ cnt,
                                                 const int *__restrict__ flag) {
-  __shared__ __attribute__((aligned(16))) double sA[T64 * LM];
+  __shared__ __attribute__((aligned(16))) double sA[T64 * LM + 2];
   __shared__ __attribute__((aligned(16))) double sB[T64 * LM];
   if (*flag) return;
-  const int2 pr = targets[blockIdx.x];
+  const int4 it = items[blockIdx.x];
+  const int2 pr = targets[it.x];
   const int ti = pr.x, tj = pr.y;
-  const int q0 = kstart[blockIdx.x], q1 = kstart[blockIdx.x + 1];
+  const int q0 = it.y, q1 = it.z, sid = it.w;   // sid < 0: unsplit target
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
   const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
   const int li = lane & 15, lk = lane >> 4;
-  double *C = tile_ptr(S, tid_map, T, ti, tj);
-  double cval[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) cval[4 * q + reg] = C[(rb + lk + 4 * reg) * T64 + cb + li];
-  }
-  dbl4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
-  for (int q = q0; q < q1; ++q) {
+  dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+  dbl2 va[8], vb[8];
+  auto fetch = [&](int q) {
     const int k = ks[q];
     const double *Ai = tile_ptr(S, tid_map, T, ti, k);
     const double *Bj = tile_ptr(S, tid_map, T, tj, k);
-    dbl2 va[8], vb[8];
 #pragma unroll
     for (int e8 = 0; e8 < 8; ++e8) {
       const int e = e8 * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
       va[e8] = *reinterpret_cast<const dbl2 *>(Ai + r * T64 + c2);
       vb[e8] = *reinterpret_cast<const dbl2 *>(Bj + r * T64 + c2);
     }
+  };
+  if (q0 < q1) fetch(q0);
+  for (int q = q0; q < q1; ++q) {
     if (q > q0) __syncthreads();   // previous column's fragments consumed
 #pragma unroll
     for (int e8 = 0; e8 < 8; ++e8) {
@@ -356,6 +359,7 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
       *reinterpret_cast<dbl2 *>(&sB[r * LM + c2]) = vb[e8];
     }
     __syncthreads();
+    if (q + 1 < q1) fetch(q + 1);
 #pragma unroll 4
     for (int kk = 0; kk < T64 / 4; ++kk) {
       const int kc = kk * 4 + lk;
@@ -363,21 +367,63 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
       const double a1 = sA[(r0 + 16 + li) * LM + kc];
       const double b0 = sB[(c0 + li) * LM + kc];
       const double b1 = sB[(c0 + 16 + li) * LM + kc];
-      acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+    }
+  }
+  if (sid >= 0) {
+    // split target (sid = split id << 8 | chunk): publish this chunk's partial
+    // (fragment order, lane-contiguous 16-B stores), draw a ticket; the last
+    // arriver sums every chunk's partial in chunk order
+    const int2 sp = split[sid >> 8];   // {n_chunks, first slot}
+    dbl2 *mine = reinterpret_cast<dbl2 *>(part + (long)(sp.y + (sid & 255)) * 4096);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      mine[(2 * q) * 256 + tid] = dbl2{acc[q][0], acc[q][1]};
+      mine[(2 * q + 1) * 256 + tid] = dbl2{acc[q][2], acc[q][3]};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *is_last = reinterpret_cast<int *>(&sA[T64 * LM]);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(cnt + (sid >> 8), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *is_last = old == sp.x - 1;
+      if (old == sp.x - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!*is_last) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = dbl4{0, 0, 0, 0};
+    for (int c = 0; c < sp.x; ++c) {
+      const dbl2 *pc = reinterpret_cast<const dbl2 *>(part + (long)(sp.y + c) * 4096);
+      dbl2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pc[u * 256 + tid];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[q][0] += v[2 * q].x;
+        acc[q][1] += v[2 * q].y;
+        acc[q][2] += v[2 * q + 1].x;
+        acc[q][3] += v[2 * q + 1].y;
+      }
     }
   }
   // f64 MFMA C/D layout: col = lane & 15, row = (lane >> 4) + 4 * reg
-  const dbl4 accs[4] = {acc00, acc01, acc10, acc11};
+  double *C = tile_ptr(S, tid_map, T, ti, tj);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int row = rb + lk + 4 * reg, col = cb + li;
-      C[row * T64 + col] = cval[4 * q + reg] - accs[q][reg];
+      C[row * T64 + col] -= acc[q][reg];
     }
   }
 }
@@ -444,7 +490,14 @@ __global__ __launch_bounds__(64) void k_bs_solve(const double *__restrict__ Ld, 
   const long row0 = (long)k * T64;
   load_tile64(Ld + (long)k * T64 * T64, T64, Lk, lane);
   double acc = 0.0;
-  for (int g = gbeg[blockIdx.x]; g < gbeg[blockIdx.x + 1]; ++g) acc += part[(long)g * T64 + lane];
+  const int ga = gbeg[blockIdx.x], gb = gbeg[blockIdx.x + 1];
+  for (int g = ga; g < gb; g += 8) {   // 8 loads in flight, summed in plan order
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (g + u < gb) ? part[(long)(g + u) * T64 + lane] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
   double zr = (row0 + lane < nR) ? z[row0 + lane] - acc : 0.0;
   __syncthreads();
   const double my_inv = (row0 + lane < nR) ? 1.0 / Lk[lane * LP + lane] : 0.0;   // y = 0 past nR
@@ -490,16 +543,17 @@ void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s) {
 }
 
 void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, LaunchTiming *timing) {
+  if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
   for (int l = 0; l < P.nlev; ++l) {
     const int np = P.h_panel_off[l + 1] - P.h_panel_off[l];
     hipLaunchKernelGGL(k_panel, dim3((unsigned)np), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag,
                        P.panel + P.h_panel_off[l], flag);
-    const int nu = P.h_upd_off[l + 1] - P.h_upd_off[l];
-    if (nu > 0) {
+    const int ni = P.h_item_off[l + 1] - P.h_item_off[l];
+    if (ni > 0) {
       const bool rec = timing && timing->used < timing->cap;
       if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
-      hipLaunchKernelGGL(k_update, dim3((unsigned)nu), dim3(256), 0, s, S, P.tile_id, P.T,
-                         P.upd_targets + P.h_upd_off[l], P.upd_kstart + P.h_upd_off[l], P.upd_ks, flag);
+      hipLaunchKernelGGL(k_update, dim3((unsigned)ni), dim3(256), 0, s, S, P.tile_id, P.T, P.upd_targets,
+                         P.upd_items + P.h_item_off[l], P.upd_ks, P.upd_split, P.upd_part, P.upd_cnt, flag);
       if (rec) {
         (void)hipEventRecord(timing->ev[2 * timing->used + 1], s);
         timing->used++;

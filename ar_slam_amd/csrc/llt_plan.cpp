@@ -9,6 +9,9 @@
 //  3. a level schedule of the tile elimination tree: tile columns of equal
 //     height are independent and are factored in one launch, their updates
 //     applied in one launch; the backward solve walks the levels in reverse.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include "lm_internal.h"
 
 #include <algorithm>
@@ -174,6 +177,8 @@ std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>
   return d.parts;
 }
 
+constexpr int kSplitMin = 6;   // k-lists longer than this are split
+
 void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hipStream_t s) {
   llt_plan_free(plan);
   plan.T = T;
@@ -210,6 +215,9 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
 
   std::vector<int2> panel, targets;
   std::vector<int> kstart{0}, ks, bcols, gbeg{0};
+  std::vector<int4> items;
+  std::vector<int2> split;
+  plan.h_item_off.assign(1, 0);
   std::vector<int2> gather;
   plan.h_panel_off.assign(1, 0);
   plan.h_upd_off.assign(1, 0);
@@ -251,14 +259,42 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
           plan.total_upd_tiles++;
         }
     }
+    std::vector<int4> litems;
     for (size_t t = 0; t < lt.size(); ++t) {
       tgt_id[(long)lt[t].x * T + lt[t].y] = -1;
+      const int tg = (int)targets.size(), q0 = (int)ks.size();
       targets.push_back(lt[t]);
       ks.insert(ks.end(), lks[t].begin(), lks[t].end());
       kstart.push_back((int)ks.size());
+      // split a long k-list into ~sqrt(m) chunks: chunk GEMMs run in parallel,
+      // the last arriver reads ~sqrt(m) partial tiles
+      const int m = (int)lks[t].size();
+      if (m > kSplitMin) {
+        int nch = std::min(255, (int)std::ceil(std::sqrt((double)m)));
+        const int ch = (m + nch - 1) / nch;
+        nch = (m + ch - 1) / ch;
+        const int sid = (int)split.size();
+        split.push_back(make_int2(nch, (int)plan.n_part));
+        plan.n_part += nch;
+        for (int c = 0; c < nch; ++c)
+          litems.push_back(make_int4(tg, q0 + c * ch, std::min(q0 + (c + 1) * ch, q0 + m), sid * 256 + c));
+      } else {
+        litems.push_back(make_int4(tg, q0, q0 + m, -1));
+      }
     }
+    // longest items first (they bound the launch)
+    std::stable_sort(litems.begin(), litems.end(),
+                     [](const int4 &a, const int4 &b) { return a.z - a.y > b.z - b.y; });
+    items.insert(items.end(), litems.begin(), litems.end());
+    plan.h_item_off.push_back((int)items.size());
     plan.h_upd_off.push_back((int)targets.size());
     plan.h_upd_flops.push_back(fl);
+    if (std::getenv("ARSLAM_PLAN_STATS")) {
+      size_t mx = 0, tot = 0;
+      for (size_t t = 0; t < lt.size(); ++t) { mx = std::max(mx, lks[t].size()); tot += lks[t].size(); }
+      std::fprintf(stderr, "level %d: panel %d targets %zu ks %zu max_ks %zu\n", l,
+                   plan.h_panel_off[l + 1] - plan.h_panel_off[l], lt.size(), tot, mx);
+    }
     plan.total_upd_flops += fl;
   }
   // backward solve: levels from the root down; each column gathers from its
@@ -281,6 +317,11 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   plan.upd_targets = upload(targets, s);
   plan.upd_kstart = upload(kstart, s);
   plan.upd_ks = upload(ks, s);
+  plan.upd_items = upload(items, s);
+  plan.upd_split = upload(split, s);
+  plan.n_split = (long)split.size();
+  check(hipMalloc(&plan.upd_cnt, std::max<size_t>(split.size(), 1) * sizeof(int)), "hipMalloc(upd_cnt)");
+  check(hipMalloc(&plan.upd_part, std::max<long>(plan.n_part, 1) * 4096 * sizeof(double)), "hipMalloc(upd_part)");
   plan.bs_cols = upload(bcols, s);
   plan.bs_gather = upload(gather, s);
   plan.bs_gbeg = upload(gbeg, s);
@@ -292,7 +333,8 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
 
 void llt_plan_free(LltPlan &plan) {
   for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
-                  (void *)plan.upd_ks, (void *)plan.bs_cols, (void *)plan.bs_gather,
+                  (void *)plan.upd_ks, (void *)plan.upd_items, (void *)plan.upd_split,
+                  (void *)plan.upd_cnt, (void *)plan.upd_part, (void *)plan.bs_cols, (void *)plan.bs_gather,
                   (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.tile_id, (void *)plan.ldiag})
     if (p) (void)hipFree(p);
   plan = LltPlan{};

@@ -73,6 +73,15 @@ struct LltPlan {
   int2 *upd_targets = nullptr;  // (i,j) tiles updated by a level
   int *upd_kstart = nullptr;    // CSR over targets of the contributing columns k
   int *upd_ks = nullptr;
+  // work items of the update launches: {target, q0, q1, split} -- a target with
+  // a long k-list is split into chunks whose partial products go to upd_part
+  // and are summed in chunk order by the last-arriving chunk (deterministic)
+  int4 *upd_items = nullptr;
+  int2 *upd_split = nullptr;    // [n_split] {n_chunks, first partial slot}
+  int *upd_cnt = nullptr;       // [n_split] arrival counters (zeroed per factorization)
+  double *upd_part = nullptr;   // [n_part * 4096]
+  long n_split = 0, n_part = 0;
+  std::vector<int> h_item_off;      // [nlev+1]
   int *bs_cols = nullptr;       // backward-solve columns, root level first
   int2 *bs_gather = nullptr;    // (i,k) tiles gathered by each backward level, root level first
   int *bs_gbeg = nullptr;       // [ncols+1] gather range of each backward column (bs_cols order)

@@ -465,6 +465,8 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_parts.alloc((size_t)arslam::NPART * std::max(nc, 1));
   n_fparts = (int)((std::max(nR, 1L) + 255) / 256);
   d_fparts.alloc(2L * std::max(n_fparts, 1));
+  // stays zero when there are no reduced rows (k_update_f is then not launched)
+  HIP_CHECK(hipMemsetAsync(d_fparts.p, 0, d_fparts.n * sizeof(double), stream));
   d_red.alloc(16);
   d_norms.alloc(8);
   d_flag.alloc(1);
