@@ -105,3 +105,37 @@ extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double
   (void)hipFree(d_flag);
   return ARSLAM_OK;
 }
+
+extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
+                                         arslam_plan_info *info, int *tag_row) {
+  if (!p || !info || ordering < 0 || ordering > 2) return ARSLAM_E_INVALID_ARG;
+  try {
+    std::memset(info, 0, sizeof(*info));
+    const arslam::HostProblem h = arslam::host_problem(p, nullptr);
+    arslam::ReducedLayout L = arslam::reduced_layout(h, ordering, skip_zero_tiles != 0, nullptr, nullptr);
+    info->n_reduced = L.nR;
+    info->n_padded = L.N;
+    info->pad_rows = L.pad_rows;
+    info->tiles_per_side = L.T;
+    info->n_parts = L.n_parts;
+    info->camera_row = L.cam_row;
+    if (tag_row)
+      for (int t = 0; t < h.nt; ++t) tag_row[t] = L.tag_row[t];
+    if (L.nR > 0) {
+      arslam::LltPlan plan;
+      arslam::llt_plan_symbolic(plan, L.T, L.N, L.pattern);
+      info->n_levels = plan.nlev;
+      info->n_assembled_tiles = plan.n_assembled;
+      info->n_factor_tiles = plan.n_tiles;
+      info->n_update_tiles = plan.total_upd_tiles;
+      info->n_update_items = (long)plan.h_items.size();
+      info->n_split_targets = (long)plan.h_split.size();
+      info->update_flops = plan.total_upd_flops;
+    }
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}

@@ -494,9 +494,9 @@ __global__ __launch_bounds__(64) void k_bs_solve(const double *__restrict__ Ld, 
   for (int g = ga; g < gb; g += 8) {   // 8 loads in flight, summed in plan order
     double v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (g + u < gb) ? part[(long)(g + u) * T64 + lane] : 0.0;
+    for (int u = 0; u < 8; ++u) v[u] = part[(long)min(g + u, gb - 1) * T64 + lane];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc += v[u];
+    for (int u = 0; u < 8; ++u) acc += (g + u < gb) ? v[u] : 0.0;
   }
   double zr = (row0 + lane < nR) ? z[row0 + lane] - acc : 0.0;
   __syncthreads();

@@ -1,0 +1,481 @@
+// host_structure.cpp -- host-only problem structure and reduced-system
+// layout (see host_structure.h).  Restates the parameter-block bookkeeping of
+// ceres::Problem as ar_slam builds it (AddResidualBlock, ar_slam_util.cpp:
+// 720-727, 829-836, 956-963; SetParameterBlockConstant, :965, :972) and the
+// DENSE_SCHUR split (captures eliminated, tags + camera reduced).
+#include "host_structure.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+
+namespace arslam {
+
+namespace {
+
+long round_up(long v, long m) { return (v + m - 1) / m * m; }
+
+// BFS over `mark == tag` nodes from start; fills level of each visited node
+// (-1 unvisited) and returns the visit order.
+std::vector<int> bfs(int start, const std::vector<std::vector<int>> &adj, const std::vector<int> &mark,
+                     int tag, std::vector<int> &lev) {
+  std::vector<int> order{start};
+  lev[start] = 0;
+  for (size_t h = 0; h < order.size(); ++h) {
+    const int u = order[h];
+    for (int v : adj[u])
+      if (mark[v] == tag && lev[v] < 0) {
+        lev[v] = lev[u] + 1;
+        order.push_back(v);
+      }
+  }
+  return order;
+}
+
+// pseudo-peripheral node of the component of `start` (George-Liu)
+int peripheral(int start, const std::vector<std::vector<int>> &adj, const std::vector<int> &mark,
+               int tag, std::vector<int> &lev) {
+  int best = start, depth = -1;
+  for (int it = 0; it < 6; ++it) {
+    const std::vector<int> ord = bfs(best, adj, mark, tag, lev);
+    const int d = lev[ord.back()];
+    int far = ord.back();
+    for (int u : ord)   // among the last level, the one of least degree
+      if (lev[u] == d && adj[u].size() < adj[far].size()) far = u;
+    for (int u : ord) lev[u] = -1;
+    if (d <= depth) break;
+    depth = d;
+    best = far;
+  }
+  return best;
+}
+
+struct Dissector {
+  const std::vector<std::vector<int>> &adj;
+  const std::vector<double> &xyz;   // optional 3-D embedding (tag positions), 3 per node
+  int leaf;
+  std::vector<int> mark, lev;
+  int next_tag = 1;
+  std::vector<std::vector<int>> parts;   // elimination order
+
+  Dissector(const std::vector<std::vector<int>> &a, const std::vector<double> &coords, int leaf_size)
+      : adj(a), xyz(coords), leaf(leaf_size), mark(a.size(), 0), lev(a.size(), -1) {}
+
+  // nodes: all with mark == tag
+  void run(std::vector<int> nodes, int tag) {
+    if (nodes.empty()) return;
+    // split into connected components
+    std::vector<std::vector<int>> comps;
+    for (int u : nodes) {
+      if (lev[u] >= 0) continue;
+      std::vector<int> c = bfs(u, adj, mark, tag, lev);
+      comps.push_back(std::move(c));
+    }
+    for (int u : nodes) lev[u] = -1;
+    for (auto &c : comps) dissect(c, tag);
+  }
+
+  // BFS-level separator: the level that balances the two sides
+  bool level_separator(std::vector<int> &comp, int tag, std::vector<int> &A, std::vector<int> &B,
+                       std::vector<int> &S) {
+    const int s = peripheral(comp[0], adj, mark, tag, lev);
+    std::vector<int> ord = bfs(s, adj, mark, tag, lev);
+    const int depth = lev[ord.back()];
+    if (depth < 2) {
+      for (int u : ord) lev[u] = -1;
+      return false;
+    }
+    std::vector<int> cnt(depth + 1, 0);
+    for (int u : ord) cnt[lev[u]]++;
+    int sep = 1, acc = cnt[0];
+    const int half = (int)ord.size() / 2;
+    while (sep < depth - 1 && acc + cnt[sep] / 2 < half) acc += cnt[sep++];
+    for (int u : ord) {
+      if (lev[u] < sep) A.push_back(u);
+      else if (lev[u] > sep) B.push_back(u);
+      else S.push_back(u);
+    }
+    for (int u : ord) lev[u] = -1;
+    return true;
+  }
+
+  // Geometric separator: cut the component by a plane normal to one of its
+  // principal axes at a quantile of the projections; the separator is the
+  // smaller one-sided boundary of the cut edges.  The best (smallest, then
+  // most balanced) of several cuts is kept.
+  bool geometric_separator(std::vector<int> &comp, int tag, std::vector<int> &A, std::vector<int> &B,
+                           std::vector<int> &S) {
+    const int m = (int)comp.size();
+    double c[3] = {0, 0, 0}, C[9] = {0};
+    for (int u : comp)
+      for (int a = 0; a < 3; ++a) c[a] += xyz[3L * u + a] / m;
+    for (int u : comp)
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) C[3 * a + b] += (xyz[3L * u + a] - c[a]) * (xyz[3L * u + b] - c[b]);
+    // two leading principal axes by power iteration with deflation
+    double axes[2][3];
+    double D[9];
+    std::copy(C, C + 9, D);
+    for (int k = 0; k < 2; ++k) {
+      double v[3] = {1.0, 0.7, 0.3};
+      double lam = 0.0;
+      for (int it = 0; it < 100; ++it) {
+        double w[3];
+        for (int a = 0; a < 3; ++a) w[a] = D[3 * a] * v[0] + D[3 * a + 1] * v[1] + D[3 * a + 2] * v[2];
+        const double nw = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        if (nw == 0.0) break;
+        for (int a = 0; a < 3; ++a) v[a] = w[a] / nw;
+        lam = nw;
+      }
+      for (int a = 0; a < 3; ++a) axes[k][a] = v[a];
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) D[3 * a + b] -= lam * v[a] * v[b];
+    }
+    std::vector<int> side(adj.size(), 0);
+    std::vector<std::pair<double, int>> pr(m);
+    long best_score = -1;
+    std::vector<int> best_side;
+    for (int k = 0; k < 2; ++k) {
+      for (int i = 0; i < m; ++i) {
+        const int u = comp[i];
+        pr[i] = {axes[k][0] * xyz[3L * u] + axes[k][1] * xyz[3L * u + 1] + axes[k][2] * xyz[3L * u + 2], u};
+      }
+      std::sort(pr.begin(), pr.end());
+      for (int qi = 6; qi <= 14; ++qi) {   // cut at quantiles 0.30 .. 0.70
+        const int cut = m * qi / 20;
+        if (cut < 1 || cut >= m) continue;
+        for (int i = 0; i < m; ++i) side[pr[i].second] = i < cut ? 1 : 2;
+        // one-sided boundaries
+        int sa = 0, sb = 0;
+        for (int u : comp) {
+          bool bd = false;
+          for (int v : adj[u])
+            if (mark[v] == tag && side[v] != side[u]) { bd = true; break; }
+          if (bd) (side[u] == 1 ? sa : sb)++;
+        }
+        const int sep_side = sa <= sb ? 1 : 2;
+        const int ssz = std::min(sa, sb);
+        const int na = cut - (sep_side == 1 ? ssz : 0), nbb = m - cut - (sep_side == 2 ? ssz : 0);
+        if (std::min(na, nbb) < m / 5) continue;
+        const long score = (long)ssz * 4 * m + std::abs(na - nbb);
+        if (best_score < 0 || score < best_score) {
+          best_score = score;
+          best_side.assign(m, 0);
+          for (int i = 0; i < m; ++i) {
+            const int u = comp[i];
+            bool bd = false;
+            if (side[u] == sep_side)
+              for (int v : adj[u])
+                if (mark[v] == tag && side[v] != side[u]) { bd = true; break; }
+            best_side[i] = bd ? 0 : side[u];
+          }
+        }
+      }
+    }
+    for (int u : comp) side[u] = 0;
+    if (best_score < 0) return false;
+    for (int i = 0; i < m; ++i) (best_side[i] == 1 ? A : best_side[i] == 2 ? B : S).push_back(comp[i]);
+    return true;
+  }
+
+  void dissect(std::vector<int> &comp, int tag) {
+    if ((int)comp.size() <= leaf) {
+      leaf_part(comp, tag);
+      return;
+    }
+    std::vector<int> A, B, S;
+    bool ok = false;
+    if (!xyz.empty()) {
+      ok = geometric_separator(comp, tag, A, B, S);
+      std::vector<int> A2, B2, S2;
+      if (level_separator(comp, tag, A2, B2, S2) && (!ok || S2.size() < S.size())) {
+        A.swap(A2); B.swap(B2); S.swap(S2);
+        ok = true;
+      }
+    } else {
+      ok = level_separator(comp, tag, A, B, S);
+    }
+    if (!ok) {
+      leaf_part(comp, tag);
+      return;
+    }
+    absorb(A, B, S, tag);
+    const int ta = ++next_tag, tb = ++next_tag, ts = ++next_tag;
+    for (int u : A) mark[u] = ta;
+    for (int u : B) mark[u] = tb;
+    for (int u : S) mark[u] = ts;
+    run(A, ta);
+    run(B, tb);
+    parts.push_back(S);
+  }
+
+  // Grow the separator into the larger side (nodes adjacent to it first) until
+  // its 6 rows per tag fill whole 64-row tiles: rows that would otherwise be
+  // alignment padding become separator rows, and the children shrink.  Any
+  // superset of a separator taken from one side still separates.
+  void absorb(std::vector<int> &A, std::vector<int> &B, std::vector<int> &S, int tag) {
+    const long rows = 6L * (long)S.size();
+    int extra = (int)((round_up(rows, kTileRows) - rows) / 6);
+    std::vector<int> &X = A.size() >= B.size() ? A : B;
+    if (extra <= 0 || (int)X.size() <= extra) return;
+    const int tx = ++next_tag;
+    for (int u : X) mark[u] = tx;
+    std::vector<char> take(adj.size(), 0);
+    std::vector<int> frontier;
+    for (int u : S)
+      for (int v : adj[u])
+        if (mark[v] == tx && !take[v] && extra > 0) { take[v] = 1; frontier.push_back(v); --extra; }
+    for (size_t h = 0; h < frontier.size() && extra > 0; ++h)
+      for (int v : adj[frontier[h]])
+        if (mark[v] == tx && !take[v] && extra > 0) { take[v] = 1; frontier.push_back(v); --extra; }
+    std::vector<int> keep;
+    for (int u : X) (take[u] ? S : keep).push_back(u);
+    for (int u : X) mark[u] = tag;
+    X.swap(keep);
+  }
+
+  void leaf_part(std::vector<int> &comp, int tag) {
+    // within a leaf keep BFS order (locality)
+    std::vector<int> ord = bfs(comp[0], adj, mark, tag, lev);
+    for (int u : ord) lev[u] = -1;
+    parts.push_back(ord);
+  }
+};
+
+}  // namespace
+
+std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj) {
+  std::vector<int> order;
+  order.reserve(n);
+  std::vector<int> mark(n, 0), lev(n, -1);
+  std::vector<char> done(n, 0);
+  for (;;) {
+    int start = -1;
+    for (int v = 0; v < n; ++v)
+      if (!done[v] && (start < 0 || adj[v].size() < adj[start].size())) start = v;
+    if (start < 0) break;
+    start = peripheral(start, adj, mark, 0, lev);
+    std::deque<int> q{start};
+    done[start] = 1;
+    while (!q.empty()) {
+      const int u = q.front();
+      q.pop_front();
+      order.push_back(u);
+      std::vector<int> nb;
+      for (int v : adj[u])
+        if (!done[v]) { done[v] = 1; nb.push_back(v); }
+      std::stable_sort(nb.begin(), nb.end(),
+                       [&](int a, int b) { return adj[a].size() < adj[b].size(); });
+      for (int v : nb) q.push_back(v);
+    }
+  }
+  std::reverse(order.begin(), order.end());
+  return order;
+}
+
+std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf,
+                                       const std::vector<double> &xyz) {
+  Dissector d(adj, xyz, leaf);
+  std::vector<int> all(n);
+  for (int i = 0; i < n; ++i) all[i] = i;
+  d.run(all, 0);
+  return d.parts;
+}
+
+
+HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum) {
+  api_check(p != nullptr, ARSLAM_E_INVALID_ARG, "null problem");
+  api_check(p->n_cap >= 0 && p->n_tag >= 0 && p->n_obs >= 0, ARSLAM_E_INVALID_ARG, "negative sizes");
+  api_check(p->camera && (!p->n_cap || p->cap) && (!p->n_tag || p->tag), ARSLAM_E_INVALID_ARG,
+            "null parameter arrays");
+  api_check(!p->n_obs || (p->obs_cap && p->obs_tag && p->corners), ARSLAM_E_INVALID_ARG,
+            "null observation arrays");
+  HostProblem h;
+  const int nc = h.nc = p->n_cap, nt = h.nt = p->n_tag, nb = h.nb = p->n_obs;
+  const long n = h.n = 3 + 6L * nc + 6L * nt;
+  // capture-major observation order (stable)
+  h.cap_start.assign(nc + 1, 0);
+  for (int b = 0; b < nb; ++b) {
+    api_check(p->obs_cap[b] >= 0 && p->obs_cap[b] < nc, ARSLAM_E_INVALID_ARG, "obs_cap out of range");
+    api_check(p->obs_tag[b] >= 0 && p->obs_tag[b] < nt, ARSLAM_E_INVALID_ARG, "obs_tag out of range");
+    h.cap_start[p->obs_cap[b] + 1]++;
+  }
+  for (int c = 0; c < nc; ++c) {
+    h.maxk = std::max(h.maxk, h.cap_start[c + 1]);
+    h.cap_start[c + 1] += h.cap_start[c];
+  }
+  api_check(h.maxk <= kMaxObsPerCapture, ARSLAM_E_UNSUPPORTED, "more than 64 observations in one capture");
+  std::vector<int> order(nb);
+  {
+    std::vector<int> fill(h.cap_start.begin(), h.cap_start.end() - 1);
+    for (int b = 0; b < nb; ++b) order[fill[p->obs_cap[b]]++] = b;
+  }
+  h.obs_tag.resize(nb);
+  h.obs_lblk.resize(nb);
+  h.cap_blk_start.assign(nc + 1, 0);
+  h.corners.resize(8L * nb);
+  h.blk_tag.reserve(nb);
+  for (int c = 0; c < nc; ++c) {
+    h.cap_blk_start[c] = (int)h.blk_tag.size();
+    for (int q = h.cap_start[c]; q < h.cap_start[c + 1]; ++q) {
+      const int b = order[q];
+      const int t = p->obs_tag[b];
+      h.obs_tag[q] = t;
+      std::memcpy(&h.corners[8L * q], p->corners + 8L * b, 8 * sizeof(double));
+      int u = -1;
+      for (int i = h.cap_blk_start[c]; i < (int)h.blk_tag.size(); ++i)
+        if (h.blk_tag[i] == t) { u = i - h.cap_blk_start[c]; break; }
+      if (u < 0) { u = (int)h.blk_tag.size() - h.cap_blk_start[c]; h.blk_tag.push_back(t); }
+      h.obs_lblk[q] = u + 1;
+    }
+  }
+  h.cap_blk_start[nc] = (int)h.blk_tag.size();
+  // tag CSR over the capture-major order
+  h.tag_start.assign(nt + 1, 0);
+  h.tag_obs.resize(nb);
+  for (int q = 0; q < nb; ++q) h.tag_start[h.obs_tag[q] + 1]++;
+  for (int t = 0; t < nt; ++t) h.tag_start[t + 1] += h.tag_start[t];
+  {
+    std::vector<int> fill(h.tag_start.begin(), h.tag_start.end() - 1);
+    for (int q = 0; q < nb; ++q) h.tag_obs[fill[h.obs_tag[q]]++] = q;
+  }
+  // free slots (global tag use over ranks)
+  std::vector<double> tag_deg(nt + 1, 0.0);
+  for (int q = 0; q < nb; ++q) tag_deg[h.obs_tag[q]] += 1.0;
+  tag_deg[nt] = nb;
+  if (tag_deg_sum) tag_deg_sum(tag_deg);
+  h.nb_global = (long)tag_deg[nt];
+  h.slot_free.assign(n, 0);
+  const bool cam_free = !p->camera_const && tag_deg[nt] > 0;
+  for (int j = 0; j < 3; ++j) h.slot_free[j] = cam_free;
+  for (int c = 0; c < nc; ++c) {
+    const bool f = h.cap_start[c + 1] > h.cap_start[c] && !(p->cap_const && p->cap_const[c]);
+    for (int j = 0; j < 6; ++j) h.slot_free[3 + 6L * c + j] = f;
+  }
+  for (int t = 0; t < nt; ++t) {
+    const bool f = tag_deg[t] > 0 && !(p->tag_const && p->tag_const[t]);
+    for (int j = 0; j < 6; ++j) h.slot_free[3 + 6L * nc + 6L * t + j] = f;
+  }
+  h.obs_active.resize(nb);
+  for (int q = 0; q < nb; ++q) {
+    const int c = p->obs_cap[order[q]];
+    h.obs_active[q] = h.slot_free[0] || h.slot_free[3 + 6L * c] || h.slot_free[3 + 6L * nc + 6L * h.obs_tag[q]];
+  }
+  h.x0.resize(n);
+  std::memcpy(h.x0.data(), p->camera, 3 * sizeof(double));
+  if (nc) std::memcpy(h.x0.data() + 3, p->cap, 6L * nc * sizeof(double));
+  if (nt) std::memcpy(h.x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
+  return h;
+}
+
+ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
+                             const ReduceMaxU8 &pattern_max) {
+  // Rows exist only for free tags and a free camera (constant / unused blocks
+  // are not parameters).  Tags are ordered natural, RCM or by nested
+  // dissection; with ND every part starts on a tile boundary so the tile
+  // elimination tree follows the dissection tree.
+  const int nc = h.nc, nt = h.nt;
+  ReducedLayout L;
+  L.tag_row.assign(std::max(nt, 1), -1);
+  std::vector<char> tfree(nt, 0);
+  for (int t = 0; t < nt; ++t) tfree[t] = h.slot_free[3 + 6L * nc + 6L * t];
+  std::vector<std::vector<int>> adj(nt);
+  if (ordering != 0 && nt > 1) {
+    if (adj_max) {   // co-visibility is global over ranks
+      api_check(nt <= 16384, ARSLAM_E_UNSUPPORTED, "multi-GPU reduced ordering limited to 16384 tags");
+      std::vector<uint8_t> bm((size_t)nt * nt, 0);
+      for (int c = 0; c < nc; ++c)
+        for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a)
+          for (int b = h.cap_blk_start[c]; b < h.cap_blk_start[c + 1]; ++b)
+            if (a != b) bm[(size_t)h.blk_tag[a] * nt + h.blk_tag[b]] = 1;
+      adj_max(bm);
+      for (int a = 0; a < nt; ++a)
+        for (int b = 0; b < nt; ++b)
+          if (bm[(size_t)a * nt + b] && tfree[a] && tfree[b]) adj[a].push_back(b);
+    } else {
+      for (int c = 0; c < nc; ++c)
+        for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a)
+          for (int b = h.cap_blk_start[c]; b < h.cap_blk_start[c + 1]; ++b)
+            if (a != b && tfree[h.blk_tag[a]] && tfree[h.blk_tag[b]]) adj[h.blk_tag[a]].push_back(h.blk_tag[b]);
+      for (auto &v : adj) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+      }
+    }
+  }
+  std::vector<std::vector<int>> parts;
+  if (ordering == 2 && nt > 1) {
+    // tag positions (initial values) embed the co-visibility graph for geometric separators
+    std::vector<double> xyz(3L * nt);
+    for (int t = 0; t < nt; ++t)
+      for (int a = 0; a < 3; ++a) xyz[3L * t + a] = h.x0[3 + 6L * nc + 6L * t + a];
+    // leaves of up to 32 tags (192 rows = 3 whole tiles): a smaller dissection
+    // would not shorten the elimination tree, only add padding and parts
+    parts = nd_parts(nt, adj, 32, xyz);
+  } else {
+    std::vector<int> order;
+    if (ordering == 1 && nt > 1) order = rcm_order(nt, adj);
+    else for (int t = 0; t < nt; ++t) order.push_back(t);
+    parts.push_back(order);
+  }
+  long row = 0, real = 0;
+  for (auto &part : parts) {
+    bool any = false;
+    for (int t : part) any = any || tfree[t];
+    if (!any) continue;
+    L.n_parts++;
+    if (ordering == 2) row = round_up(row, kTileRows);
+    for (int t : part) {
+      if (!tfree[t]) continue;
+      L.tag_row[t] = (int)row;
+      row += 6;
+      real += 6;
+    }
+  }
+  L.pad_rows = row - real;
+  L.row_slot.assign(row, -1);
+  for (int t = 0; t < nt; ++t)
+    if (L.tag_row[t] >= 0)
+      for (int j = 0; j < 6; ++j) L.row_slot[L.tag_row[t] + j] = (int)(3 + 6L * nc + 6L * t + j);
+  if (h.slot_free[0]) {
+    L.cam_row = (int)row;
+    for (int j = 0; j < 3; ++j) L.row_slot.push_back(j);
+    row += 3;
+  }
+  L.nR = row;
+  if (L.nR == 0) return L;
+  L.N = round_up(L.nR + 1, kTileRows);
+  const int T = L.T = (int)(L.N / kTileRows);
+  L.pattern.assign((size_t)T * T, 0);
+  if (!sparse) {
+    for (int i = 0; i < T; ++i)
+      for (int j = 0; j <= i; ++j) L.pattern[(size_t)i * T + j] = 1;
+    return L;
+  }
+  std::vector<int> ts;
+  for (int c = 0; c < nc; ++c) {
+    ts.clear();
+    if (L.cam_row >= 0) {
+      ts.push_back(L.cam_row / kTileRows);
+      ts.push_back((L.cam_row + 2) / kTileRows);
+    }
+    for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a) {
+      const int r0 = L.tag_row[h.blk_tag[a]];
+      if (r0 < 0) continue;
+      ts.push_back(r0 / kTileRows);
+      ts.push_back((r0 + 5) / kTileRows);
+    }
+    std::sort(ts.begin(), ts.end());
+    ts.erase(std::unique(ts.begin(), ts.end()), ts.end());
+    for (size_t a = 0; a < ts.size(); ++a)
+      for (size_t b = 0; b <= a; ++b) L.pattern[(size_t)ts[a] * T + ts[b]] = 1;
+  }
+  const int rhs = (int)(L.nR / kTileRows);
+  for (int j = 0; j <= rhs; ++j) L.pattern[(size_t)rhs * T + j] = 1;
+  if (pattern_max) pattern_max(L.pattern);
+  return L;
+}
+
+}  // namespace arslam

@@ -1,0 +1,82 @@
+// host_structure.h -- host-only structure of a loaded problem (no HIP):
+// capture-major observation CSR, parameter freedom, and the layout + tile
+// pattern of the reduced (tag + camera) system.  Used by the solver's load
+// and by arslam_debug_reduced_plan (CPU-testable).
+#pragma once
+
+#include "arslam_lm.h"
+
+#include <cstdint>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace arslam {
+
+constexpr int kTileRows = 64;
+constexpr int kMaxObsPerCapture = 64;
+
+// An error with the C-ABI code it maps to.
+struct ApiError : std::runtime_error {
+  int code;
+  ApiError(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+inline void api_check(bool ok, int code, const char *msg) {
+  if (!ok) throw ApiError(code, msg);
+}
+
+// In-place all-reduce hooks of the capture-sharded path (null: one rank).
+using ReduceSumF64 = std::function<void(std::vector<double> &)>;
+using ReduceMaxU8 = std::function<void(std::vector<uint8_t> &)>;
+
+// Capture-major observation order and parameter freedom.  A block is a
+// parameter iff some residual uses it and it is not held constant (Ceres
+// removes unused and constant blocks; ar_slam_util.cpp:965,972).  Tag use and
+// the observation count are global over ranks (tag_deg_sum).
+struct HostProblem {
+  int nc = 0, nt = 0, nb = 0;
+  long n = 0;                       // 3 + 6 nc + 6 nt parameter slots
+  int maxk = 0;                     // most observations in one capture
+  std::vector<int> cap_start;       // [nc+1] observations of capture c (capture-major)
+  std::vector<int> obs_tag;         // [nb]
+  std::vector<int> obs_lblk;        // [nb] 1 + local tag block of the observation in its capture
+  std::vector<int> cap_blk_start;   // [nc+1] distinct tags of capture c
+  std::vector<int> blk_tag;         // tag of each (capture, local block)
+  std::vector<int> tag_start;       // [nt+1] tag CSR over the capture-major order
+  std::vector<int> tag_obs;         // [nb]
+  std::vector<double> corners;      // [8 nb] capture-major
+  std::vector<unsigned char> slot_free, obs_active;
+  std::vector<double> x0;           // [n] initial slots
+  long nb_global = 0;
+};
+
+// Reverse Cuthill-McKee order of an undirected graph (adjacency lists).
+std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj);
+// Nested-dissection parts (leaves and separators) in elimination order.
+// xyz (optional, 3 per node): an embedding for geometric separators; the
+// smaller of the geometric and the BFS-level separator is used.
+std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf,
+                                       const std::vector<double> &xyz = {});
+
+HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum);
+
+// Row layout of the reduced system and its tile pattern (before fill).
+//   ordering 0 natural, 1 reverse Cuthill-McKee, 2 nested dissection (parts
+//   aligned to 64-row tiles); the camera's 3 rows come last; the rhs is row nR.
+struct ReducedLayout {
+  std::vector<int> tag_row;         // [nt] first row of tag t, -1 if not a parameter
+  std::vector<int> row_slot;        // [nR] parameter slot of each row, -1 for padding
+  int cam_row = -1;
+  long nR = 0, N = 0;               // rows; N = round_up(nR + 1, 64)
+  int T = 0;                        // tiles per side
+  std::vector<uint8_t> pattern;     // [T*T] lower tile pattern of the assembled system
+  int n_parts = 0;                  // ordering parts (ND: leaves + separators)
+  long pad_rows = 0;                // alignment padding rows among the tag rows
+};
+
+ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
+                             const ReduceMaxU8 &pattern_max);
+
+}  // namespace arslam

@@ -36,150 +36,11 @@ T *upload(const std::vector<T> &h, hipStream_t s) {
   return d;
 }
 
-// BFS over `mark == tag` nodes from start; fills level of each visited node
-// (-1 unvisited) and returns the visit order.
-std::vector<int> bfs(int start, const std::vector<std::vector<int>> &adj, const std::vector<int> &mark,
-                     int tag, std::vector<int> &lev) {
-  std::vector<int> order{start};
-  lev[start] = 0;
-  for (size_t h = 0; h < order.size(); ++h) {
-    const int u = order[h];
-    for (int v : adj[u])
-      if (mark[v] == tag && lev[v] < 0) {
-        lev[v] = lev[u] + 1;
-        order.push_back(v);
-      }
-  }
-  return order;
-}
-
-// pseudo-peripheral node of the component of `start` (George-Liu)
-int peripheral(int start, const std::vector<std::vector<int>> &adj, const std::vector<int> &mark,
-               int tag, std::vector<int> &lev) {
-  int best = start, depth = -1;
-  for (int it = 0; it < 6; ++it) {
-    const std::vector<int> ord = bfs(best, adj, mark, tag, lev);
-    const int d = lev[ord.back()];
-    int far = ord.back();
-    for (int u : ord)   // among the last level, the one of least degree
-      if (lev[u] == d && adj[u].size() < adj[far].size()) far = u;
-    for (int u : ord) lev[u] = -1;
-    if (d <= depth) break;
-    depth = d;
-    best = far;
-  }
-  return best;
-}
-
-struct Dissector {
-  const std::vector<std::vector<int>> &adj;
-  int leaf;
-  std::vector<int> mark, lev;
-  int next_tag = 1;
-  std::vector<std::vector<int>> parts;   // elimination order
-
-  Dissector(const std::vector<std::vector<int>> &a, int leaf_size)
-      : adj(a), leaf(leaf_size), mark(a.size(), 0), lev(a.size(), -1) {}
-
-  // nodes: all with mark == tag
-  void run(std::vector<int> nodes, int tag) {
-    if (nodes.empty()) return;
-    // split into connected components
-    std::vector<std::vector<int>> comps;
-    for (int u : nodes) {
-      if (lev[u] >= 0) continue;
-      std::vector<int> c = bfs(u, adj, mark, tag, lev);
-      comps.push_back(std::move(c));
-    }
-    for (int u : nodes) lev[u] = -1;
-    for (auto &c : comps) dissect(c, tag);
-  }
-
-  void dissect(std::vector<int> &comp, int tag) {
-    if ((int)comp.size() <= leaf) {
-      leaf_part(comp, tag);
-      return;
-    }
-    const int s = peripheral(comp[0], adj, mark, tag, lev);
-    std::vector<int> ord = bfs(s, adj, mark, tag, lev);
-    const int depth = lev[ord.back()];
-    if (depth < 2) {
-      for (int u : ord) lev[u] = -1;
-      leaf_part(comp, tag);
-      return;
-    }
-    std::vector<int> cnt(depth + 1, 0);
-    for (int u : ord) cnt[lev[u]]++;
-    // separator level: balances the two sides, never the first or last level
-    int sep = 1, acc = cnt[0];
-    const int half = (int)ord.size() / 2;
-    while (sep < depth - 1 && acc + cnt[sep] / 2 < half) acc += cnt[sep++];
-    std::vector<int> A, B, S;
-    for (int u : ord) {
-      if (lev[u] < sep) A.push_back(u);
-      else if (lev[u] > sep) B.push_back(u);
-      else S.push_back(u);
-    }
-    for (int u : ord) lev[u] = -1;
-    const int ta = ++next_tag, tb = ++next_tag, ts = ++next_tag;
-    for (int u : A) mark[u] = ta;
-    for (int u : B) mark[u] = tb;
-    for (int u : S) mark[u] = ts;
-    run(A, ta);
-    run(B, tb);
-    parts.push_back(S);
-  }
-
-  void leaf_part(std::vector<int> &comp, int tag) {
-    // within a leaf keep BFS order (locality)
-    std::vector<int> ord = bfs(comp[0], adj, mark, tag, lev);
-    for (int u : ord) lev[u] = -1;
-    parts.push_back(ord);
-  }
-};
-
 }  // namespace
-
-std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj) {
-  std::vector<int> order;
-  order.reserve(n);
-  std::vector<int> mark(n, 0), lev(n, -1);
-  std::vector<char> done(n, 0);
-  for (;;) {
-    int start = -1;
-    for (int v = 0; v < n; ++v)
-      if (!done[v] && (start < 0 || adj[v].size() < adj[start].size())) start = v;
-    if (start < 0) break;
-    start = peripheral(start, adj, mark, 0, lev);
-    std::deque<int> q{start};
-    done[start] = 1;
-    while (!q.empty()) {
-      const int u = q.front();
-      q.pop_front();
-      order.push_back(u);
-      std::vector<int> nb;
-      for (int v : adj[u])
-        if (!done[v]) { done[v] = 1; nb.push_back(v); }
-      std::stable_sort(nb.begin(), nb.end(),
-                       [&](int a, int b) { return adj[a].size() < adj[b].size(); });
-      for (int v : nb) q.push_back(v);
-    }
-  }
-  std::reverse(order.begin(), order.end());
-  return order;
-}
-
-std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf) {
-  Dissector d(adj, leaf);
-  std::vector<int> all(n);
-  for (int i = 0; i < n; ++i) all[i] = i;
-  d.run(all, 0);
-  return d.parts;
-}
 
 constexpr int kSplitMin = 6;   // k-lists longer than this are split
 
-void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hipStream_t s) {
+void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) {
   llt_plan_free(plan);
   plan.T = T;
   plan.lda = lda;
@@ -213,12 +74,13 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   for (int k = 0; k < T; ++k) levcols[height[k]].push_back(k);
   plan.nlev = nlev;
 
-  std::vector<int2> panel, targets;
-  std::vector<int> kstart{0}, ks, bcols, gbeg{0};
-  std::vector<int4> items;
-  std::vector<int2> split;
+  std::vector<int2> &panel = plan.h_panel, &targets = plan.h_targets, &gather = plan.h_gather,
+                    &split = plan.h_split;
+  std::vector<int> &kstart = plan.h_kstart, &ks = plan.h_ks, &bcols = plan.h_bcols, &gbeg = plan.h_gbeg;
+  std::vector<int4> &items = plan.h_items;
+  kstart.assign(1, 0);
+  gbeg.assign(1, 0);
   plan.h_item_off.assign(1, 0);
-  std::vector<int2> gather;
   plan.h_panel_off.assign(1, 0);
   plan.h_upd_off.assign(1, 0);
   plan.h_bs_off.assign(1, 0);
@@ -313,22 +175,31 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
     for (int j = 0; j <= i; ++j)
       if (P[(long)i * T + j] && plan.h_tile_id[(long)i * T + j] < 0) plan.h_tile_id[(long)i * T + j] = (int)nid++;
   plan.n_tiles = nid;
-  plan.panel = upload(panel, s);
-  plan.upd_targets = upload(targets, s);
-  plan.upd_kstart = upload(kstart, s);
-  plan.upd_ks = upload(ks, s);
-  plan.upd_items = upload(items, s);
-  plan.upd_split = upload(split, s);
-  plan.n_split = (long)split.size();
-  check(hipMalloc(&plan.upd_cnt, std::max<size_t>(split.size(), 1) * sizeof(int)), "hipMalloc(upd_cnt)");
+}
+
+void llt_plan_upload(LltPlan &plan, hipStream_t s) {
+  const int T = plan.T;
+  plan.panel = upload(plan.h_panel, s);
+  plan.upd_targets = upload(plan.h_targets, s);
+  plan.upd_kstart = upload(plan.h_kstart, s);
+  plan.upd_ks = upload(plan.h_ks, s);
+  plan.upd_items = upload(plan.h_items, s);
+  plan.upd_split = upload(plan.h_split, s);
+  plan.n_split = (long)plan.h_split.size();
+  check(hipMalloc(&plan.upd_cnt, std::max<size_t>(plan.h_split.size(), 1) * sizeof(int)), "hipMalloc(upd_cnt)");
   check(hipMalloc(&plan.upd_part, std::max<long>(plan.n_part, 1) * 4096 * sizeof(double)), "hipMalloc(upd_part)");
-  plan.bs_cols = upload(bcols, s);
-  plan.bs_gather = upload(gather, s);
-  plan.bs_gbeg = upload(gbeg, s);
-  check(hipMalloc(&plan.bs_part, std::max<size_t>(gather.size(), 1) * 64 * sizeof(double)), "hipMalloc(bs_part)");
+  plan.bs_cols = upload(plan.h_bcols, s);
+  plan.bs_gather = upload(plan.h_gather, s);
+  plan.bs_gbeg = upload(plan.h_gbeg, s);
+  check(hipMalloc(&plan.bs_part, std::max<size_t>(plan.h_gather.size(), 1) * 64 * sizeof(double)), "hipMalloc(bs_part)");
   plan.tile_id = upload(plan.h_tile_id, s);
   check(hipMalloc(&plan.ldiag, (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
   check(hipStreamSynchronize(s), "plan sync");
+}
+
+void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hipStream_t s) {
+  llt_plan_symbolic(plan, T, lda, P);
+  llt_plan_upload(plan, s);
 }
 
 void llt_plan_free(LltPlan &plan) {

@@ -14,6 +14,8 @@
 #include <cstdint>
 #include <vector>
 
+#include "host_structure.h"
+
 namespace arslam {
 
 constexpr int kWave = 64;
@@ -96,17 +98,23 @@ struct LltPlan {
   std::vector<int> h_bs_off;        // [nlev+1], in backward (root-first) order
   std::vector<int> h_bsg_off;       // [nlev+1], gather tasks per backward level
   std::vector<double> h_upd_flops;  // useful flops of each level's update
+  // host copies of the device lists (llt_plan_symbolic)
+  std::vector<int2> h_panel, h_targets, h_gather, h_split;
+  std::vector<int> h_kstart, h_ks, h_bcols, h_gbeg;
+  std::vector<int4> h_items;
   double total_upd_flops = 0.0;
   long total_upd_tiles = 0;
 };
 
-// Symbolic tile fill of the lower pattern (T*T bytes, in/out) and device lists.
+// Symbolic tile fill of the lower pattern (T*T bytes, in/out) and the host
+// task lists (no HIP calls: usable without a device).
+void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern);
+// Upload the host lists and allocate the plan's device buffers.
+void llt_plan_upload(LltPlan &plan, hipStream_t s);
+// llt_plan_symbolic + llt_plan_upload
 void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern, hipStream_t s);
 void llt_plan_free(LltPlan &plan);
-// Reverse Cuthill-McKee order of an undirected graph (adjacency lists).
-std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj);
-// Nested-dissection parts (leaves and separators) in elimination order.
-std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf);
+
 
 // ---- lm_kernels.hip ----
 void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,

@@ -389,7 +389,14 @@ __global__ void k_tag_reduce(DevProblem P, const double *__restrict__ obs_tg,
   if (e >= 12L * P.nt) return;
   const int t = (int)(e / 12), j = (int)(e % 12);
   double s = 0.0;
-  for (int q = P.tag_start[t]; q < P.tag_start[t + 1]; ++q) s += obs_tg[12L * P.tag_obs[q] + j];
+  const int qa = P.tag_start[t], qb = P.tag_start[t + 1];
+  for (int q0 = qa; q0 < qb; q0 += 8) {   // 8 gathers in flight; summed in observation order
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = obs_tg[12L * P.tag_obs[min(q0 + u, qb - 1)] + j];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (q0 + u < qb) ? v[u] : 0.0;
+  }
   const long slot = slot_tag(P, t) + (j % 6);
   const double v = P.slot_free[slot] ? s : 0.0;
   if (j < 6) g[slot] = v; else colnorm[slot] = v;
@@ -731,48 +738,52 @@ __global__ __launch_bounds__(kWave) void k_cost(DevProblem P, const double *__re
 // Deterministic single-block reduction of the per-capture partials.
 // out[p] for p < NPART: sum (max for the *BAD flags); out[NPART] = F-side step^2,
 // out[NPART+1] = F-side non-finite flag.
+// One block per LM scalar p (deterministic: fixed element -> thread
+// assignment, fixed tree); 8 loads in flight per thread.
 __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
                                                        const double *__restrict__ fparts,
                                                        int nfparts, double *__restrict__ out) {
   __shared__ double red[1024];
   const int t = threadIdx.x;
-  for (int p = 0; p < NPART + 2; ++p) {
-    const bool is_max = (p == P_YBAD || p == P_CBAD || p == NPART + 1);
-    double acc = 0.0;
-    if (p < NPART) {
-      for (int i = t; i < nc; i += 1024) {
-        const double v = parts[(long)p * nc + i];
-        acc = is_max ? fmax(acc, v) : acc + v;
-      }
-    } else if (fparts) {
-      for (int i = t; i < nfparts; i += 1024) {
-        const double v = fparts[2L * i + (p - NPART)];
-        acc = is_max ? fmax(acc, v) : acc + v;
-      }
+  const int p = blockIdx.x;
+  const bool is_max = (p == P_YBAD || p == P_CBAD || p == NPART + 1);
+  const double *src = p < NPART ? parts + (long)p * nc : fparts;
+  const int len = p < NPART ? nc : (fparts ? nfparts : 0);
+  const int stride = p < NPART ? 1 : 2, off0 = p < NPART ? 0 : p - NPART;
+  double acc = 0.0;
+  for (int i0 = t; i0 < len; i0 += 8 * 1024) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(long)stride * min(i0 + u * 1024, len - 1) + off0];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double w = (i0 + u * 1024 < len) ? v[u] : 0.0;
+      acc = is_max ? fmax(acc, w) : acc + w;
     }
-    red[t] = acc;
-    __syncthreads();
-    for (int off = 512; off > 0; off >>= 1) {
-      if (t < off) red[t] = is_max ? fmax(red[t], red[t + off]) : red[t] + red[t + off];
-      __syncthreads();
-    }
-    if (t == 0) out[p] = red[0];
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (int off = 512; off > 0; off >>= 1) {
+    if (t < off) red[t] = is_max ? fmax(red[t], red[t + off]) : red[t] + red[t + off];
     __syncthreads();
   }
+  if (t == 0) out[p] = red[0];
 }
 
 // Norms over free parameter slots, split into capture slots (out[0..2]) and
 // camera + tag slots (out[3..5]): max |g|, sum g^2, sum x^2.  The split lets
 // the capture-sharded path reduce only the disjoint capture part across ranks.
-__global__ __launch_bounds__(1024) void k_slot_norms(long n, long cap_lo, long cap_hi,
-                                                     const unsigned char *__restrict__ free_,
-                                                     const double *__restrict__ g,
-                                                     const double *__restrict__ x,
-                                                     double *__restrict__ out) {
-  __shared__ double red[6][1024];
+constexpr int kNormBlocks = 64;
+
+__global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long cap_hi,
+                                                    const unsigned char *__restrict__ free_,
+                                                    const double *__restrict__ g,
+                                                    const double *__restrict__ x,
+                                                    double *__restrict__ part) {
+  __shared__ double red[6][256];
   const int t = threadIdx.x;
   double v[6] = {0, 0, 0, 0, 0, 0};
-  for (long i = t; i < n; i += 1024) {
+  for (long i = (long)blockIdx.x * 256 + t; i < n; i += (long)kNormBlocks * 256) {
     if (!free_[i]) continue;
     const int o = (i >= cap_lo && i < cap_hi) ? 0 : 3;
     const double gv = g[i], xv = x[i];
@@ -782,7 +793,7 @@ __global__ __launch_bounds__(1024) void k_slot_norms(long n, long cap_lo, long c
   }
   for (int q = 0; q < 6; ++q) red[q][t] = v[q];
   __syncthreads();
-  for (int off = 512; off > 0; off >>= 1) {
+  for (int off = 128; off > 0; off >>= 1) {
     if (t < off) {
       red[0][t] = fmax(red[0][t], red[0][t + off]);
       red[1][t] += red[1][t + off];
@@ -791,6 +802,22 @@ __global__ __launch_bounds__(1024) void k_slot_norms(long n, long cap_lo, long c
       red[4][t] += red[4][t + off];
       red[5][t] += red[5][t + off];
     }
+    __syncthreads();
+  }
+  if (t < 6) part[6L * blockIdx.x + t] = red[t][0];
+}
+
+// second stage: out[q] = reduction over the kNormBlocks partials (fixed tree)
+__global__ __launch_bounds__(64) void k_slot_norms_final(const double *__restrict__ part,
+                                                         double *__restrict__ out) {
+  __shared__ double red[6][kNormBlocks];
+  const int t = threadIdx.x;
+  for (int q = 0; q < 6; ++q) red[q][t] = part[6L * t + q];
+  __syncthreads();
+  for (int off = kNormBlocks / 2; off > 0; off >>= 1) {
+    if (t < off)
+      for (int q = 0; q < 6; ++q)
+        red[q][t] = (q % 3 == 0) ? fmax(red[q][t], red[q][t + off]) : red[q][t] + red[q][t + off];
     __syncthreads();
   }
   if (t < 6) out[t] = red[t][0];
@@ -896,11 +923,14 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
                          hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_parts, dim3(1), dim3(1024), 0, s, parts, nc, fparts, nfparts, out);
+  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out);
 }
 
 void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_slot_norms, dim3(1), dim3(1024), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g, x, out);
+  // out[0..7] results, out[8..] the per-block partials (see d_norms)
+  hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g, x,
+                     out + 8);
+  hipLaunchKernelGGL(k_slot_norms_final, dim3(1), dim3(kNormBlocks), 0, s, out + 8, out);
 }
 
 void launch_camera_slots(const DevProblem &P, const double *red, double *g, double *colnorm,

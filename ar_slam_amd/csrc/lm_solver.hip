@@ -27,10 +27,7 @@ namespace {
 
 thread_local std::string g_last_error;
 
-struct Error : std::runtime_error {
-  int code;
-  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
-};
+using Error = arslam::ApiError;
 
 #define HIP_CHECK(expr)                                                                      \
   do {                                                                                       \
@@ -127,6 +124,7 @@ struct arslam_lm {
   bool has_f = false;
   std::vector<unsigned char> slot_free;
   std::vector<double> x0;   // initial slots
+  long nb_global = 0;       // observations over all ranks
   arslam::DevProblem P{};
   hipStream_t stream = nullptr;
   int device = 0;
@@ -230,218 +228,54 @@ long round_up(long v, long m) { return (v + m - 1) / m * m; }
 }  // namespace
 
 void arslam_lm::load(const arslam_soa_problem *p) {
-  fail_if(!p, ARSLAM_E_INVALID_ARG, "null problem");
-  fail_if(p->n_cap < 0 || p->n_tag < 0 || p->n_obs < 0, ARSLAM_E_INVALID_ARG, "negative sizes");
-  fail_if(!p->camera || (p->n_cap && !p->cap) || (p->n_tag && !p->tag), ARSLAM_E_INVALID_ARG,
-          "null parameter arrays");
-  fail_if(p->n_obs && (!p->obs_cap || !p->obs_tag || !p->corners), ARSLAM_E_INVALID_ARG,
-          "null observation arrays");
+  loaded = false;
+  if (nranks > 1) ensure_stream();   // the structure exchange below runs on the device
+  // host structure; with several ranks the tag use, the co-visibility and the
+  // tile pattern are made global by max/sum all-reduces (same on every rank)
+  arslam::ReduceSumF64 deg_sum;
+  arslam::ReduceMaxU8 u8_max;
+  if (nranks > 1) {
+    deg_sum = [&](std::vector<double> &v) {
+      DevBuf<double> tmp;
+      tmp.alloc(v.size());
+      tmp.upload(v.data(), v.size(), stream);
+      allreduce(tmp.p, v.size(), ARSLAM_OP_SUM);
+      HIP_CHECK(hipMemcpyAsync(v.data(), tmp.p, v.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+    };
+    u8_max = [&](std::vector<uint8_t> &v) {
+      DevBuf<uint8_t> tmp;
+      tmp.alloc(v.size());
+      tmp.upload(v.data(), v.size(), stream);
+      allreduce_any(tmp.p, v.size(), ARSLAM_DT_U8, ARSLAM_OP_MAX);
+      HIP_CHECK(hipMemcpyAsync(v.data(), tmp.p, v.size(), hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+    };
+  }
+  arslam::HostProblem h = arslam::host_problem(p, deg_sum);   // validates p
   ensure_stream();
   soa = *p;
-  nc = p->n_cap;
-  nt = p->n_tag;
-  nb = p->n_obs;
-  n = 3 + 6L * nc + 6L * nt;
-
-  // capture-major observation order (stable)
-  std::vector<int> cap_start(nc + 1, 0);
-  for (int b = 0; b < nb; ++b) {
-    fail_if(p->obs_cap[b] < 0 || p->obs_cap[b] >= nc, ARSLAM_E_INVALID_ARG, "obs_cap out of range");
-    fail_if(p->obs_tag[b] < 0 || p->obs_tag[b] >= nt, ARSLAM_E_INVALID_ARG, "obs_tag out of range");
-    cap_start[p->obs_cap[b] + 1]++;
-  }
-  int maxk = 0;
-  for (int c = 0; c < nc; ++c) {
-    maxk = std::max(maxk, cap_start[c + 1]);
-    cap_start[c + 1] += cap_start[c];
-  }
-  fail_if(maxk > arslam::kMaxTagsPerCapture, ARSLAM_E_UNSUPPORTED,
-          "more than 64 observations in one capture");
-  std::vector<int> order(nb);
-  {
-    std::vector<int> fill(cap_start.begin(), cap_start.end() - 1);
-    for (int b = 0; b < nb; ++b) order[fill[p->obs_cap[b]]++] = b;
-  }
-  std::vector<int> obs_tag(nb), obs_lblk(nb), cap_blk_start(nc + 1, 0), blk_tag;
-  std::vector<double> corners(8L * nb);
-  blk_tag.reserve(nb);
-  for (int c = 0; c < nc; ++c) {
-    cap_blk_start[c] = (int)blk_tag.size();
-    for (int q = cap_start[c]; q < cap_start[c + 1]; ++q) {
-      const int b = order[q];
-      const int t = p->obs_tag[b];
-      obs_tag[q] = t;
-      std::memcpy(&corners[8L * q], p->corners + 8L * b, 8 * sizeof(double));
-      int u = -1;
-      for (int i = cap_blk_start[c]; i < (int)blk_tag.size(); ++i)
-        if (blk_tag[i] == t) { u = i - cap_blk_start[c]; break; }
-      if (u < 0) { u = (int)blk_tag.size() - cap_blk_start[c]; blk_tag.push_back(t); }
-      obs_lblk[q] = u + 1;
-    }
-  }
-  cap_blk_start[nc] = (int)blk_tag.size();
-  // tag CSR over the capture-major order
-  std::vector<int> tag_start(nt + 1, 0), tag_obs(nb);
-  for (int q = 0; q < nb; ++q) tag_start[obs_tag[q] + 1]++;
-  for (int t = 0; t < nt; ++t) tag_start[t + 1] += tag_start[t];
-  {
-    std::vector<int> fill(tag_start.begin(), tag_start.end() - 1);
-    for (int q = 0; q < nb; ++q) tag_obs[fill[obs_tag[q]]++] = q;
-  }
-  // Free slots: a block is a parameter iff a residual uses it and it is not
-  // held constant (Ceres removes unused and constant blocks).  Tag use and
-  // the observation count are global over ranks.
-  std::vector<double> tag_deg(nt + 1, 0.0);
-  for (int q = 0; q < nb; ++q) tag_deg[obs_tag[q]] += 1.0;
-  tag_deg[nt] = nb;
-  if (nranks > 1) {
-    DevBuf<double> tmp;
-    tmp.alloc(nt + 1);
-    tmp.upload(tag_deg.data(), nt + 1, stream);
-    allreduce(tmp.p, nt + 1, ARSLAM_OP_SUM);
-    HIP_CHECK(hipMemcpyAsync(tag_deg.data(), tmp.p, (nt + 1) * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
-  }
-  slot_free.assign(n, 0);
-  const bool cam_free = !p->camera_const && tag_deg[nt] > 0;
-  for (int j = 0; j < 3; ++j) slot_free[j] = cam_free;
-  for (int c = 0; c < nc; ++c) {
-    const bool f = cap_start[c + 1] > cap_start[c] && !(p->cap_const && p->cap_const[c]);
-    for (int j = 0; j < 6; ++j) slot_free[3 + 6L * c + j] = f;
-  }
-  for (int t = 0; t < nt; ++t) {
-    const bool f = tag_deg[t] > 0 && !(p->tag_const && p->tag_const[t]);
-    for (int j = 0; j < 6; ++j) slot_free[3 + 6L * nc + 6L * t + j] = f;
-  }
-  std::vector<unsigned char> obs_active(nb);
-  for (int q = 0; q < nb; ++q) {
-    const int c = p->obs_cap[order[q]];
-    obs_active[q] = slot_free[0] || slot_free[3 + 6L * c] || slot_free[3 + 6L * nc + 6L * obs_tag[q]];
-  }
-  x0.resize(n);
-  std::memcpy(x0.data(), p->camera, 3 * sizeof(double));
-  if (nc) std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
-  if (nt) std::memcpy(x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
-
-  // ---- reduced-system ordering and tile plan ----
-  // Rows exist only for free tags and a free camera (constant / unused blocks
-  // are not parameters).  Tags are ordered natural, RCM or by nested
-  // dissection; with ND every part starts on a tile boundary so the tile
-  // elimination tree follows the dissection tree.
-  std::vector<int> tag_row(std::max(nt, 1), -1);
-  std::vector<int> row_slot;
-  int cam_row = -1;
-  const bool sparse = opt.cholesky_skip_zero_tiles != 0;
-  const int ordering = opt.reduced_ordering;
-  {
-    std::vector<char> tfree(nt, 0);
-    for (int t = 0; t < nt; ++t) tfree[t] = slot_free[3 + 6L * nc + 6L * t];
-    std::vector<std::vector<int>> adj(nt);
-    if (ordering != 0 && nt > 1) {
-      if (nranks > 1) {
-        fail_if(nt > 16384, ARSLAM_E_UNSUPPORTED, "multi-GPU reduced ordering limited to 16384 tags");
-        std::vector<uint8_t> bm((size_t)nt * nt, 0);
-        for (int c = 0; c < nc; ++c)
-          for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a)
-            for (int b = cap_blk_start[c]; b < cap_blk_start[c + 1]; ++b)
-              if (a != b) bm[(size_t)blk_tag[a] * nt + blk_tag[b]] = 1;
-        DevBuf<uint8_t> tmp;
-        tmp.alloc(bm.size());
-        tmp.upload(bm.data(), bm.size(), stream);
-        allreduce_any(tmp.p, bm.size(), ARSLAM_DT_U8, ARSLAM_OP_MAX);
-        HIP_CHECK(hipMemcpyAsync(bm.data(), tmp.p, bm.size(), hipMemcpyDeviceToHost, stream));
-        HIP_CHECK(hipStreamSynchronize(stream));
-        for (int a = 0; a < nt; ++a)
-          for (int b = 0; b < nt; ++b)
-            if (bm[(size_t)a * nt + b] && tfree[a] && tfree[b]) adj[a].push_back(b);
-      } else {
-        for (int c = 0; c < nc; ++c)
-          for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a)
-            for (int b = cap_blk_start[c]; b < cap_blk_start[c + 1]; ++b)
-              if (a != b && tfree[blk_tag[a]] && tfree[blk_tag[b]]) adj[blk_tag[a]].push_back(blk_tag[b]);
-        for (auto &v : adj) {
-          std::sort(v.begin(), v.end());
-          v.erase(std::unique(v.begin(), v.end()), v.end());
-        }
-      }
-    }
-    std::vector<std::vector<int>> parts;
-    if (ordering == 2 && nt > 1) {
-      parts = arslam::nd_parts(nt, adj, 10);
-    } else {
-      std::vector<int> order;
-      if (ordering == 1 && nt > 1) order = arslam::rcm_order(nt, adj);
-      else for (int t = 0; t < nt; ++t) order.push_back(t);
-      parts.push_back(order);
-    }
-    long row = 0;
-    for (auto &part : parts) {
-      bool any = false;
-      for (int t : part) any = any || tfree[t];
-      if (!any) continue;
-      if (ordering == 2) row = round_up(row, arslam::kTile);
-      for (int t : part) {
-        if (!tfree[t]) continue;
-        tag_row[t] = (int)row;
-        for (int j = 0; j < 6; ++j) row_slot.push_back(3 + 6 * nc + 6 * t + j);
-        row += 6;
-      }
-      while ((long)row_slot.size() < row) row_slot.push_back(-1);
-    }
-    // alignment padding rows inside the tag block
-    {
-      std::vector<int> rs(row, -1);
-      for (int t = 0; t < nt; ++t)
-        if (tag_row[t] >= 0)
-          for (int j = 0; j < 6; ++j) rs[tag_row[t] + j] = 3 + 6 * nc + 6 * t + j;
-      row_slot = rs;
-    }
-    if (slot_free[0]) {
-      cam_row = (int)row;
-      for (int j = 0; j < 3; ++j) row_slot.push_back(j);
-      row += 3;
-    }
-    nR = row;
-  }
+  nc = h.nc;
+  nt = h.nt;
+  nb = h.nb;
+  n = h.n;
+  nb_global = h.nb_global;
+  slot_free = h.slot_free;
+  x0 = h.x0;
+  const int maxk = h.maxk;
+  arslam::ReducedLayout L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0,
+                                                   u8_max, u8_max);
+  const std::vector<int> &cap_start = h.cap_start, &obs_tag = h.obs_tag, &obs_lblk = h.obs_lblk,
+                         &cap_blk_start = h.cap_blk_start, &blk_tag = h.blk_tag, &tag_start = h.tag_start,
+                         &tag_obs = h.tag_obs, &tag_row = L.tag_row, &row_slot = L.row_slot;
+  const std::vector<double> &corners = h.corners;
+  const std::vector<unsigned char> &obs_active = h.obs_active;
+  const int cam_row = L.cam_row;
+  nR = L.nR;
   has_f = nR > 0;
   if (has_f) {
-    N = round_up(nR + 1, arslam::kTile);
-    const int T = (int)(N / arslam::kTile);
-    std::vector<uint8_t> pattern((size_t)T * T, 0);
-    if (!sparse) {
-      for (int i = 0; i < T; ++i)
-        for (int j = 0; j <= i; ++j) pattern[(size_t)i * T + j] = 1;
-    } else {
-      std::vector<int> ts;
-      for (int c = 0; c < nc; ++c) {
-        ts.clear();
-        if (cam_row >= 0) {
-          ts.push_back(cam_row / arslam::kTile);
-          ts.push_back((cam_row + 2) / arslam::kTile);
-        }
-        for (int a = cap_blk_start[c]; a < cap_blk_start[c + 1]; ++a) {
-          const int r0 = tag_row[blk_tag[a]];
-          if (r0 < 0) continue;
-          ts.push_back(r0 / arslam::kTile);
-          ts.push_back((r0 + 5) / arslam::kTile);
-        }
-        std::sort(ts.begin(), ts.end());
-        ts.erase(std::unique(ts.begin(), ts.end()), ts.end());
-        for (size_t a = 0; a < ts.size(); ++a)
-          for (size_t b = 0; b <= a; ++b) pattern[(size_t)ts[a] * T + ts[b]] = 1;
-      }
-      const int rhs = (int)(nR / arslam::kTile);
-      for (int j = 0; j <= rhs; ++j) pattern[(size_t)rhs * T + j] = 1;
-      if (nranks > 1) {
-        DevBuf<uint8_t> tmp;
-        tmp.alloc(pattern.size());
-        tmp.upload(pattern.data(), pattern.size(), stream);
-        allreduce_any(tmp.p, pattern.size(), ARSLAM_DT_U8, ARSLAM_OP_MAX);
-        HIP_CHECK(hipMemcpyAsync(pattern.data(), tmp.p, pattern.size(), hipMemcpyDeviceToHost, stream));
-        HIP_CHECK(hipStreamSynchronize(stream));
-      }
-    }
-    arslam::llt_plan_build(plan, T, N, pattern, stream);
+    N = L.N;
+    arslam::llt_plan_build(plan, L.T, N, L.pattern, stream);
   } else {
     N = 0;
     arslam::llt_plan_free(plan);
@@ -468,7 +302,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   // stays zero when there are no reduced rows (k_update_f is then not launched)
   HIP_CHECK(hipMemsetAsync(d_fparts.p, 0, d_fparts.n * sizeof(double), stream));
   d_red.alloc(16);
-  d_norms.alloc(8);
+  d_norms.alloc(8 + 6 * 64);   // results + k_slot_norms block partials
   d_flag.alloc(1);
   d_tag_row.alloc(tag_row.size()); d_tag_row.upload(tag_row.data(), tag_row.size(), stream);
   d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
@@ -746,17 +580,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->minimizer_time_s = now_s() - t_start;
   write_back(d_xbest.p);
   s->total_time_s = now_s() - t_start;
-  long nb_all = nb;
-  if (nranks > 1) {
-    double v = nb;
-    DevBuf<double> tmp;
-    tmp.alloc(1);
-    tmp.upload(&v, 1, stream);
-    allreduce(tmp.p, 1, ARSLAM_OP_SUM);
-    HIP_CHECK(hipMemcpyAsync(&v, tmp.p, sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
-    nb_all = (long)v;
-  }
+  const long nb_all = nb_global;
   s->n_obs = (int)nb_all;
   s->final_rms_px = nb_all ? std::sqrt(2.0 * s->final_cost / (4.0 * nb_all)) : 0.0;
   s->t_linearize_ms = timers[PH_LIN].acc_ms;

@@ -43,7 +43,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
            "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm", "arslam_lm_set_comm_callback",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
-           "arslam_debug_residual_jacobian", "arslam_debug_dense_llt"]
+           "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_reduced_plan"]
 
 _dp = C.POINTER(C.c_double)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
@@ -366,3 +366,22 @@ def debug_dense_llt(A, b):
     _check(lib().arslam_debug_dense_llt(n, A.ctypes.data_as(_dp), b.ctypes.data_as(_dp),
                                         y.ctypes.data_as(_dp), C.byref(info)))
     return A, y, info.value
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("n_reduced", C.c_long), ("n_padded", C.c_long), ("pad_rows", C.c_long),
+                ("tiles_per_side", C.c_int), ("n_parts", C.c_int), ("camera_row", C.c_int),
+                ("n_levels", C.c_int), ("n_assembled_tiles", C.c_long), ("n_factor_tiles", C.c_long),
+                ("n_update_tiles", C.c_long), ("n_update_items", C.c_long), ("n_split_targets", C.c_long),
+                ("update_flops", C.c_double)]
+
+
+def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, cap_const=None,
+                       tag_const=None, ordering=2, skip_zero_tiles=1):
+    """Host-only symbolic analysis (no device): reduced layout + tile plan.  Returns (info dict, tag_row)."""
+    A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const, cap_const, tag_const)
+    info = PlanInfo()
+    tag_row = np.zeros(max(A.tag.shape[0], 1), np.int32)
+    _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
+                                           tag_row.ctypes.data_as(_ip)))
+    return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]

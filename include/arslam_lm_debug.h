@@ -6,6 +6,8 @@
 #ifndef ARSLAM_LM_DEBUG_H
 #define ARSLAM_LM_DEBUG_H
 
+#include "arslam_lm.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -21,6 +23,30 @@ int arslam_debug_residual_jacobian(int n, const double *cam, const double *cap, 
  * n x n row-major SPD matrix A (in place: on return A holds L) and solve
  * A y = b.  *info = 0 on success, k+1 if pivot k was not positive. */
 int arslam_debug_dense_llt(long n, double *A, const double *b, double *y, int *info);
+
+/* Host-only symbolic analysis of the reduced system (no device needed): the
+ * row layout arslam_lm_load_soa would choose for problem p under the given
+ * ordering (0 natural, 1 RCM, 2 nested dissection) and tile pattern
+ * (skip_zero_tiles), its tile Cholesky plan, and optionally the first row of
+ * each tag (tag_row[n_tag], -1 if the tag is not a parameter). */
+typedef struct {
+  long n_reduced;          /* rows of the reduced system (6 per free tag + 3 camera) */
+  long n_padded;           /* tiles_per_side * 64 */
+  long pad_rows;           /* alignment padding rows among the tag rows */
+  int tiles_per_side;
+  int n_parts;             /* ordering parts (ND leaves + separators) */
+  int camera_row;          /* -1 if the camera is constant */
+  int n_levels;            /* height of the tile elimination tree */
+  long n_assembled_tiles;  /* tiles the Schur assembly writes */
+  long n_factor_tiles;     /* after symbolic fill */
+  long n_update_tiles;     /* (target, column) tile products per factorization */
+  long n_update_items;     /* update work items (after splitting long k-lists) */
+  long n_split_targets;
+  double update_flops;     /* algorithmic flops of the trailing updates per factorization */
+} arslam_plan_info;
+
+int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
+                              arslam_plan_info *info, int *tag_row);
 
 #ifdef __cplusplus
 }
