@@ -16,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libarslam_lm.so")
 SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "debug_api.hip", "llt_plan.cpp",
-           "host_structure.cpp"]
+           "host_structure.cpp", "localize.hip"]
 ARCH = os.environ.get("ARSLAM_ARCH", "gfx950")
 
 
@@ -31,7 +31,7 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", f) for f in ("arslam_lm.h", "arslam_lm_debug.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", f) for f in ("arslam_lm.h", "arslam_lm_debug.h", "arslam_localize.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

@@ -23,6 +23,9 @@ struct ApiError : std::runtime_error {
   ApiError(int c, const std::string &m) : std::runtime_error(m), code(c) {}
 };
 
+// message returned by arslam_lm_last_error() on the calling thread
+void set_last_error(const std::string &msg);
+
 inline void api_check(bool ok, int code, const char *msg) {
   if (!ok) throw ApiError(code, msg);
 }

@@ -605,6 +605,13 @@ void arslam_lm::solve(arslam_lm_summary *s) {
 namespace {
 
 template <class F>
+int guarded(F &&f);
+}  // namespace
+namespace arslam {
+void set_last_error(const std::string &msg) { g_last_error = msg; }
+}  // namespace arslam
+namespace {
+template <class F>
 int guarded(F &&f) {
   try {
     f();

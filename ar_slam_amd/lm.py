@@ -43,7 +43,9 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
            "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm", "arslam_lm_set_comm_callback",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
-           "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_reduced_plan"]
+           "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_reduced_plan",
+           "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
+           "arslam_localizer_load", "arslam_localizer_solve"]
 
 _dp = C.POINTER(C.c_double)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
@@ -139,6 +141,12 @@ def lib():
     L.arslam_lm_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
     L.arslam_lm_set_comm_callback.argtypes = [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, C.c_void_p]
     L.arslam_lm_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
+    L.arslam_localize_many.argtypes = [C.POINTER(LocalizeBatchC), C.POINTER(Options), C.POINTER(LocalizeResult)]
+    L.arslam_localizer_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
+    L.arslam_localizer_destroy.argtypes = [C.c_void_p]
+    L.arslam_localizer_destroy.restype = None
+    L.arslam_localizer_load.argtypes = [C.c_void_p, C.POINTER(LocalizeBatchC)]
+    L.arslam_localizer_solve.argtypes = [C.c_void_p, _dp, C.POINTER(LocalizeResult), C.POINTER(C.c_double)]
     L.arslam_lm_get_options.argtypes = [C.c_void_p, C.POINTER(Options)]
     L.arslam_lm_destroy.argtypes = [C.c_void_p]
     L.arslam_lm_destroy.restype = None
@@ -385,3 +393,85 @@ def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const
     _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
                                            tag_row.ctypes.data_as(_ip)))
     return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]
+
+
+# ---- batched localize (include/arslam_localize.h) ----
+LOC_SKIPPED = -1
+
+
+class LocalizeBatchC(C.Structure):
+    _fields_ = [("n_query", C.c_int), ("n_tag", C.c_int), ("n_obs", C.c_int),
+                ("camera", _dp), ("tag", _dp), ("tag_in_map", _up), ("query_start", _ip),
+                ("obs_tag", _ip), ("corners", _dp), ("pose", _dp), ("init_from_map", C.c_int)]
+
+
+class LocalizeResult(C.Structure):
+    _fields_ = [("status", C.c_int), ("rule", C.c_int), ("num_iterations", C.c_int),
+                ("num_successful_steps", C.c_int), ("num_unsuccessful_steps", C.c_int),
+                ("init_obs", C.c_int), ("initial_cost", C.c_double), ("final_cost", C.c_double)]
+
+
+def _loc_results(res):
+    n = len(res)
+    f = {k: np.array([getattr(r, k) for r in res]) for k, _ in LocalizeResult._fields_}
+    f["rule_name"] = [RULES.get(r, str(r)) for r in f["rule"]] if n else []
+    return f
+
+
+class _LocArrays:
+    def __init__(self, batch, init_from_map, pose):
+        self.camera = _f64(batch.camera).copy()
+        self.tag = _f64(batch.tag, (-1, 6)).copy()
+        self.q_start = np.ascontiguousarray(batch.q_start, np.int32)
+        self.obs_tag = np.ascontiguousarray(batch.obs_tag, np.int32)
+        self.corners = _f64(batch.corners, (-1, 8))
+        nq = self.q_start.shape[0] - 1
+        self.pose = np.zeros((nq, 6)) if pose is None else _f64(pose, (-1, 6)).copy()
+        tim = getattr(batch, "tag_in_map", None)
+        self.tim = None if tim is None else np.ascontiguousarray(tim, np.uint8)
+        self.s = LocalizeBatchC(nq, self.tag.shape[0], self.obs_tag.shape[0],
+                                self.camera.ctypes.data_as(_dp), self.tag.ctypes.data_as(_dp),
+                                None if self.tim is None else self.tim.ctypes.data_as(_up),
+                                self.q_start.ctypes.data_as(_ip), self.obs_tag.ctypes.data_as(_ip),
+                                self.corners.ctypes.data_as(_dp), self.pose.ctypes.data_as(_dp),
+                                int(bool(init_from_map)))
+
+
+def localize_many(batch, init_from_map=True, pose=None, **opts):
+    """localizeMany on the device (one-shot).  ``batch`` has camera, tag, q_start, obs_tag,
+    corners, tag_in_map (synth.LocalizeBatch).  Returns (pose (Nq,6), results dict of arrays)."""
+    A = _LocArrays(batch, init_from_map, pose)
+    res = (LocalizeResult * max(A.s.n_query, 1))()
+    _check(lib().arslam_localize_many(C.byref(A.s), C.byref(make_options(**opts)), res))
+    return A.pose, _loc_results(res[:A.s.n_query])
+
+
+class Localizer:
+    """Resident batched localizer: load a batch once, solve it many times."""
+
+    def __init__(self, batch, init_from_map=True, pose=None, **opts):
+        self._h = C.c_void_p()
+        _check(lib().arslam_localizer_create(C.byref(self._h), C.byref(make_options(**opts))))
+        self.A = _LocArrays(batch, init_from_map, pose)
+        _check(lib().arslam_localizer_load(self._h, C.byref(self.A.s)))
+        self.n_query = self.A.s.n_query
+
+    def solve(self, download=True):
+        """Returns (pose or None, results or None, kernel_ms)."""
+        ms = C.c_double(0.0)
+        pose = np.zeros((self.n_query, 6)) if download else None
+        res = (LocalizeResult * max(self.n_query, 1))() if download else None
+        _check(lib().arslam_localizer_solve(self._h, None if pose is None else pose.ctypes.data_as(_dp),
+                                            res, C.byref(ms)))
+        return pose, (None if res is None else _loc_results(res[:self.n_query])), ms.value
+
+    def close(self):
+        if self._h:
+            lib().arslam_localizer_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

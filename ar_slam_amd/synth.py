@@ -5,7 +5,9 @@ benchmark and parity graph is generated here from a fixed seed.  The model
 is the reference's own:
 
 * tag pose ``[t_t, w_t]`` maps tag-frame points to world,
-  ``X_w = R(w_t) X_t + t_t`` (``ar_slam_util.cpp:144-148``);
+  ``X_w = R(w_t) X_t + t_t`` (``ar_slam_util.cpp:144-148``); tags lie in the
+  plane z = 0 with their z axis pointing away from the cameras (the marker
+  faces the camera, as the reference's initialisers assume);
 * capture ``inv_pose = [t_c, w_c]`` maps world to camera,
   ``X_c = R(w_c) (X_w + t_c)`` (``ar_slam_util.cpp:150-155``), so the
   camera centre is ``-t_c``;
@@ -148,17 +150,21 @@ def _rot_axis(axis, ang):
 
 
 def _sample_cameras(rng, n, x_lo, x_hi, y_lo, y_hi, max_tilt):
-    """World->camera rotations and centres for downward-looking captures."""
+    """World->camera rotations and centres of captures looking at the tag plane.
+
+    World z points from the cameras towards the tag plane (z = 0), so an
+    untilted camera has R = Rz(roll); roll and tag yaw stay within +-90 deg so
+    no pose sits near the angle-axis singularity at |w| = pi.
+    """
     pos = np.stack([rng.uniform(x_lo, x_hi, n), rng.uniform(y_lo, y_hi, n),
-                    rng.uniform(0.6, 1.2, n)], 1)
-    roll = rng.uniform(-np.pi, np.pi, n)
+                    -rng.uniform(0.6, 1.2, n)], 1)
+    roll = rng.uniform(-0.5 * np.pi, 0.5 * np.pi, n)
     tilt = rng.uniform(0.0, max_tilt, n)
     tilt_dir = rng.uniform(-np.pi, np.pi, n)
-    R_down = np.array([[1.0, 0, 0], [0, -1.0, 0], [0, 0, -1.0]])   # cam z -> world -z
     R_roll = _rot_axis(np.tile([0, 0, 1.0], (n, 1)), roll)
     tilt_axis = np.stack([np.cos(tilt_dir), np.sin(tilt_dir), np.zeros(n)], 1)
     R_tilt = rodrigues(tilt_axis * tilt[:, None])
-    R_wc = R_tilt @ R_down[None] @ R_roll
+    R_wc = R_tilt @ R_roll
     R_cw = np.transpose(R_wc, (0, 2, 1))
     return R_cw, pos
 
@@ -189,7 +195,10 @@ def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
     tag_true = np.zeros((n_tag, 6))
     tag_true[:, 0] = gx.ravel()
     tag_true[:, 1] = gy.ravel()
-    tag_true[:, 5] = rng.uniform(-np.pi, np.pi, n_tag)
+    # tags face the cameras: in the reference's marker frame (x right, y down,
+    # z away from the viewer; ar_slam_util.hpp:340-345 and calcInitValues
+    # :52-95) the tag z axis points away from the cameras, i.e. along world +z
+    tag_true[:, 5] = rng.uniform(-0.5 * np.pi, 0.5 * np.pi, n_tag)
     camera_true = np.array([F_TRUE, 0.0, 0.0])
 
     # tag corner world points (Nt,4,3)
@@ -258,6 +267,75 @@ def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
     camera0 = np.array([f_init, 0.0, 0.0])
     return Graph(camera0, cap0, tag0, obs_cap, obs_tag, np.ascontiguousarray(corners),
                  camera_true, cap_true, tag_true, name)
+
+
+@dataclasses.dataclass
+class LocalizeBatch:
+    """Independent localize queries against a fixed map (cfg5).
+
+    The map is a graph's tags at their true poses with the true focal, both
+    constant (ar_slam_util.cpp:965,972); each query is one new capture whose
+    observations ``[q_start[q], q_start[q+1])`` are in block order.
+    """
+
+    camera: np.ndarray      # (3,)
+    tag: np.ndarray         # (Nt,6) map
+    q_start: np.ndarray     # (Nq+1,) int32
+    obs_tag: np.ndarray     # (Nb,) int32
+    corners: np.ndarray     # (Nb,8)
+    pose_true: np.ndarray   # (Nq,6)
+    tag_in_map: np.ndarray  # (Nt,) uint8
+
+    @property
+    def n_query(self):
+        return self.q_start.shape[0] - 1
+
+    @property
+    def n_obs(self):
+        return self.obs_tag.shape[0]
+
+
+def make_localize_batch(map_name="cfg3", n_query=4096, seed=3, k=8, noise_px=0.5,
+                        max_tilt=np.deg2rad(20.0)):
+    """cfg5: ``n_query`` captures of the ``map_name`` tag grid (truth), k tags each."""
+    _, grid_x, grid_y, _ = CONFIGS[map_name]
+    g = config_graph(map_name)
+    tag = g.tag_true.copy()
+    n_tag = tag.shape[0]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    corners_w = np.empty((n_tag, 4, 3))
+    for i, d in enumerate(ARUCO_DIRECTIONS):
+        c = np.tile([0.5 * ARUCO_SIZE * d[0], 0.5 * ARUCO_SIZE * d[1], 0.0], (n_tag, 1))
+        corners_w[:, i] = angle_axis_rotate(tag[:, 3:], c) + tag[:, :3]
+    centres = tag[:, :3]
+    x_lo, x_hi = -0.1, (grid_x - 1) * TAG_SPACING + 0.1
+    y_lo, y_hi = -0.1, (grid_y - 1) * TAG_SPACING + 0.1
+    pose = np.zeros((n_query, 6))
+    obs = np.zeros((n_query, k), np.int64)
+    filled = 0
+    n_cand = min(n_tag, 128)
+    while filled < n_query:
+        m = max(64, min(4096, (n_query - filled) * 2))
+        R_cw, pos = _sample_cameras(rng, m, x_lo, x_hi, y_lo, y_hi, max_tilt)
+        d2 = ((centres[None, :, :2] - pos[:, None, :2]) ** 2).sum(-1)
+        cand = np.argpartition(d2, n_cand - 1, axis=1)[:, :n_cand] if n_cand < n_tag \
+            else np.tile(np.arange(n_tag), (m, 1))
+        for i in range(m):
+            if filled >= n_query:
+                break
+            sel = _visible_nearest(R_cw[i], pos[i], corners_w, centres, cand[i], k)
+            if sel is None:
+                continue
+            obs[filled] = sel
+            pose[filled, :3] = -pos[i]
+            pose[filled, 3:] = log_so3(R_cw[i:i + 1])[0]
+            filled += 1
+    q_of = np.repeat(np.arange(n_query), k)
+    obs_tag = obs.ravel().astype(np.int32)
+    corners = project_corners(g.camera_true, pose[q_of], tag[obs_tag])
+    corners += rng.normal(0.0, noise_px, corners.shape)
+    return LocalizeBatch(g.camera_true.copy(), tag, (np.arange(n_query + 1) * k).astype(np.int32),
+                         obs_tag, np.ascontiguousarray(corners), pose, np.ones(n_tag, np.uint8))
 
 
 def config_graph(name, **kw):

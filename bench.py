@@ -66,6 +66,72 @@ def cpu_baseline(g, threads, sample_iters=1):
                       f"{dt:.1f} s"}
 
 
+def bench_localize(args, world, rank):
+    """cfg5: batched localizeMany of 4096 queries against cfg3's map (BASELINE.json configs[4]).
+
+    One step = one solve of the whole batch (every query's independent LM to
+    its own termination) from the resident initial state.  Reported as
+    queries/s; the per-query-iteration rate and the kernel's HBM roofline
+    (algorithmic bytes: per query-iteration 2 passes over the observation
+    records (72 B each) and the tag poses they gather (48 B each), plus the
+    pose) ride along."""
+    from ar_slam_amd import build, lm, synth
+    import torch
+    build.build()
+    b = synth.make_localize_batch(n_query=4096)
+    loc = lm.Localizer(b, device=0 if world == 1 else int(os.environ.get("LOCAL_RANK", "0")))
+    _, res, _ = loc.solve()
+    for _ in range(args.warmup):
+        loc.solve(download=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = 0.0
+    for _ in range(args.steps):
+        _, _, ms = loc.solve(download=False)
+        kms += ms
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:   # replicas: every rank localizes its own batch; the job is the slowest rank
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    q_iters = int(res["num_iterations"].sum())
+    k_obs = b.n_obs / b.n_query
+    bytes_per_qi = 2 * k_obs * (72 + 48) + 48
+    avg_kernel_s = kms / args.steps * 1e-3
+    achieved = bytes_per_qi * q_iters / avg_kernel_s / 1e9
+    out = {"metric": "localize queries/s, 4096-query batch against the 2k-tag cfg3 map",
+           "value": world * b.n_query * args.steps / elapsed, "unit": "queries/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic (seeded generator, SURVEY.md §8d cfg5)",
+           "config": {"workload": f"cfg5: {b.n_query} queries x {int(k_obs)} tags, map = cfg3 tags",
+                      "parallelism": "one wavefront per query"},
+           "query_iterations_per_s": world * q_iters * args.steps / elapsed,
+           "mean_iterations_per_query": q_iters / b.n_query,
+           "roofline": {"bound": "hbm", "kernel": "k_localize", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "avg_launch_us": avg_kernel_s * 1e6,
+                        "bytes_per_query_iteration": bytes_per_qi},
+           "cpu_baseline": None}
+    if not args.no_cpu_baseline and world == 1:
+        from oracle import oracle as O
+        O.build()
+        sub = synth.make_localize_batch(n_query=4096)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 10.0:
+            O.localize_many(sub)
+            n += sub.n_query
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": n / dt, "unit": "queries/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} queries (the cfg5 batch repeated) through the CPU oracle's "
+                                         f"localizeMany, single thread, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def load_pmc_traffic():
     """Per-launch HBM bytes of the dominant kernel from the committed PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_dominant.json")
@@ -99,6 +165,11 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    if args.config == "cfg5":
+        bench_localize(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     from ar_slam_amd import build, lm, synth
     build.build()
     g = synth.config_graph(args.config)

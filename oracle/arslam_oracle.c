@@ -937,3 +937,156 @@ double or_cost(const or_problem *p) {
   }
   return cost;
 }
+
+/* ------------------------------------------------------------------------ */
+/* initialisers (ar_slam_util.cpp:41-128) and localize (:888-979)            */
+/* ------------------------------------------------------------------------ */
+
+/* Ceres 2.0 rotation.h */
+static void aa_to_quat(const double aa[3], double q[4]) {
+  const double theta_sq = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+  if (theta_sq > 0.0) {
+    const double theta = sqrt(theta_sq);
+    const double half = theta * 0.5;
+    const double k = sin(half) / theta;
+    q[0] = cos(half);
+    q[1] = aa[0] * k; q[2] = aa[1] * k; q[3] = aa[2] * k;
+  } else {
+    const double k = 0.5;
+    q[0] = 1.0;
+    q[1] = aa[0] * k; q[2] = aa[1] * k; q[3] = aa[2] * k;
+  }
+}
+
+static void quat_product(const double z[4], const double w[4], double zw[4]) {
+  zw[0] = z[0] * w[0] - z[1] * w[1] - z[2] * w[2] - z[3] * w[3];
+  zw[1] = z[0] * w[1] + z[1] * w[0] + z[2] * w[3] - z[3] * w[2];
+  zw[2] = z[0] * w[2] - z[1] * w[3] + z[2] * w[0] + z[3] * w[1];
+  zw[3] = z[0] * w[3] + z[1] * w[2] - z[2] * w[1] + z[3] * w[0];
+}
+
+static void quat_to_aa(const double q[4], double aa[3]) {
+  const double q1 = q[1], q2 = q[2], q3 = q[3];
+  const double sin_sq = q1 * q1 + q2 * q2 + q3 * q3;
+  double k;
+  if (sin_sq > 0.0) {
+    const double sin_theta = sqrt(sin_sq);
+    const double cos_theta = q[0];
+    const double two_theta = 2.0 * ((cos_theta < 0.0) ? atan2(-sin_theta, -cos_theta)
+                                                       : atan2(sin_theta, cos_theta));
+    k = two_theta / sin_theta;
+  } else {
+    k = 2.0;
+  }
+  aa[0] = q1 * k; aa[1] = q2 * k; aa[2] = q3 * k;
+}
+
+void or_compose_axis_angle(const double rot1[3], const double rot2[3], double out[3]) {
+  double q1[4], q2[4], q3[4];
+  aa_to_quat(rot1, q1);
+  aa_to_quat(rot2, q2);
+  quat_product(q1, q2, q3);
+  quat_to_aa(q3, out);
+}
+
+static double normalize_angle(double a) {   /* ar_slam_util.hpp:348-351 */
+  return fmod(fmod(a, 2 * M_PI) + 3 * M_PI, 2 * M_PI) - M_PI;
+}
+
+void or_calc_init_values(const double corners[8], double focal, double out[4]) {
+  static const double dir[4][2] = {{-1, -1}, {1, -1}, {1, 1}, {-1, 1}};   /* ar_slam_util.hpp:340-345 */
+  double max_dist_sq = 0.0, avg_x = 0.0, avg_y = 0.0;
+  for (int i = 0; i < 4; ++i) {
+    const double *p1 = corners + 2 * i, *p2 = corners + 2 * ((i + 1) & 3);
+    const double d = pow(p1[0] - p2[0], 2) + pow(p1[1] - p2[1], 2);
+    if (d > max_dist_sq) max_dist_sq = d;
+    avg_x += p1[0];
+    avg_y += p1[1];
+  }
+  avg_x *= 0.25;
+  avg_y *= 0.25;
+  double avg_angle = 0.0;
+  for (int i = 0; i < 4; ++i) {
+    const double expected = atan2(dir[i][1], dir[i][0]);
+    const double actual = atan2(corners[2 * i + 1] - avg_y, corners[2 * i] - avg_x);
+    const double delta = normalize_angle(actual - expected);
+    avg_angle += normalize_angle(delta - avg_angle) / (i + 1);
+  }
+  const double local_z = focal * kArucoSize / sqrt(max_dist_sq);
+  out[0] = avg_x * local_z / focal;
+  out[1] = avg_y * local_z / focal;
+  out[2] = local_z;
+  out[3] = avg_angle;
+}
+
+void or_init_capture_pose(const double corners[8], const double camera[3], const double ar_pose[6],
+                          double inv_cap_pose[6]) {
+  double v[4];
+  or_calc_init_values(corners, camera[0], v);
+  const double local_position[3] = {v[0], v[1], v[2]};
+  const double local_rot[3] = {0.0, 0.0, v[3]};
+  const double inv_ar_rot[3] = {-ar_pose[3], -ar_pose[4], -ar_pose[5]};
+  or_compose_axis_angle(local_rot, inv_ar_rot, inv_cap_pose + 3);
+  const double cap_rotation[3] = {-inv_cap_pose[3], -inv_cap_pose[4], -inv_cap_pose[5]};
+  or_angle_axis_rotate(cap_rotation, local_position, inv_cap_pose);
+  inv_cap_pose[0] -= ar_pose[0];
+  inv_cap_pose[1] -= ar_pose[1];
+  inv_cap_pose[2] -= ar_pose[2];
+}
+
+void or_init_ar_pose(const double corners[8], const double camera[3], const double inv_cap_pose[6],
+                     double ar_pose[6]) {
+  double v[4];
+  or_calc_init_values(corners, camera[0], v);
+  const double local_position[3] = {v[0], v[1], v[2]};
+  const double cap_rotation[3] = {-inv_cap_pose[3], -inv_cap_pose[4], -inv_cap_pose[5]};
+  or_angle_axis_rotate(cap_rotation, local_position, ar_pose);
+  ar_pose[0] -= inv_cap_pose[0];
+  ar_pose[1] -= inv_cap_pose[1];
+  ar_pose[2] -= inv_cap_pose[2];
+  const double local_rot[3] = {0.0, 0.0, v[3]};
+  const double cap_rot[3] = {-inv_cap_pose[3], -inv_cap_pose[4], -inv_cap_pose[5]};
+  or_compose_axis_angle(cap_rot, local_rot, ar_pose + 3);
+}
+
+int or_localize_many(int n_query, const int *q_start, const int *obs_tag, const double *corners,
+                     const double camera[3], const double *tag, int n_tag,
+                     const unsigned char *tag_in_map, int init_from_map, double *pose,
+                     const or_options *o, int *status, or_summary *summaries) {
+  int n_done = 0;
+  for (int q = 0; q < n_query; ++q) {
+    const int o0 = q_start[q], k = q_start[q + 1] - o0;
+    double *x = pose + 6L * q;
+    int init = -1;
+    for (int j = 0; j < k; ++j)
+      if (!tag_in_map || tag_in_map[obs_tag[o0 + j]]) { init = o0 + j; break; }
+    if (init < 0 && init_from_map) { status[q] = -1; continue; }   /* :929-933 */
+    if (k == 0) { status[q] = -1; continue; }
+    if (init_from_map) or_init_capture_pose(corners + 8L * init, camera, tag + 6L * obs_tag[init], x);
+    /* one capture, its blocks' tags and the camera constant: :956-972.  The
+     * problem holds only this capture's tags (compact local indices). */
+    double cam[3] = {camera[0], camera[1], camera[2]};
+    int *oc = calloc(k, sizeof(int)), *ot = malloc(sizeof(int) * k), *loc = malloc(sizeof(int) * k);
+    int nl = 0;
+    for (int j = 0; j < k; ++j) {
+      const int t = obs_tag[o0 + j];
+      int u = -1;
+      for (int i = 0; i < nl; ++i)
+        if (loc[i] == t) { u = i; break; }
+      if (u < 0) { u = nl; loc[nl++] = t; }
+      ot[j] = u;
+    }
+    (void)n_tag;
+    unsigned char *tc = malloc(nl);
+    memset(tc, 1, nl);
+    double *tg = malloc(sizeof(double) * 6 * nl);
+    for (int i = 0; i < nl; ++i) memcpy(tg + 6L * i, tag + 6L * loc[i], 6 * sizeof(double));
+    or_problem pr = {1, nl, k, cam, x, tg, oc, ot, corners + 8L * o0, 1, NULL, tc};
+    or_summary s;
+    status[q] = or_solve(&pr, o, &s, NULL);
+    if (summaries) summaries[q] = s;
+    free(oc); free(ot); free(loc); free(tc); free(tg);
+    ++n_done;
+  }
+  return n_done;
+}

@@ -124,6 +124,31 @@ int or_solve(or_problem *p, const or_options *o, or_summary *s, const or_comm *c
  * CPU baseline. */
 int or_llt_lower(double *A, long n, long ld, int num_threads);
 
+/* ---- initialisers (ar_slam_util.cpp:41-128) ---- */
+/* composeAxisAngle :41-50 (Ceres AngleAxisToQuaternion / QuaternionProduct /
+ * QuaternionToAngleAxis) */
+void or_compose_axis_angle(const double rot1[3], const double rot2[3], double out[3]);
+/* calcInitValues :52-95: (local_x, local_y, local_z, rot_z) of a tag seen in a rect */
+void or_calc_init_values(const double corners[8], double focal, double out[4]);
+/* initCapturePose :98-115 / initArPose :118-128 */
+void or_init_capture_pose(const double corners[8], const double camera[3], const double ar_pose[6],
+                          double inv_cap_pose[6]);
+void or_init_ar_pose(const double corners[8], const double camera[3], const double inv_cap_pose[6],
+                     double ar_pose[6]);
+
+/* ---- localizeMany / localizeOne (ar_slam_util.cpp:888-979) ----
+ * Query q owns observations [q_start[q], q_start[q+1]) in block order.  With
+ * init_from_map, the pose is initialised by initCapturePose from the first
+ * block whose tag is in the map (tag_in_map; NULL = all) and the query is
+ * skipped (status -1, pose untouched) when there is none (:929-933);
+ * otherwise pose[] is the initial value.  Each query is then one ceres::Solve
+ * with its tags and the camera constant (:965, :972).  status[q] = Ceres
+ * termination type, or -1 if skipped; summaries[q] optional. */
+int or_localize_many(int n_query, const int *q_start, const int *obs_tag, const double *corners,
+                     const double camera[3], const double *tag, int n_tag,
+                     const unsigned char *tag_in_map, int init_from_map, double *pose,
+                     const or_options *o, int *status, or_summary *summaries);
+
 #ifdef __cplusplus
 }
 #endif

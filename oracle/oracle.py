@@ -97,6 +97,13 @@ def lib():
         L.or_solve.restype = C.c_int
         L.or_llt_lower.argtypes = [_dp, C.c_long, C.c_long, C.c_int]
         L.or_llt_lower.restype = C.c_int
+        L.or_init_capture_pose.argtypes = [_dp, _dp, _dp, _dp]
+        L.or_init_ar_pose.argtypes = [_dp, _dp, _dp, _dp]
+        L.or_compose_axis_angle.argtypes = [_dp, _dp, _dp]
+        L.or_calc_init_values.argtypes = [_dp, C.c_double, _dp]
+        L.or_localize_many.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_int, C.POINTER(C.c_ubyte),
+                                       C.c_int, _dp, C.POINTER(Options), _ip, C.POINTER(Summary)]
+        L.or_localize_many.restype = C.c_int
         _lib = L
     return _lib
 
@@ -177,6 +184,50 @@ def solve(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, cap_c
 
 def solve_graph(g, **opts):
     return solve(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, **opts)
+
+
+def init_capture_pose(corners, camera, ar_pose):
+    """initCapturePose (ar_slam_util.cpp:98-115) -> inv_cap_pose (6,)."""
+    c, cam, ar = (np.ascontiguousarray(a, np.float64) for a in (corners, camera, ar_pose))
+    out = np.zeros(6)
+    lib().or_init_capture_pose(_p(c), _p(cam), _p(ar), _p(out))
+    return out
+
+
+def init_ar_pose(corners, camera, inv_cap_pose):
+    """initArPose (ar_slam_util.cpp:118-128) -> ar_pose (6,)."""
+    c, cam, cp = (np.ascontiguousarray(a, np.float64) for a in (corners, camera, inv_cap_pose))
+    out = np.zeros(6)
+    lib().or_init_ar_pose(_p(c), _p(cam), _p(cp), _p(out))
+    return out
+
+
+def compose_axis_angle(r1, r2):
+    a, b = (np.ascontiguousarray(x, np.float64) for x in (r1, r2))
+    out = np.zeros(3)
+    lib().or_compose_axis_angle(_p(a), _p(b), _p(out))
+    return out
+
+
+def localize_many(batch, init_from_map=True, pose=None, with_summaries=False, **opts):
+    """localizeMany (ar_slam_util.cpp:888-979) over a synth.LocalizeBatch.
+
+    Returns (pose (Nq,6), status (Nq,) with -1 for skipped queries, summaries or None)."""
+    nq = batch.n_query
+    pose = np.zeros((nq, 6)) if pose is None else np.ascontiguousarray(pose, np.float64).copy()
+    status = np.zeros(nq, np.int32)
+    q_start = np.ascontiguousarray(batch.q_start, np.int32)
+    obs_tag = np.ascontiguousarray(batch.obs_tag, np.int32)
+    corners = np.ascontiguousarray(batch.corners, np.float64)
+    camera = np.ascontiguousarray(batch.camera, np.float64)
+    tag = np.ascontiguousarray(batch.tag, np.float64)
+    tim = None if batch.tag_in_map is None else np.ascontiguousarray(batch.tag_in_map, np.uint8)
+    sums = (Summary * nq)() if with_summaries else None
+    o = default_options(**opts)
+    lib().or_localize_many(nq, _p(q_start, _ip), _p(obs_tag, _ip), _p(corners), _p(camera), _p(tag),
+                           tag.shape[0], None if tim is None else tim.ctypes.data_as(C.POINTER(C.c_ubyte)),
+                           int(bool(init_from_map)), _p(pose), C.byref(o), _p(status, _ip), sums)
+    return pose, status, ([summary_dict(s) for s in sums] if with_summaries else None)
 
 
 def make_comm(rank, sum_fn, max_fn):

@@ -71,8 +71,23 @@ def lm_trace(name, threads=8):
         json.dump(out, f, indent=1)
 
 
+def localize_golden(n_query=4096):
+    """cfg5: localizeMany (ar_slam_util.cpp:888-979) of n_query queries against cfg3's map."""
+    b = synth.make_localize_batch(n_query=n_query)
+    pose, status, sums = O.localize_many(b, with_summaries=True)
+    np.savez_compressed(os.path.join(HERE, "loc_cfg5.npz"), pose=pose, status=status,
+                        initial_cost=np.array([s["initial_cost"] for s in sums]),
+                        final_cost=np.array([s["final_cost"] for s in sums]),
+                        n_iters=np.array([len(s["iterations"]) for s in sums], np.int32),
+                        rule=np.array([s["rule"] for s in sums]))
+
+
 if __name__ == "__main__":
     names = sys.argv[1:] or ["tiny", "small", "medium", "cfg2"]
+    if "loc" in names:
+        localize_golden()
+        print("wrote loc")
+        names = [n for n in names if n != "loc"]
     if "kat" in names or not sys.argv[1:]:
         jacobian_kat()
     for n in names:

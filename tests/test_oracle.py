@@ -208,3 +208,60 @@ def test_dense_llt_matches_numpy(oracle):
     np.testing.assert_allclose(np.tril(L), np.linalg.cholesky(A), rtol=1e-10, atol=1e-10)
     A[5, 5] = -1.0
     assert oracle.llt_lower(A.copy()) == 6
+
+
+def _rotm(w):
+    return synth.rodrigues(np.atleast_2d(w))[0]
+
+
+def test_compose_axis_angle_is_rotation_product(oracle):
+    """composeAxisAngle (ar_slam_util.cpp:41-50) == R(r1) R(r2)."""
+    rng = np.random.default_rng(4)
+    for _ in range(50):
+        r1, r2 = rng.normal(0, 1.2, 3), rng.normal(0, 1.2, 3)
+        out = oracle.compose_axis_angle(r1, r2)
+        np.testing.assert_allclose(_rotm(out), _rotm(r1) @ _rotm(r2), atol=1e-12)
+    np.testing.assert_allclose(oracle.compose_axis_angle(np.zeros(3), np.zeros(3)), np.zeros(3))
+
+
+def test_init_capture_pose_recovers_face_on_capture(oracle):
+    """initCapturePose (:98-115) from a noise-free, nearly face-on view lands near the truth,
+    and initArPose (:118-128) inverts it."""
+    b = synth.make_localize_batch(n_query=64, noise_px=0.0)
+    errs = []
+    for q in range(b.n_query):
+        o = b.q_start[q]
+        tag = b.tag[b.obs_tag[o]]
+        p = oracle.init_capture_pose(b.corners[o], b.camera, tag)
+        errs.append(np.linalg.norm(p[:3] - b.pose_true[q, :3]))
+        back = oracle.init_ar_pose(b.corners[o], b.camera, p)
+        np.testing.assert_allclose(back[:3], tag[:3], atol=1e-9)
+        np.testing.assert_allclose(_rotm(back[3:]), _rotm(tag[3:]), atol=1e-9)
+    assert np.median(errs) < 0.3   # ignores tilt and perspective: tens of cm, not metres
+
+
+def test_localize_many_golden(oracle):
+    """cfg5 (4096 queries against cfg3's map) matches the committed localize fixture."""
+    gold = np.load(os.path.join(GOLDEN, "loc_cfg5.npz"))
+    b = synth.make_localize_batch(n_query=4096)
+    pose, status, sums = oracle.localize_many(b, with_summaries=True)
+    np.testing.assert_array_equal(status, gold["status"])
+    np.testing.assert_allclose(pose, gold["pose"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose([s["final_cost"] for s in sums], gold["final_cost"], rtol=1e-12)
+    assert (status == 0).all()                        # every query converges
+    R = synth.rodrigues(pose[:, 3:])
+    Rt = synth.rodrigues(b.pose_true[:, 3:])
+    ang = np.arccos(np.clip((np.einsum("nij,nij->n", R, Rt) - 1) / 2, -1, 1))
+    assert np.median(np.linalg.norm(pose[:, :3] - b.pose_true[:, :3], axis=1)) < 5e-3
+    assert np.median(ang) < 5e-3
+
+
+def test_localize_skip_rule(oracle):
+    """localizeOne skips a capture with no map-connected tag (:929-933)."""
+    b = synth.make_localize_batch(n_query=8)
+    b.tag_in_map = np.ones(b.tag.shape[0], np.uint8)
+    b.tag_in_map[b.obs_tag[b.q_start[2]:b.q_start[3]]] = 0
+    pose0 = np.full((8, 6), 7.0)
+    pose, status, _ = oracle.localize_many(b, pose=pose0)
+    assert status[2] == -1 and (pose[2] == 7.0).all()
+    assert (status[[0, 1, 3]] == 0).all()

@@ -1,9 +1,15 @@
-import numpy as np, sys
+import sys
+import numpy as np
 sys.path.insert(0, '.')
 from ar_slam_amd import lm, synth
-g = synth.config_graph("medium")
-tag_const = np.ones(g.n_tag, np.uint8)
-ours = lm.solve_soa(g.camera_true.copy(), g.cap, g.tag_true, g.obs_cap, g.obs_tag, g.corners, camera_const=True, tag_const=tag_const)
-s = ours[3]
-print({k: v for k, v in s.items() if k != 'iterations'})
-for it in s['iterations'][:8]: print(it)
+from oracle import oracle as O
+b = synth.make_localize_batch(n_query=512)
+pose, res = lm.localize_many(b)
+pose_o, st, sums = O.localize_many(b, with_summaries=True)
+for q in (10, 19):
+    print("query", q, "gpu:", {k: res[k][q] for k in ("status", "rule", "num_iterations", "num_successful_steps", "num_unsuccessful_steps", "initial_cost", "final_cost")})
+    s = sums[q]
+    print("  oracle:", s["termination"], s["rule"], s["initial_cost"], s["final_cost"], s["num_successful_steps"], s["num_unsuccessful_steps"])
+    for it in s["iterations"]:
+        print("   ", it["iteration"], repr(it["cost"]), it["cost_change"], it["relative_decrease"], it["trust_region_radius"], it["step_is_successful"], it["step_norm"])
+    print("  pose diff", pose[q] - pose_o[q])
