@@ -17,6 +17,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libarslam_lm.so")
 SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "debug_api.hip", "llt_plan.cpp",
            "host_structure.cpp", "localize.hip"]
+HOST = os.path.join(HERE, "host")
+HOST_SOURCES = ["yaml_lite.cpp", "ar_slam_solver.cpp", "slam_capi.cpp"]   # plain C++ (g++)
 ARCH = os.environ.get("ARSLAM_ARCH", "gfx950")
 
 
@@ -31,7 +33,8 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", f) for f in ("arslam_lm.h", "arslam_lm_debug.h", "arslam_localize.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(HOST, f) for f in os.listdir(HOST)] + \
+        [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
@@ -47,6 +50,14 @@ def build(force=False, verbose=False):
     for src in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
         cmd = [hipcc()] + flags + (["-x", "hip"] if src.endswith(".cpp") else []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+    for src in HOST_SOURCES:
+        obj = os.path.join(objdir, "host_" + os.path.splitext(src)[0] + ".o")
+        cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+               "-I", HOST, "-c", os.path.join(HOST, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -45,7 +45,15 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_reduced_plan",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
-           "arslam_localizer_load", "arslam_localizer_solve"]
+           "arslam_localizer_load", "arslam_localizer_solve",
+           "arslam_slam_create", "arslam_slam_destroy", "arslam_slam_set_verbose", "arslam_slam_load_yaml",
+           "arslam_slam_load_yaml_string", "arslam_slam_save_yaml", "arslam_slam_add_detections",
+           "arslam_slam_solve", "arslam_slam_solve_incremental", "arslam_slam_localize_many",
+           "arslam_slam_num_captures", "arslam_slam_num_arucos", "arslam_slam_num_blocks",
+           "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_capture",
+           "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
+           "arslam_slam_block", "arslam_slam_camera", "arslam_slam_set_camera",
+           "arslam_slam_get_transforms", "arslam_slam_camera_info"]
 
 _dp = C.POINTER(C.c_double)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
@@ -141,6 +149,17 @@ def lib():
     L.arslam_lm_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
     L.arslam_lm_set_comm_callback.argtypes = [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, C.c_void_p]
     L.arslam_lm_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
+    for fn in ("arslam_slam_destroy", "arslam_slam_set_verbose", "arslam_slam_load_yaml",
+               "arslam_slam_load_yaml_string", "arslam_slam_save_yaml", "arslam_slam_add_detections",
+               "arslam_slam_solve", "arslam_slam_solve_incremental", "arslam_slam_localize_many",
+               "arslam_slam_num_captures", "arslam_slam_num_arucos", "arslam_slam_num_blocks",
+               "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_capture",
+               "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
+               "arslam_slam_block", "arslam_slam_camera", "arslam_slam_set_camera",
+               "arslam_slam_get_transforms", "arslam_slam_camera_info"):
+        getattr(L, fn).argtypes = None
+    L.arslam_slam_destroy.restype = None
+    L.arslam_slam_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
     L.arslam_localize_many.argtypes = [C.POINTER(LocalizeBatchC), C.POINTER(Options), C.POINTER(LocalizeResult)]
     L.arslam_localizer_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
     L.arslam_localizer_destroy.argtypes = [C.c_void_p]
@@ -475,3 +494,140 @@ class Localizer:
             self.close()
         except Exception:
             pass
+
+
+# ---- ArSlamSolver host mirror (include/arslam_slam.h) ----
+class Transform(C.Structure):
+    _fields_ = [("child_frame_id", C.c_char * 128), ("translation", C.c_double * 3),
+                ("rotation", C.c_double * 4)]
+
+
+class SlamSolver:
+    """ArSlamSolver (ar_slam_util.hpp:361-497) over the C++ host mirror: captures, arucos and
+    blocks addressed by index; uids / ids are strings."""
+
+    def __init__(self, verbose=False, **opts):
+        self._h = C.c_void_p()
+        _check(lib().arslam_slam_create(C.byref(self._h), C.byref(make_options(**opts))))
+        lib().arslam_slam_set_verbose(self._h, int(bool(verbose)))
+
+    def close(self):
+        if self._h:
+            lib().arslam_slam_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_yaml(self, path):
+        _check(lib().arslam_slam_load_yaml(self._h, str(path).encode()))
+
+    def load_yaml_string(self, text):
+        _check(lib().arslam_slam_load_yaml_string(self._h, text.encode()))
+
+    def save_yaml(self, path):
+        _check(lib().arslam_slam_save_yaml(self._h, str(path).encode()))
+
+    def add_detections(self, capture_uid, ids, corners, image_width=1020, image_height=768, image_path=""):
+        """Detections.msg -> capture index, or None when ignored (addDetections :591-627)."""
+        corners = _f64(corners, (-1, 8))
+        n = corners.shape[0]
+        if len(ids) != n:
+            raise ValueError("one id per detection")
+        arr = (C.c_char_p * max(n, 1))(*[str(i).encode() for i in ids])
+        idx = C.c_int(-1)
+        _check(lib().arslam_slam_add_detections(self._h, str(capture_uid).encode(), C.c_int(image_width),
+                                                C.c_int(image_height), str(image_path).encode(), C.c_int(n),
+                                                arr, corners.ctypes.data_as(_dp), C.byref(idx)))
+        return None if idx.value < 0 else idx.value
+
+    def solve(self):
+        _check(lib().arslam_slam_solve(self._h))
+
+    def solve_incremental(self):
+        _check(lib().arslam_slam_solve_incremental(self._h))
+
+    def localize_many(self, first_loc_cap_idx):
+        _check(lib().arslam_slam_localize_many(self._h, C.c_int(first_loc_cap_idx)))
+
+    @property
+    def num_captures(self):
+        return lib().arslam_slam_num_captures(self._h)
+
+    @property
+    def num_arucos(self):
+        return lib().arslam_slam_num_arucos(self._h)
+
+    @property
+    def num_blocks(self):
+        return lib().arslam_slam_num_blocks(self._h)
+
+    @property
+    def num_solves(self):
+        return lib().arslam_slam_num_solves(self._h)
+
+    def last_summary(self):
+        s = Summary()
+        _check(lib().arslam_slam_last_summary(self._h, C.byref(s)))
+        return s.to_dict()
+
+    def capture(self, c):
+        buf = C.create_string_buffer(256)
+        pose = np.zeros(6)
+        _check(lib().arslam_slam_capture(self._h, C.c_int(c), buf, C.c_int(256), pose.ctypes.data_as(_dp)))
+        return buf.value.decode(), pose
+
+    def set_capture_pose(self, c, pose):
+        p = _f64(pose).reshape(6).copy()
+        _check(lib().arslam_slam_set_capture_pose(self._h, C.c_int(c), p.ctypes.data_as(_dp)))
+
+    def aruco(self, a):
+        buf = C.create_string_buffer(256)
+        pose = np.zeros(6)
+        init = C.c_int(0)
+        _check(lib().arslam_slam_aruco(self._h, C.c_int(a), buf, C.c_int(256), pose.ctypes.data_as(_dp),
+                                       C.byref(init)))
+        return buf.value.decode(), pose, bool(init.value)
+
+    def set_aruco_pose(self, a, pose):
+        p = _f64(pose).reshape(6).copy()
+        _check(lib().arslam_slam_set_aruco_pose(self._h, C.c_int(a), p.ctypes.data_as(_dp)))
+
+    def block(self, b):
+        c, a, added = C.c_int(), C.c_int(), C.c_int()
+        rect = np.zeros(8)
+        _check(lib().arslam_slam_block(self._h, C.c_int(b), C.byref(c), C.byref(a), rect.ctypes.data_as(_dp),
+                                       C.byref(added)))
+        return c.value, a.value, rect, bool(added.value)
+
+    def camera(self):
+        p = np.zeros(3)
+        w, h = C.c_int(), C.c_int()
+        _check(lib().arslam_slam_camera(self._h, p.ctypes.data_as(_dp), C.byref(w), C.byref(h)))
+        return p, (None if w.value < 0 else (w.value, h.value))
+
+    def set_camera(self, params):
+        p = _f64(params).reshape(3).copy()
+        _check(lib().arslam_slam_set_camera(self._h, p.ctypes.data_as(_dp)))
+
+    def capture_poses(self):
+        return np.array([self.capture(c)[1] for c in range(self.num_captures)]).reshape(-1, 6)
+
+    def aruco_poses(self):
+        return np.array([self.aruco(a)[1] for a in range(self.num_arucos)]).reshape(-1, 6)
+
+    def get_transforms(self):
+        n = C.c_int(0)
+        _check(lib().arslam_slam_get_transforms(self._h, None, C.c_int(0), C.byref(n)))
+        arr = (Transform * max(n.value, 1))()
+        _check(lib().arslam_slam_get_transforms(self._h, arr, C.c_int(n.value), C.byref(n)))
+        return [(t.child_frame_id.decode(), np.array(t.translation[:]), np.array(t.rotation[:]))
+                for t in arr[:n.value]]
+
+    def camera_info(self):
+        k, p = np.zeros(9), np.zeros(12)
+        _check(lib().arslam_slam_camera_info(self._h, k.ctypes.data_as(_dp), p.ctypes.data_as(_dp)))
+        return k.reshape(3, 3), p.reshape(3, 4)

@@ -1,0 +1,116 @@
+"""GPU tests of the ArSlamSolver host mirror's drivers against the oracle's
+restatement of the same drivers (oracle/driver.py):
+
+  * solve()            BFS from the best capture, one full solve per capture  ar_slam_util.cpp:744-866
+  * solveIncremental() the ROS node's flow                                   :629-742
+  * localizeMany()     queries against the mapped tags                       :888-979
+
+Each driver step is a ceres::Solve of the whole problem so far, so rounding
+differences between the device and the oracle compound over the chain; the
+tolerances are looser than one solve's (tests/test_gpu_parity.py):
+final focal and costs 1e-6 relative, poses 1e-5 (metres / radians).
+"""
+import numpy as np
+import pytest
+
+from ar_slam_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _detections(g, caps=None):
+    caps = range(g.n_cap) if caps is None else caps
+    for c in caps:
+        sel = g.obs_cap == c
+        yield f"cap{c}", [f"tag_{t}" for t in g.obs_tag[sel]], g.corners[sel]
+
+
+def _run_both(lm, g, driver, camera=None):
+    from oracle.driver import OracleSlam
+    s = lm.SlamSolver()
+    o = OracleSlam()
+    if camera is not None:
+        s.set_camera(camera)
+        o.camera = np.array(camera, np.float64)
+    for uid, ids, corners in _detections(g):
+        s.add_detections(uid, ids, corners)
+        o.add_detections(uid, ids, corners)
+    getattr(s, driver)()
+    getattr(o, driver)()
+    return s, o
+
+
+def _compare(s, o):
+    assert s.num_solves == o.n_solves
+    last = s.last_summary()
+    assert last["termination"] == o.last_summary["termination"]
+    assert abs(last["final_cost"] - o.last_summary["final_cost"]) <= 1e-6 * o.last_summary["final_cost"]
+    cam = s.camera()[0]
+    assert abs(cam[0] - o.camera[0]) <= 1e-6 * o.camera[0]
+    cp = s.capture_poses()
+    np.testing.assert_allclose(cp, np.array([c["pose"] for c in o.captures]), atol=1e-5)
+    ap = s.aruco_poses()
+    np.testing.assert_allclose(ap, np.array([a["pose"] for a in o.arucos]), atol=1e-5)
+    for a in range(s.num_arucos):
+        assert s.aruco(a)[2] == o.arucos[a]["initialized"]
+
+
+@pytest.mark.parametrize("name", ["tiny", "small"])
+def test_bfs_solve_matches_oracle_driver(lm, name):
+    g = synth.config_graph(name)
+    s, o = _run_both(lm, g, "solve", camera=g.camera)
+    _compare(s, o)
+    assert synth.rms_px(s.last_summary()["final_cost"], g.n_obs) < 1.0
+
+
+def test_bfs_solve_from_reference_default_focal(lm):
+    """The reference starts from f = 3000 (CameraParams, ar_slam_util.hpp:68-72)."""
+    g = synth.config_graph("tiny")
+    s, o = _run_both(lm, g, "solve")
+    _compare(s, o)
+
+
+def test_incremental_solve_matches_oracle_driver(lm):
+    g = synth.config_graph("small")
+    s, o = _run_both(lm, g, "solve_incremental", camera=g.camera)
+    _compare(s, o)
+    assert s.num_solves == g.n_cap          # every capture got connected and solved once
+
+
+def test_localize_many_after_mapping(lm, oracle):
+    """Map with the first 40 captures, then localize the other 10 against it (ar_loc flow)."""
+    g = synth.config_graph("small")
+    s = lm.SlamSolver()
+    s.set_camera(g.camera)
+    for uid, ids, corners in _detections(g, range(40)):
+        s.add_detections(uid, ids, corners)
+    s.solve()
+    first = s.num_captures
+    for uid, ids, corners in _detections(g, range(40, g.n_cap)):
+        s.add_detections(uid, ids, corners)
+    s.localize_many(first)
+    # the oracle localizes the same queries against the same (device-mapped) map
+    tag_ids = [s.aruco(a)[0] for a in range(s.num_arucos)]
+    tags = s.aruco_poses()
+    in_map = np.zeros(len(tag_ids), np.uint8)
+    for b in range(s.num_blocks):
+        c, a, _, _ = s.block(b)
+        if c < first:
+            in_map[a] = 1
+    q_start, obs_tag, corners = [0], [], []
+    for c in range(first, s.num_captures):
+        for b in range(s.num_blocks):
+            cb, a, rect, _ = s.block(b)
+            if cb == c:
+                obs_tag.append(a)
+                corners.append(rect)
+        q_start.append(len(obs_tag))
+    batch = synth.LocalizeBatch(s.camera()[0], tags, np.array(q_start, np.int32), np.array(obs_tag, np.int32),
+                                np.array(corners), None, in_map)
+    pose_o, status_o, _ = oracle.localize_many(batch)
+    poses = s.capture_poses()[first:]
+    for q in range(len(status_o)):
+        if status_o[q] < 0:
+            continue
+        np.testing.assert_allclose(poses[q], pose_o[q], atol=1e-7)
+    assert (status_o >= 0).sum() >= 8        # most queries see a mapped tag

@@ -1,0 +1,124 @@
+"""CPU tests of the C++ ArSlamSolver host mirror (ar_slam_amd/host, include/arslam_slam.h):
+the data store, addDetections, the YAML map format and the ROS-facing getters,
+none of which need a device.  Each behaviour cites the reference line it follows."""
+import numpy as np
+import pytest
+
+from ar_slam_amd import synth
+
+
+@pytest.fixture(scope="module")
+def L():
+    from ar_slam_amd import build, lm
+    build.build()
+    return lm
+
+
+def _fill(L, g, s=None):
+    s = s or L.SlamSolver()
+    for c in range(g.n_cap):
+        sel = g.obs_cap == c
+        s.add_detections(f"cap{c}", [f"tag_{t}" for t in g.obs_tag[sel]], g.corners[sel])
+    return s
+
+
+def test_add_detections_builds_the_store(L):
+    """addDetections (:591-627): one capture per message, getOrAddAruco, addBlock."""
+    g = synth.config_graph("tiny")
+    s = _fill(L, g)
+    assert s.num_captures == g.n_cap
+    assert s.num_blocks == g.n_obs
+    assert s.num_arucos == len(np.unique(g.obs_tag))
+    params, size = s.camera()
+    assert params[0] == 3000.0 and size == (1020, 768)   # CameraParams default focal (:68-72)
+    c, a, rect, added = s.block(3)
+    assert c == g.obs_cap[3] and not added
+    np.testing.assert_array_equal(rect, g.corners[3])
+    assert s.add_detections("empty", [], np.zeros((0, 8))) is None           # no detections
+    assert s.add_detections("other", ["x"], np.zeros((1, 8)), image_width=640) is None   # size mismatch
+    with pytest.raises(L.LMError):                                             # duplicate uid (:423-425)
+        s.add_detections("cap0", ["tag_1"], np.zeros((1, 8)))
+
+
+def test_yaml_round_trip_is_exact(L, tmp_path):
+    """saveYaml (:387-465) then loadYaml (:304-384) reproduces the store bit for bit."""
+    g = synth.config_graph("small")
+    s = _fill(L, g)
+    rng = np.random.default_rng(1)
+    for c in range(s.num_captures):
+        s.set_capture_pose(c, rng.normal(size=6))
+    for a in range(s.num_arucos):
+        s.set_aruco_pose(a, rng.normal(size=6))
+    s.set_camera([912.125, 1e-3, -2e-5])
+    p = tmp_path / "map.yaml"
+    s.save_yaml(p)
+    t = L.SlamSolver()
+    t.load_yaml(p)
+    assert (t.num_captures, t.num_arucos, t.num_blocks) == (s.num_captures, s.num_arucos, s.num_blocks)
+    for c in range(s.num_captures):
+        assert t.capture(c)[0] == s.capture(c)[0]
+        np.testing.assert_array_equal(t.capture(c)[1], s.capture(c)[1])
+    for a in range(s.num_arucos):
+        assert t.aruco(a)[0] == s.aruco(a)[0]
+        np.testing.assert_array_equal(t.aruco(a)[1], s.aruco(a)[1])
+    for b in range(s.num_blocks):
+        sb, tb = s.block(b), t.block(b)
+        assert sb[:2] == tb[:2]
+        np.testing.assert_array_equal(sb[2], tb[2])
+    np.testing.assert_array_equal(t.camera()[0], s.camera()[0])
+    assert t.camera()[1] == (1020, 768)
+
+
+def test_yaml_matches_pyyaml(L, tmp_path):
+    """The emitted map is standard YAML with the reference's schema, and a map written by
+    another emitter (PyYAML, block style) loads."""
+    yaml = pytest.importorskip("yaml")
+    g = synth.config_graph("tiny")
+    s = _fill(L, g)
+    p = tmp_path / "m.yaml"
+    s.save_yaml(p)
+    d = yaml.safe_load(open(p))
+    assert set(d) == {"blocks", "captures", "arucos", "camera"}
+    assert len(d["blocks"]) == g.n_obs and d["blocks"][0]["capture"] == "cap0"
+    assert d["camera"]["params"] == [3000.0, 0.0, 0.0] and d["camera"]["width"] == 1020
+    np.testing.assert_array_equal(d["blocks"][5]["aruco_rect"], g.corners[5])
+    # PyYAML's own block-style emission, with comments and quoting, loads back
+    d["captures"]["cap0"]["inv_pose"] = [0.5, -1.0, 2.0, 0.1, 0.2, 0.3]
+    text = "# written by another tool\n---\n" + yaml.safe_dump(d, default_flow_style=False, sort_keys=True)
+    t = L.SlamSolver()
+    t.load_yaml_string(text)
+    assert t.num_blocks == g.n_obs and t.num_captures == g.n_cap
+    c0 = [c for c in range(t.num_captures) if t.capture(c)[0] == "cap0"][0]
+    np.testing.assert_array_equal(t.capture(c0)[1], [0.5, -1.0, 2.0, 0.1, 0.2, 0.3])
+
+
+def test_yaml_errors(L):
+    t = L.SlamSolver()
+    with pytest.raises(L.LMError):   # aruco_rect with 7 values (:353-355)
+        t.load_yaml_string("captures:\n  c:\n    inv_pose: [0,0,0,0,0,0]\n    img_fn: a\n"
+                           "arucos:\n  t:\n    pose: [0,0,0,0,0,0]\n"
+                           "blocks:\n  - capture: c\n    aruco: t\n    aruco_rect: [1,2,3,4,5,6,7]\n"
+                           "camera:\n  params: [1,0,0]\n  width: 1\n  height: 1\n")
+    with pytest.raises(L.LMError):   # unknown capture in a block (capture_map_.at)
+        L.SlamSolver().load_yaml_string("blocks:\n  - capture: nope\n    aruco: t\n    aruco_rect: []\n")
+
+
+def test_transforms_and_camera_info(L):
+    """getTransforms (:1028-1075): arucos as world<-tag, captures inverted; getCameraInfo (:1077-1126)."""
+    g = synth.config_graph("tiny")
+    s = _fill(L, g)
+    s.set_capture_pose(0, [1.0, 2.0, 3.0, 0.0, 0.0, 0.5])
+    s.set_aruco_pose(0, [4.0, 5.0, 6.0, 0.0, 0.3, 0.0])
+    ts = s.get_transforms()
+    assert len(ts) == s.num_arucos + s.num_captures
+    name, tr, q = ts[0]
+    assert name == s.aruco(0)[0]
+    np.testing.assert_allclose(tr, [4, 5, 6])
+    np.testing.assert_allclose(q, [np.cos(0.15), 0, np.sin(0.15), 0], atol=1e-15)
+    name, tr, q = ts[s.num_arucos]
+    assert name == "cap0"
+    np.testing.assert_allclose(tr, [-1, -2, -3])
+    np.testing.assert_allclose(q, [np.cos(0.25), 0, 0, -np.sin(0.25)], atol=1e-15)
+    k, p = s.camera_info()
+    np.testing.assert_allclose(k, [[3000, 0, 510], [0, 3000, 384], [0, 0, 1]])
+    np.testing.assert_allclose(p[:, :3], k)
