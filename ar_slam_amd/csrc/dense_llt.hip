@@ -265,6 +265,54 @@ __device__ void blocked_trsm64(double *X, const double *D, const double *inv, co
   }
 }
 
+// Inverse X = L^{-1} of the 64x64 lower factor in D (after blocked_potrf64),
+// built in LDS as its transpose XT (XT[c][r] = X[r][c]) from the 16x16
+// diagonal-block inverses Li_p in LTd:  X_qq = Li_q,
+//   X_pq = -Li_p sum_{r=q}^{p-1} L_pr X_rq   (p > q).
+// Wave q owns column block q (three dependent 16x16 MFMA steps at most);
+// its 16x16 scratch sits in a part of XT that stays structurally zero.
+__device__ void blocked_trinv64(const double *D, const double *LTd, double *XT, int tid) {
+  const int q = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lk = lane >> 4;
+  const double *Lq = LTd + q * 16 * LI;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {   // XT block (q,q) = Li_q^T
+    const int idx = lane + 64 * e, i = idx >> 4, j = idx & 15;
+    XT[(16 * q + j) * LQ + 16 * q + i] = (j <= i) ? Lq[i * LI + j] : 0.0;
+  }
+  double *scr = XT + (q == 0 ? 48 : 16 * q) * LQ;   // columns 0..15 of row block 3 (q=0) or q
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int p = q + 1; p < 4; ++p) {
+    dbl4 acc = {0, 0, 0, 0};
+    for (int r = q; r < p; ++r)
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const double a = D[(16 * p + li) * LQ + 16 * r + 4 * k4 + lk];
+        const double b = XT[(16 * q + li) * LQ + 16 * r + 4 * k4 + lk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+    // acc[reg] = M[lk + 4 reg][li]; scratch rows = M^T rows
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) scr[li * LQ + lk + 4 * reg] = acc[reg];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    dbl4 x = {0, 0, 0, 0};
+    const double *Lp = LTd + p * 16 * LI;
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4)
+      x = __builtin_amdgcn_mfma_f64_16x16x4f64(Lp[li * LI + 4 * k4 + lk], scr[li * LQ + 4 * k4 + lk], x, 0, 0, 0);
+    // x[reg] = (Li_p M)[lk + 4 reg][li] = -X_pq[...]
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) XT[(16 * q + li) * LQ + 16 * p + lk + 4 * reg] = -x[reg];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // Panel tasks of one level: task (i,k) factors the diagonal tile (k,k) (every
 // task of column k does so redundantly, keeping the level to one launch) and
 // either stores L_kk (i == k) or solves tile (i,k) against it.  L_kk goes to
@@ -300,7 +348,17 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, const int
     return;
   }
   if (ti == k) {
+    // L_kk, and its inverse (for the backward solve) while the column's
+    // other tasks run their TRSMs
     store_tile_wg(Ld + (long)k * T64 * T64, T64, D, tid, true);
+    blocked_trinv64(D, LTd, X, tid);
+    __syncthreads();
+    double *Xg = Ld + ((long)T + k) * T64 * T64;
+#pragma unroll 4
+    for (int m = 0; m < 16; ++m) {
+      const int e = m * 256 + tid, r = e >> 6, c = e & 63;
+      Xg[e] = (r >= c) ? X[c * LQ + r] : 0.0;
+    }
     return;
   }
   STAMP(2);
@@ -475,53 +533,45 @@ __global__ __launch_bounds__(256) void k_bs_gather(const double *__restrict__ S,
   if (w == 0) part_out[(long)blockIdx.x * T64 + lane] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
 }
 
-__global__ __launch_bounds__(64) void k_bs_solve(const double *__restrict__ Ld, long nR,
-                                                 const int *__restrict__ cols,
-                                                 const int *__restrict__ gbeg,
-                                                 const double *__restrict__ z,
-                                                 const double *__restrict__ part,
-                                                 double *__restrict__ yF,
-                                                 const int *__restrict__ flag) {
-  __shared__ double Lk[T64 * LP];
-  __shared__ double y[T64];
+// y_k = L_kk^{-T} (z_k - sum of the column's gathered partials), with the
+// inverse X_kk from the panel: y[c] = sum_r X[r][c] acc[r] (4 waves x 16 rows,
+// fixed-order combine).  Rows past nR carry acc = 0 and y = 0.
+__global__ __launch_bounds__(256) void k_bs_solve(const double *__restrict__ Xinv, long nR,
+                                                  const int *__restrict__ cols,
+                                                  const int *__restrict__ gbeg,
+                                                  const double *__restrict__ z,
+                                                  const double *__restrict__ part,
+                                                  double *__restrict__ yF,
+                                                  const int *__restrict__ flag) {
+  __shared__ double accs[T64];
+  __shared__ double red[4][T64];
   if (*flag) return;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int k = cols[blockIdx.x];
   const long row0 = (long)k * T64;
-  load_tile64(Ld + (long)k * T64 * T64, T64, Lk, lane);
-  double acc = 0.0;
-  const int ga = gbeg[blockIdx.x], gb = gbeg[blockIdx.x + 1];
-  for (int g = ga; g < gb; g += 8) {   // 8 loads in flight, summed in plan order
-    double v[8];
+  if (w == 0) {
+    double acc = 0.0;
+    const int ga = gbeg[blockIdx.x], gb = gbeg[blockIdx.x + 1];
+    for (int g = ga; g < gb; g += 8) {   // 8 loads in flight, summed in plan order
+      double v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = part[(long)min(g + u, gb - 1) * T64 + lane];
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)min(g + u, gb - 1) * T64 + lane];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc += (g + u < gb) ? v[u] : 0.0;
+      for (int u = 0; u < 8; ++u) acc += (g + u < gb) ? v[u] : 0.0;
+    }
+    accs[lane] = (row0 + lane < nR) ? z[row0 + lane] - acc : 0.0;
   }
-  double zr = (row0 + lane < nR) ? z[row0 + lane] - acc : 0.0;
   __syncthreads();
-  const double my_inv = (row0 + lane < nR) ? 1.0 / Lk[lane * LP + lane] : 0.0;   // y = 0 past nR
-  double yv_own = 0.0;
-  for (int p = 3; p >= 0; --p) {
-    const int b0 = 16 * p;
-    for (int rr = 15; rr >= 0; --rr) {
-      const int r = b0 + rr;
-      const double yv = readlane_d(zr * my_inv, r);
-      if (lane == r) yv_own = yv;
-      if (lane >= b0 && lane < r) zr -= Lk[r * LP + lane] * yv;
-    }
-    y[lane] = yv_own;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < b0) {
-      double a2 = 0.0;
+  const double *X = Xinv + (long)k * T64 * T64;
+  double s = 0.0;
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) a2 += Lk[(b0 + rr) * LP + lane] * y[b0 + rr];
-      zr -= a2;
-    }
+  for (int rr = 0; rr < 16; ++rr) {
+    const int r = 16 * w + rr;
+    s += X[r * T64 + lane] * accs[r];
   }
-  if (row0 + lane < nR) yF[row0 + lane] = yv_own;
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && row0 + lane < nR) yF[row0 + lane] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // tests only: copy the diagonal factors L_kk into their S tiles
@@ -574,7 +624,8 @@ void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double 
       hipLaunchKernelGGL(k_bs_gather, dim3((unsigned)ng), dim3(256), 0, s, S, P.tile_id, P.T, nR, P.bs_gather + g0, yF,
                          P.bs_part + (long)g0 * T64, flag);
     const int b0 = P.h_bs_off[l], nc = P.h_bs_off[l + 1] - b0;
-    hipLaunchKernelGGL(k_bs_solve, dim3((unsigned)nc), dim3(64), 0, s, P.ldiag, nR, P.bs_cols + b0,
+    hipLaunchKernelGGL(k_bs_solve, dim3((unsigned)nc), dim3(256), 0, s, P.ldiag + (long)P.T * T64 * T64, nR,
+                       P.bs_cols + b0,
                        P.bs_gbeg + b0, z, P.bs_part, yF, flag);
   }
 }

@@ -193,7 +193,7 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   plan.bs_gbeg = upload(plan.h_gbeg, s);
   check(hipMalloc(&plan.bs_part, std::max<size_t>(plan.h_gather.size(), 1) * 64 * sizeof(double)), "hipMalloc(bs_part)");
   plan.tile_id = upload(plan.h_tile_id, s);
-  check(hipMalloc(&plan.ldiag, (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
+  check(hipMalloc(&plan.ldiag, 2 * (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
   check(hipStreamSynchronize(s), "plan sync");
 }
 

@@ -92,7 +92,7 @@ struct LltPlan {
   std::vector<int> h_tile_id;
   long n_tiles = 0;             // tiles of the factor (compact storage = n_tiles * 4096 doubles)
   long n_assembled = 0;         // tiles the Schur assembly writes (numbered first)
-  double *ldiag = nullptr;      // T x 64 x 64 diagonal factors L_kk (row-major, ld 64)
+  double *ldiag = nullptr;      // 2T x 64 x 64: diagonal factors L_kk, then their inverses (row-major)
   std::vector<int> h_panel_off;     // [nlev+1]
   std::vector<int> h_upd_off;       // [nlev+1]
   std::vector<int> h_bs_off;        // [nlev+1], in backward (root-first) order
