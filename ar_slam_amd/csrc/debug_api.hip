@@ -4,6 +4,9 @@
 #include "arslam_lm.h"
 #include "arslam_lm_debug.h"
 
+#include <cstdlib>
+#include <cstdio>
+#include <unistd.h>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -50,7 +53,14 @@ extern "C" int arslam_debug_residual_jacobian(int n, const double *cam, const do
   return ARSLAM_OK;
 }
 
+extern "C" int arslam_debug_dense_llt_ex(long n, double *A, const double *b, double *y, int *info,
+                                         int executor);
 extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double *y, int *info) {
+  return arslam_debug_dense_llt_ex(n, A, b, y, info, 0);
+}
+
+extern "C" int arslam_debug_dense_llt_ex(long n, double *A, const double *b, double *y, int *info,
+                                         int executor) {
   if (n <= 0 || !A || !b || !y || !info) return ARSLAM_E_INVALID_ARG;
   const long N = (n + 1 + arslam::kTile - 1) / arslam::kTile * arslam::kTile;
   const int T = (int)(N / arslam::kTile);
@@ -85,7 +95,34 @@ extern "C" int arslam_debug_dense_llt(long n, double *A, const double *b, double
   DBG_CHECK(hipMalloc(&d_flag, sizeof(int)));
   DBG_CHECK(hipMemcpy(d_S, tiles.data(), tiles.size() * sizeof(double), hipMemcpyHostToDevice));
   DBG_CHECK(hipMemset(d_flag, 0, sizeof(int)));
-  arslam::launch_dense_llt(plan, d_S, d_flag, 0);
+  const char *eg = std::getenv("ARSLAM_DAG_GRID");
+  const int grid = eg ? std::atoi(eg) : 512;
+  if (executor == 1 && std::getenv("ARSLAM_DAG_PROGRESS")) {
+    // debug: host-visible progress words, polled while the kernel runs
+    int *prog = nullptr;
+    DBG_CHECK(hipHostMalloc(&prog, 4 * sizeof(int) * grid, hipHostMallocCoherent));
+    std::memset(prog, 0xff, 4 * sizeof(int) * grid);
+    hipStream_t st;
+    DBG_CHECK(hipStreamCreate(&st));
+    DBG_CHECK(hipMemcpy(d_S, tiles.data(), tiles.size() * sizeof(double), hipMemcpyHostToDevice));
+    arslam::launch_dense_llt_dag(plan, d_S, d_flag, st, grid, prog);
+    for (int it = 0; it < 30; ++it) {
+      usleep(100000);
+      if (hipStreamQuery(st) == hipSuccess) break;
+      std::fprintf(stderr, "t=%d00ms:", it + 1);
+      for (int g = 0; g < grid && g < 16; ++g)
+        std::fprintf(stderr, " [wg%d t%d ph%d ty%d]", g, ((volatile int *)prog)[4 * g], ((volatile int *)prog)[4 * g + 1],
+                     ((volatile int *)prog)[4 * g + 2]);
+      std::fprintf(stderr, "\n");
+    }
+    if (hipStreamQuery(st) != hipSuccess) {
+      std::fprintf(stderr, "DAG kernel did not finish\n");
+      std::fflush(stderr);
+      std::_Exit(3);
+    }
+  }
+  if (executor == 1) arslam::launch_dense_llt_dag(plan, d_S, d_flag, 0, grid);
+  else arslam::launch_dense_llt(plan, d_S, d_flag, 0);
   arslam::launch_dense_back_solve(plan, d_S, n, d_z, d_y, d_flag, 0);
   arslam::launch_scatter_diag(plan, d_S, 0);
   DBG_CHECK(hipGetLastError());
@@ -131,6 +168,11 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
       info->n_update_items = (long)plan.h_items.size();
       info->n_split_targets = (long)plan.h_split.size();
       info->update_flops = plan.total_upd_flops;
+      info->n_dag_tasks = plan.n_dag_tasks;
+      info->dag_valid = arslam::dag_check(plan) ? 1 : 0;
+      for (int wk : {1, 2, 7, 64, 512})
+        for (unsigned seed = 1; seed <= 3 && info->dag_valid; ++seed)
+          if (!arslam::dag_simulate(plan, wk, seed)) info->dag_valid = -wk;
     }
     return ARSLAM_OK;
   } catch (const arslam::ApiError &e) {

@@ -23,6 +23,8 @@
 // factorization; the backward solve L^T y = z is one launch per tile row.
 #include "lm_internal.h"
 
+#include <algorithm>
+#include <climits>
 #include <cmath>
 
 namespace arslam {
@@ -486,6 +488,395 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent task-graph executor of the same factorization.  Every workgroup
+// loops: draw a ticket (tasks are in a topological order, dag_build), wait
+// (thread 0, bounded spin) for the task's dependency counters, run it, and
+// publish its result (stores drained, agent-scope release, counter update).
+// A waited-on task always holds a smaller ticket, i.e. it was drawn by a
+// running workgroup, so progress is guaranteed for any grid size; every
+// spin is still bounded (kSpinCap) and raises the error flag if exceeded.
+//   POTRF k   : L_kk and L_kk^{-1} into Ld (the column's TRSMs then need
+//               only a GEMM with the inverse)
+//   TRSM i,k  : L_ik = A_ik L_kk^{-T}  (MFMA, in place)
+//   update    : the plan item's sum over its columns k of L_ik L_jk^T; split
+//               items publish partials and the last arriver reduces them in
+//               chunk order; the application to the target waits for the
+//               target's earlier levels, so the summation order is fixed.
+// ---------------------------------------------------------------------------
+constexpr int kLtdSize = 4 * 16 * LI;   // 1152 doubles
+constexpr long kSpinCap = 1L << 16;   // ~0.1 s of polling: far beyond any legitimate wait
+
+// Poll a dependency counter with an atomic read-modify-write (+0): counters
+// are advanced by device-scope atomic adds, and an RMW is performed where
+// those are, so it observes them on every XCD.  (A plain relaxed load was
+// observed to spin forever on a counter another task had already advanced.)
+__device__ __forceinline__ int ld_acquire_relaxed(int *p) {
+  // compare-and-swap that never matches (counters are >= 0): returns the value
+  // without a write, and cannot be folded into a plain load as an RMW of 0 is
+  int v = INT_MIN;
+  __hip_atomic_compare_exchange_strong(p, &v, INT_MIN, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
+// Tile hand-offs between workgroups of the persistent kernel use the
+// write-through form (MI355X_MICROARCH.md, visibility): every published
+// tile is stored sc1 (8-byte agent-scope relaxed atomic stores) and every
+// load of a tile that another workgroup may write in this launch is an sc1
+// load, so no release or acquire fence is needed around the counters.
+__device__ __forceinline__ void st_wt(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double *p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// 16-byte write-through store / sc1 loads (inline asm: hipcc has no 16-byte
+// atomic form).  Loads are issued in groups inside ONE asm statement that
+// also waits for them (vmcnt(0)), so the compiler never sees an asm output
+// before its data has arrived.
+__device__ __forceinline__ void st_wt16(double *p, dbl2 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+// eight 16-byte sc1 loads p[k] -> v[k], waited
+__device__ __forceinline__ void ld_wt16x8(const double *const p[8], dbl2 v[8]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %8, off sc1\n\t"
+      "global_load_dwordx4 %1, %9, off sc1\n\t"
+      "global_load_dwordx4 %2, %10, off sc1\n\t"
+      "global_load_dwordx4 %3, %11, off sc1\n\t"
+      "global_load_dwordx4 %4, %12, off sc1\n\t"
+      "global_load_dwordx4 %5, %13, off sc1\n\t"
+      "global_load_dwordx4 %6, %14, off sc1\n\t"
+      "global_load_dwordx4 %7, %15, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+// eight 8-byte sc1 loads, waited
+__device__ __forceinline__ void ld_wt8x8(const double *const p[8], double v[8]) {
+  asm volatile(
+      "global_load_dwordx2 %0, %8, off sc1\n\t"
+      "global_load_dwordx2 %1, %9, off sc1\n\t"
+      "global_load_dwordx2 %2, %10, off sc1\n\t"
+      "global_load_dwordx2 %3, %11, off sc1\n\t"
+      "global_load_dwordx2 %4, %12, off sc1\n\t"
+      "global_load_dwordx2 %5, %13, off sc1\n\t"
+      "global_load_dwordx2 %6, %14, off sc1\n\t"
+      "global_load_dwordx2 %7, %15, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+
+// 256-thread sc1 load of a 64x64 row-major tile into LDS (pitch LQ)
+__device__ __forceinline__ void load_tile_wt(const double *__restrict__ g, double *lds, int tid) {
+  const double *p[8];
+  dbl2 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) p[q] = g + 2 * (q * 256 + tid);
+  ld_wt16x8(p, v);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
+    *reinterpret_cast<dbl2 *>(lds + r * LQ + c2) = v[q];
+  }
+}
+
+// 256-thread write-through store of a 64x64 LDS tile (pitch LQ), optionally
+// lower triangle only
+__device__ __forceinline__ void store_tile_wt(double *__restrict__ g, const double *lds, int tid, bool lower) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
+    dbl2 v = *reinterpret_cast<const dbl2 *>(lds + r * LQ + c2);
+    if (lower) {
+      if (c2 > r) v.x = 0.0;
+      if (c2 + 1 > r) v.y = 0.0;
+    }
+    st_wt16(g + 2 * e, v);
+  }
+}
+
+// thread 0: spin until counter[idx] >= val for every wait; false on timeout,
+// or at once when another workgroup already timed out (flag < 0), so a
+// broken graph drains in one spin cap instead of one per task
+__device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag) {
+  for (int w = w0; w < w1; ++w) {
+    const int2 cv = waits[w];
+    long spins = 0;
+    while (ld_acquire_relaxed(counters + cv.x) < cv.y) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(flag) < 0)) return false;
+    }
+  }
+  return true;
+}
+
+// all threads: drain this workgroup's write-through stores before thread 0
+// bumps a counter
+__device__ __forceinline__ void dag_release(int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// C = A B^T for two 64x64 LDS tiles (pitch LQ), 4 waves x 32x32; acc layout
+// of the f64 MFMA (col = lane & 15, row = (lane >> 4) + 4 reg)
+__device__ __forceinline__ void gemm64_nt(const double *sA, const double *sB, int tid, dbl4 acc[4]) {
+  const int w = tid >> 6, lane = tid & 63;
+  const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll 4
+  for (int kk = 0; kk < T64 / 4; ++kk) {
+    const int kc = kk * 4 + lk;
+    const double a0 = sA[(r0 + li) * LQ + kc];
+    const double a1 = sA[(r0 + 16 + li) * LQ + kc];
+    const double b0 = sB[(c0 + li) * LQ + kc];
+    const double b1 = sB[(c0 + 16 + li) * LQ + kc];
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+  }
+}
+
+struct DagArgs {
+  double *S;
+  const int *tid_map;
+  int T;
+  double *Ld;                 // [2T][4096]: L_kk then L_kk^{-1}
+  double *ltd;                // [T][kLtdSize]: the 16x16 diagonal-block inverses of each L_kk
+  const int4 *tasks;
+  const int *wait_off;
+  const int2 *waits;
+  int *counters;              // ready[n_tiles] | applied[n_tiles] | ticket
+  int n_tiles;
+  int n_tasks;
+  const int2 *targets;
+  const int4 *items;
+  const int *ks;
+  const int2 *split;
+  double *part;
+  int *split_cnt;
+  int *flag;
+  int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
+  unsigned long long *trace;  // debug: [n_tasks][4] s_memrealtime at draw / waits met / end, workgroup
+};
+
+__device__ __forceinline__ unsigned long long realtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+#define DAG_PROGRESS(slot, v)                                                                  \
+  do {                                                                                         \
+    if (a.progress && tid == 0)                                                                \
+      __hip_atomic_store(a.progress + 4 * blockIdx.x + (slot), (v), __ATOMIC_RELAXED,          \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                            \
+  } while (0)
+
+__global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
+  // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
+  __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 4];
+  double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
+  int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);   // [0] ticket, [1] bad, [2] ok, [3] last
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63;
+  const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+  int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.counters + 2 * a.n_tiles;
+  for (;;) {
+    if (tid == 0) sh[0] = atomicAdd(ticket, 1);
+    __syncthreads();
+    const int t = sh[0];
+    __syncthreads();
+    DAG_PROGRESS(0, t);
+    DAG_PROGRESS(1, 1);
+    if (t >= a.n_tasks) break;
+    const int4 task = a.tasks[t];
+    DAG_PROGRESS(2, task.x);
+    if (a.trace && tid == 0) { a.trace[4L * t] = realtime(); a.trace[4L * t + 3] = blockIdx.x; }
+    if (tid == 0) {
+      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], a.wait_off[t + 1], a.flag);
+      if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
+      sh[2] = ok;
+    }
+    __syncthreads();
+    DAG_PROGRESS(1, 2);
+    if (a.trace && tid == 0) a.trace[4L * t + 1] = realtime();
+    if (task.x == 0) {
+      // ---- POTRF k: publish L_kk and its 16x16 block inverses, then (off the
+      // critical path) the full inverse for the backward solve ----
+      const int k = task.y;
+      if (task.z >= 0) {
+        // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
+        const int4 it = a.items[task.z];
+        dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        for (int q = it.y; q < it.z; ++q) {
+          if (q > it.y) __syncthreads();
+          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, a.ks[q]), D, tid);
+          __syncthreads();
+          gemm64_nt(D, D, tid, acc);
+        }
+        __syncthreads();
+        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), D, tid);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) D[(rb + lk + 4 * reg) * LQ + cb + li] -= acc[q][reg];
+        }
+      } else {
+        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), D, tid);
+      }
+      __syncthreads();
+      const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid);
+      if (!ok && tid == 0) {
+        int first = 0;
+        while (first < T64 && D[first * LQ + first] > 0.0) ++first;
+        atomicCAS(a.flag, 0, 1 + k * T64 + first);
+      }
+      store_tile_wt(a.Ld + (long)k * T64 * T64, D, tid, true);
+      double *ltd_g = a.ltd + (long)k * kLtdSize;
+      for (int e = tid; e < kLtdSize / 2; e += 256)
+        st_wt16(ltd_g + 2 * e, *reinterpret_cast<const dbl2 *>(LTd + 2 * e));
+      dag_release(tid);
+      if (tid == 0) __hip_atomic_fetch_add(ready + task.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      blocked_trinv64(D, LTd, X, tid);
+      __syncthreads();
+      double *Xg = a.Ld + ((long)a.T + k) * T64 * T64;
+#pragma unroll 4
+      for (int m = 0; m < 16; ++m) {
+        const int e = m * 256 + tid, r = e >> 6, c = e & 63;
+        Xg[e] = (r >= c) ? X[c * LQ + r] : 0.0;   // read by the next kernel only
+      }
+    } else if (task.x == 1) {
+      // ---- TRSM i,k: L_ik L_kk^T = A_ik, blocked with the 16x16 inverses ----
+      const int i = task.y, k = task.z;
+      double *Ct = tile_ptr(a.S, a.tid_map, a.T, i, k);
+      load_tile_wt(Ct, X, tid);
+      load_tile_wt(a.Ld + (long)k * T64 * T64, D, tid);
+      {
+        const double *ltd_g = a.ltd + (long)k * kLtdSize;
+        const double *p8[8];
+        dbl2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = tid + 256 * u;
+          p8[u] = ltd_g + 2 * (e < kLtdSize / 2 ? e : 0);
+        }
+        ld_wt16x8(p8, v);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int e = tid + 256 * u;
+          if (e < kLtdSize / 2) *reinterpret_cast<dbl2 *>(LTd + 2 * e) = v[u];
+        }
+      }
+      __syncthreads();
+      blocked_trsm64(X, D, inv, LTd, tid);
+      store_tile_wt(Ct, X, tid, false);
+      dag_release(tid);
+      if (tid == 0) __hip_atomic_fetch_add(ready + task.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      // ---- update item ----
+      const int4 it = a.items[task.y];
+      const int2 pr = a.targets[it.x];
+      const int ti = pr.x, tj = pr.y, sid = it.w;
+      dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+      for (int q = it.y; q < it.z; ++q) {
+        const int k = a.ks[q];
+        if (q > it.y) __syncthreads();
+        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tid);
+        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, tj, k), X, tid);
+        __syncthreads();
+        gemm64_nt(D, X, tid, acc);
+      }
+      bool apply = true;
+      if (sid >= 0) {
+        const int2 sp = a.split[sid >> 8];
+        double *mine = a.part + (long)(sp.y + (sid & 255)) * 4096;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) st_wt(mine + (4 * q + reg) * 256 + tid, acc[q][reg]);
+        dag_release(tid);
+        if (tid == 0) {
+          const int old = __hip_atomic_fetch_add(a.split_cnt + (sid >> 8), 1, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+          sh[3] = old == sp.x - 1;
+        }
+        __syncthreads();
+        apply = sh[3] != 0;
+        if (apply) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = dbl4{0, 0, 0, 0};
+          for (int c = 0; c < sp.x; ++c) {
+            const double *pc = a.part + (long)(sp.y + c) * 4096;
+            double v[16];
+            const double *p8[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) p8[u] = pc + u * 256 + tid;
+            ld_wt8x8(p8, v);
+            ld_wt8x8(p8 + 8, v + 8);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+              for (int reg = 0; reg < 4; ++reg) acc[q][reg] += v[4 * q + reg];
+          }
+        }
+      }
+      DAG_PROGRESS(1, 3);
+      if (apply) {
+        // in level order: wait until the target's earlier levels were applied
+        if (tid == 0) {
+          long spins = 0;
+          bool ok = true;
+          while (ld_acquire_relaxed(applied + task.w) < task.z) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(a.flag) < 0)) {
+              ok = false;
+              break;
+            }
+          }
+          if (!ok) atomicCAS(a.flag, 0, -(2000000 + t));
+        }
+        __syncthreads();
+        double *C = tile_ptr(a.S, a.tid_map, a.T, ti, tj);
+        double cv[16];   // two groups of eight loads in flight
+        {
+          const double *p8[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) p8[4 * q + reg] = C + (rb + lk + 4 * reg) * T64 + cb + li;
+          }
+          ld_wt8x8(p8, cv);
+          ld_wt8x8(p8 + 8, cv + 8);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            st_wt(C + (rb + lk + 4 * reg) * T64 + cb + li, cv[4 * q + reg] - acc[q][reg]);
+        }
+        dag_release(tid);
+        if (tid == 0) __hip_atomic_fetch_add(applied + task.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    DAG_PROGRESS(1, 4);
+    if (a.trace && tid == 0) a.trace[4L * t + 2] = realtime();
+  }
+  DAG_PROGRESS(1, 9);
+}
+
 // z[j] = L[nR][j], the forward-substituted right-hand side: from S for the
 // tiles left of the rhs row's own tile, from that tile's diagonal factor in Ld.
 __global__ void k_init_z(const double *__restrict__ S, const int *__restrict__ tid_map, int T,
@@ -611,6 +1002,18 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
       }
     }
   }
+}
+
+void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
+                          unsigned long long *trace) {
+  if (P.n_dag_tasks == 0) return;
+  (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2) * sizeof(int), s);
+  if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
+  DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_wait_off, P.dag_waits, P.dag_counters,
+            (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
+            P.upd_part, P.upd_cnt, flag, progress, trace};
+  const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);
+  hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
 
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,

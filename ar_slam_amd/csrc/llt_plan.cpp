@@ -40,6 +40,156 @@ T *upload(const std::vector<T> &h, hipStream_t s) {
 
 constexpr int kSplitMin = 6;   // k-lists longer than this are split
 
+// Task graph of the tile factorization for the persistent executor.  Tasks:
+// POTRF(k) (also forms L_kk^{-1}), TRSM(i,k) (L_ik = A_ik L_kk^{-T}) and the
+// plan's update items.  An item's product waits for the TRSMs of its
+// columns; its application to the target waits until the target's earlier
+// levels were applied (so every tile sums its updates in level order, as the
+// level-synchronous path does).  Tickets follow an as-soon-as-possible time
+// estimate, a topological order in which every awaited task -- including any
+// chunk of an earlier level of the same target, which may be the one that
+// applies it -- has a smaller ticket; so the ticketed persistent kernel
+// cannot deadlock.
+void dag_build(LltPlan &plan) {
+  const int T = plan.T;
+  const long nt = plan.n_tiles;
+  auto tid = [&](int i, int j) { return plan.h_tile_id[(long)i * T + j]; };
+  const int nlev = plan.nlev;
+  // applications per target tile and per-(target, level) sequence number
+  std::vector<int> n_apply(nt, 0);
+  std::vector<int> item_seq(plan.h_items.size(), 0);
+  for (int l = 0; l < nlev; ++l) {
+    const int t0 = plan.h_upd_off[l], t1 = plan.h_upd_off[l + 1];
+    std::vector<int> seq_of_target(t1 - t0, 0);
+    for (int t = t0; t < t1; ++t) {
+      const int2 tg = plan.h_targets[t];
+      seq_of_target[t - t0] = n_apply[tid(tg.x, tg.y)]++;
+    }
+    for (int it = plan.h_item_off[l]; it < plan.h_item_off[l + 1]; ++it)
+      item_seq[it] = seq_of_target[plan.h_items[it].x - t0];
+  }
+  struct Node { double est; int type; int idx; int4 task; std::vector<int2> waits; };
+  std::vector<Node> nodes;
+  const double c_potrf = 12.0, c_trsm = 3.0, eps = 1e-3;
+  std::vector<double> potrf_done(T, 0.0), trsm_done(nt, 0.0), last_apply(nt, 0.0), last_chunk_start(nt, -1.0);
+  std::vector<double> level_apply(nt, 0.0);
+  for (int l = 0; l < nlev; ++l) {
+    // factor tasks of the level's columns
+    for (int p = plan.h_panel_off[l]; p < plan.h_panel_off[l + 1]; ++p) {
+      const int2 pk = plan.h_panel[p];
+      const int i = pk.x, k = pk.y;
+      Node n;
+      if (i == k) {
+        n.type = 0;
+        n.task = make_int4(0, k, -1, tid(k, k));
+        n.est = last_apply[tid(k, k)];
+        if (n_apply[tid(k, k)]) n.waits.push_back(make_int2((int)nt + tid(k, k), n_apply[tid(k, k)]));
+        potrf_done[k] = n.est + c_potrf;
+      } else {
+        n.type = 1;
+        n.task = make_int4(1, i, k, tid(i, k));
+        n.waits.push_back(make_int2(tid(k, k), 1));
+        if (n_apply[tid(i, k)]) n.waits.push_back(make_int2((int)nt + tid(i, k), n_apply[tid(i, k)]));
+        n.est = 0.0;   // fixed below once the column's POTRF time is known
+      }
+      n.idx = p;
+      nodes.push_back(std::move(n));
+    }
+    for (size_t m = nodes.size() - (plan.h_panel_off[l + 1] - plan.h_panel_off[l]); m < nodes.size(); ++m)
+      if (nodes[m].type == 1) {
+        const int i = nodes[m].task.y, k = nodes[m].task.z;
+        nodes[m].est = std::max(potrf_done[k], last_apply[tid(i, k)]);
+        trsm_done[tid(i, k)] = nodes[m].est + c_trsm;
+      }
+    // update items of the level
+    std::vector<double> apply_ready(nt, 0.0);
+    std::vector<int> touched;
+    for (int it = plan.h_item_off[l]; it < plan.h_item_off[l + 1]; ++it) {
+      const int4 item = plan.h_items[it];
+      const int2 tg = plan.h_targets[item.x];
+      const int tt = tid(tg.x, tg.y);
+      Node n;
+      n.type = 2;
+      n.idx = it;
+      n.task = make_int4(2, it, item_seq[it], tt);
+      double e = last_chunk_start[tt] + eps;   // after every chunk of the target's earlier levels
+      for (int q = item.y; q < item.z; ++q) {
+        const int k = plan.h_ks[q];
+        n.waits.push_back(make_int2(tid(tg.x, k), 1));
+        e = std::max(e, trsm_done[tid(tg.x, k)]);
+        if (tg.y != tg.x) {
+          n.waits.push_back(make_int2(tid(tg.y, k), 1));
+          e = std::max(e, trsm_done[tid(tg.y, k)]);
+        }
+      }
+      n.est = e;
+      const double fin = e + 2.0 * (item.z - item.y);
+      if (apply_ready[tt] == 0.0) touched.push_back(tt);
+      apply_ready[tt] = std::max(apply_ready[tt], fin);
+      level_apply[tt] = std::max(level_apply[tt], e);
+      nodes.push_back(std::move(n));
+    }
+    for (int tt : touched) {
+      last_apply[tt] = std::max(apply_ready[tt], last_apply[tt]) + 2.0;
+      last_chunk_start[tt] = level_apply[tt];
+    }
+  }
+  // Fold the last update of each diagonal tile into its POTRF task when that
+  // update is one unsplit item: the POTRF then computes A_kk - sum L_kj L_kj^T
+  // itself, taking a task and a hand-off off the critical chain.
+  {
+    std::vector<int> last_item(nt, -1), last_count(nt, 0);
+    for (size_t m = 0; m < nodes.size(); ++m) {
+      if (nodes[m].type != 2) continue;
+      const int tt = nodes[m].task.w, seq = nodes[m].task.z;
+      if (seq + 1 != n_apply[tt]) continue;   // not the final level of this tile
+      last_item[tt] = (int)m;
+      last_count[tt]++;
+    }
+    std::vector<char> drop(nodes.size(), 0);
+    for (auto &n : nodes) {
+      if (n.type != 0) continue;
+      const int tt = n.task.w;
+      const int m = last_item[tt];
+      if (m < 0 || last_count[tt] != 1 || plan.h_items[nodes[m].task.y].w >= 0) continue;
+      n.task.z = nodes[m].task.y;   // item folded into the POTRF
+      std::vector<int2> w;
+      for (const int2 &x : n.waits)
+        if (x.x != (int)nt + tt) w.push_back(x);
+      if (n_apply[tt] > 1) w.push_back(make_int2((int)nt + tt, n_apply[tt] - 1));
+      w.insert(w.end(), nodes[m].waits.begin(), nodes[m].waits.end());
+      n.waits = std::move(w);
+      drop[m] = 1;
+    }
+    std::vector<Node> kept;
+    for (size_t m = 0; m < nodes.size(); ++m)
+      if (!drop[m]) kept.push_back(std::move(nodes[m]));
+    nodes.swap(kept);
+  }
+  std::vector<int> order(nodes.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    if (nodes[a].est != nodes[b].est) return nodes[a].est < nodes[b].est;
+    return nodes[a].type < nodes[b].type;
+  });
+  plan.h_dag_tasks.clear();
+  plan.h_dag_waits.clear();
+  plan.h_dag_wait_off.assign(1, 0);
+  for (int o : order) {
+    plan.h_dag_tasks.push_back(nodes[o].task);
+    plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].waits.begin(), nodes[o].waits.end());
+    plan.h_dag_wait_off.push_back((int)plan.h_dag_waits.size());
+  }
+  plan.n_dag_tasks = (long)plan.h_dag_tasks.size();
+  long n_potrf = 0, n_trsm = 0;
+  for (const int4 &t : plan.h_dag_tasks) {
+    n_potrf += t.x == 0;
+    n_trsm += t.x == 1;
+  }
+  const double t3 = 64.0 * 64.0 * 64.0;
+  plan.total_factor_flops = plan.total_upd_flops + n_potrf * (t3 / 3.0 + t3 / 3.0) + n_trsm * 2.0 * t3;
+}
+
 void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) {
   llt_plan_free(plan);
   plan.T = T;
@@ -175,6 +325,81 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
     for (int j = 0; j <= i; ++j)
       if (P[(long)i * T + j] && plan.h_tile_id[(long)i * T + j] < 0) plan.h_tile_id[(long)i * T + j] = (int)nid++;
   plan.n_tiles = nid;
+  dag_build(plan);
+}
+
+bool dag_check(const LltPlan &plan) {
+  const long nt = plan.n_tiles;
+  std::vector<int> cnt(2 * nt + 1, 0), arrived(plan.h_split.size(), 0);
+  for (long t = 0; t < plan.n_dag_tasks; ++t) {
+    for (int w = plan.h_dag_wait_off[t]; w < plan.h_dag_wait_off[t + 1]; ++w)
+      if (cnt[plan.h_dag_waits[w].x] < plan.h_dag_waits[w].y) return false;
+    const int4 task = plan.h_dag_tasks[t];
+    if (task.x == 0 || task.x == 1) {
+      cnt[task.w] = 1;
+      continue;
+    }
+    const int sid = plan.h_items[task.y].w;
+    if (sid >= 0 && ++arrived[sid >> 8] < plan.h_split[sid >> 8].x) continue;   // not the last chunk
+    if (cnt[nt + task.w] != task.z) return false;   // level order of the applications
+    cnt[nt + task.w]++;
+  }
+  return true;
+}
+
+// Randomised interleaving of n_workers concurrent workers running the
+// persistent executor's protocol (draw ticket, static waits, run, split
+// arrival, level-ordered application).  Returns false on a deadlock.
+bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
+  const long nt = plan.n_tiles;
+  std::vector<int> cnt(2 * nt + 1, 0), arrived(plan.h_split.size(), 0);
+  struct W { long t = -1; int phase = 0; };   // 0 draw, 1 wait, 2 apply-wait
+  std::vector<W> ws(n_workers);
+  long next = 0, finished = 0;
+  unsigned rng = seed ? seed : 1u;
+  auto rnd = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
+  while (finished < plan.n_dag_tasks) {
+    bool progressed = false;
+    const int start = (int)(rnd() % (unsigned)n_workers);
+    for (int m = 0; m < n_workers && !progressed; ++m) {
+      W &w = ws[(start + m) % n_workers];
+      if (w.phase == 0) {
+        if (next >= plan.n_dag_tasks) continue;
+        w.t = next++;
+        w.phase = 1;
+        progressed = true;
+      } else if (w.phase == 1) {
+        bool ok = true;
+        for (int q = plan.h_dag_wait_off[w.t]; q < plan.h_dag_wait_off[w.t + 1] && ok; ++q)
+          ok = cnt[plan.h_dag_waits[q].x] >= plan.h_dag_waits[q].y;
+        if (!ok) continue;
+        progressed = true;
+        const int4 task = plan.h_dag_tasks[w.t];
+        if (task.x != 2) {
+          cnt[task.w] = 1;
+          w.phase = 0;
+          ++finished;
+          continue;
+        }
+        const int sid = plan.h_items[task.y].w;
+        if (sid >= 0 && ++arrived[sid >> 8] < plan.h_split[sid >> 8].x) {
+          w.phase = 0;
+          ++finished;
+          continue;
+        }
+        w.phase = 2;
+      } else {
+        const int4 task = plan.h_dag_tasks[w.t];
+        if (cnt[nt + task.w] < task.z) continue;
+        cnt[nt + task.w]++;
+        progressed = true;
+        w.phase = 0;
+        ++finished;
+      }
+    }
+    if (!progressed) return false;
+  }
+  return true;
 }
 
 void llt_plan_upload(LltPlan &plan, hipStream_t s) {
@@ -193,7 +418,12 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   plan.bs_gbeg = upload(plan.h_gbeg, s);
   check(hipMalloc(&plan.bs_part, std::max<size_t>(plan.h_gather.size(), 1) * 64 * sizeof(double)), "hipMalloc(bs_part)");
   plan.tile_id = upload(plan.h_tile_id, s);
-  check(hipMalloc(&plan.ldiag, 2 * (size_t)T * 64 * 64 * sizeof(double)), "hipMalloc(ldiag)");
+  // L_kk, L_kk^{-1}, and the 16x16 block inverses (4 x 16 x 18) of each column
+  check(hipMalloc(&plan.ldiag, ((size_t)2 * T * 64 * 64 + (size_t)T * 1152) * sizeof(double)), "hipMalloc(ldiag)");
+  plan.dag_tasks = upload(plan.h_dag_tasks, s);
+  plan.dag_wait_off = upload(plan.h_dag_wait_off, s);
+  plan.dag_waits = upload(plan.h_dag_waits, s);
+  check(hipMalloc(&plan.dag_counters, (2 * (size_t)plan.n_tiles + 2) * sizeof(int)), "hipMalloc(dag_counters)");
   check(hipStreamSynchronize(s), "plan sync");
 }
 
@@ -206,7 +436,9 @@ void llt_plan_free(LltPlan &plan) {
   for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
                   (void *)plan.upd_ks, (void *)plan.upd_items, (void *)plan.upd_split,
                   (void *)plan.upd_cnt, (void *)plan.upd_part, (void *)plan.bs_cols, (void *)plan.bs_gather,
-                  (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.tile_id, (void *)plan.ldiag})
+                  (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.tile_id, (void *)plan.ldiag,
+                  (void *)plan.dag_tasks, (void *)plan.dag_wait_off, (void *)plan.dag_waits,
+                  (void *)plan.dag_counters})
     if (p) (void)hipFree(p);
   plan = LltPlan{};
 }

@@ -98,17 +98,34 @@ struct LltPlan {
   std::vector<int> h_bs_off;        // [nlev+1], in backward (root-first) order
   std::vector<int> h_bsg_off;       // [nlev+1], gather tasks per backward level
   std::vector<double> h_upd_flops;  // useful flops of each level's update
+  // persistent task-graph executor (launch_dense_llt_dag): tasks in ticket
+  // order {type, a, b, c} (0 POTRF k; 1 TRSM i,k; 2 update item a, level
+  // sequence b, target tile c), each with a list of {counter, value} waits;
+  // counters = [ready(n_tiles) | applied(n_tiles) | ticket]
+  int4 *dag_tasks = nullptr;
+  int *dag_wait_off = nullptr;
+  int2 *dag_waits = nullptr;
+  int *dag_counters = nullptr;
+  long n_dag_tasks = 0;
+  std::vector<int4> h_dag_tasks;
+  std::vector<int> h_dag_wait_off;
+  std::vector<int2> h_dag_waits;
   // host copies of the device lists (llt_plan_symbolic)
   std::vector<int2> h_panel, h_targets, h_gather, h_split;
   std::vector<int> h_kstart, h_ks, h_bcols, h_gbeg;
   std::vector<int4> h_items;
   double total_upd_flops = 0.0;
+  double total_factor_flops = 0.0;   // updates + POTRF (+ inverse) + TRSM of the task graph
   long total_upd_tiles = 0;
 };
 
 // Symbolic tile fill of the lower pattern (T*T bytes, in/out) and the host
 // task lists (no HIP calls: usable without a device).
 void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern);
+// Ticket-order check of the task graph: executing the tasks one at a time in
+// ticket order, is every wait already satisfied when its task runs?
+bool dag_check(const LltPlan &plan);
+bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed);
 // Upload the host lists and allocate the plan's device buffers.
 void llt_plan_upload(LltPlan &plan, hipStream_t s);
 // llt_plan_symbolic + llt_plan_upload
@@ -159,6 +176,10 @@ struct LaunchTiming {
 // y = L^{-T} z into yF[0..nR).
 void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
                       LaunchTiming *timing = nullptr);
+// The same factorization as one persistent launch over the plan's task graph
+// (tickets in a topological order, dependency counters in global memory).
+void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups,
+                          int *progress = nullptr, unsigned long long *trace = nullptr);
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s);
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s);

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -208,9 +209,15 @@ struct arslam_lm {
   }
   void allreduce(double *buf, size_t count, int op) { allreduce_any(buf, count, ARSLAM_DT_F64, op); }
 
+  int dag_workgroups = 512;
+  bool dag_traced = false;
+
   void ensure_stream() {
     if (opt.device >= 0) HIP_CHECK(hipSetDevice(opt.device));
     HIP_CHECK(hipGetDevice(&device));
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+      dag_workgroups = 2 * cus;   // two 73 KB-LDS workgroups per CU
     if (!stream) HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &t : timers) t.init();
   }
@@ -488,7 +495,36 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
       timing_begin();
-      arslam::launch_dense_llt(plan, d_S.p, d_flag.p, stream, opt.kernel_timing ? &upd_timing : nullptr);
+      if (opt.factor_executor == 1) {
+        const bool rec = opt.kernel_timing && upd_timing.used < upd_timing.cap;
+        if (rec) HIP_CHECK(hipEventRecord(upd_timing.ev[2 * upd_timing.used], stream));
+        static const char *trace_path = std::getenv("ARSLAM_DAG_TRACE");   // debug: dump one task timeline
+        if (trace_path && !dag_traced) {
+          DevBuf<unsigned long long> tr;
+          tr.alloc(4 * plan.n_dag_tasks);
+          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, tr.p);
+          std::vector<unsigned long long> h(4 * plan.n_dag_tasks);
+          HIP_CHECK(hipMemcpyAsync(h.data(), tr.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
+          HIP_CHECK(hipStreamSynchronize(stream));
+          if (FILE *f = std::fopen(trace_path, "wb")) {
+            const long n = plan.n_dag_tasks;
+            std::fwrite(&n, 8, 1, f);
+            std::fwrite(plan.h_dag_tasks.data(), sizeof(int4), n, f);
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+          }
+          dag_traced = true;
+        } else {
+          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups);
+        }
+        if (rec) {
+          HIP_CHECK(hipEventRecord(upd_timing.ev[2 * upd_timing.used + 1], stream));
+          upd_timing.used++;
+          upd_timing.flops += plan.total_factor_flops;
+        }
+      } else {
+        arslam::launch_dense_llt(plan, d_S.p, d_flag.p, stream, opt.kernel_timing ? &upd_timing : nullptr);
+      }
       timers[PH_CHOL].stop(stream);
       timers[PH_SOLVE].start(stream);
       arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
@@ -657,6 +693,7 @@ int arslam_lm_options_init(arslam_lm_options *o) {
   o->cholesky_skip_zero_tiles = 1;
   o->reduced_ordering = 2;
   o->kernel_timing = 0;
+  o->factor_executor = 1;
   return ARSLAM_OK;
 }
 
@@ -681,6 +718,8 @@ int arslam_lm_set_options(arslam_lm *h, const arslam_lm_options *opt) {
   return guarded([&] {
     fail_if(opt->elimination != ARSLAM_ELIM_AUTO && opt->elimination != ARSLAM_ELIM_CAPTURES,
             ARSLAM_E_UNSUPPORTED, "only capture elimination is implemented");
+    fail_if(opt->factor_executor != 0 && opt->factor_executor != 1, ARSLAM_E_INVALID_ARG,
+            "factor_executor must be 0 or 1");
     fail_if(opt->max_num_iterations < 0 || opt->max_num_iterations > ARSLAM_LM_MAX_ITERS,
             ARSLAM_E_INVALID_ARG, "max_num_iterations out of range");
     if (opt->device != h->opt.device || opt->reduced_ordering != h->opt.reduced_ordering ||

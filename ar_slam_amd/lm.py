@@ -43,7 +43,8 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
            "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm", "arslam_lm_set_comm_callback",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
-           "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_reduced_plan",
+           "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
+           "arslam_debug_reduced_plan",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
            "arslam_slam_create", "arslam_slam_destroy", "arslam_slam_set_verbose", "arslam_slam_load_yaml",
@@ -81,7 +82,7 @@ class Options(C.Structure):
                 ("minimizer_progress_to_stdout", C.c_int),
                 ("update_state_every_iteration", C.c_int),
                 ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int),
-                ("reduced_ordering", C.c_int), ("kernel_timing", C.c_int)]
+                ("reduced_ordering", C.c_int), ("kernel_timing", C.c_int), ("factor_executor", C.c_int)]
 
 
 class Iteration(C.Structure):
@@ -383,15 +384,15 @@ def debug_residual_jacobian(cam, cap, tag, corners):
     return r, J
 
 
-def debug_dense_llt(A, b):
+def debug_dense_llt(A, b, executor=0):
     """Device Cholesky + solve of the SPD matrix A (lower triangle used). Returns (L, y, info)."""
     A = _f64(A).copy()
     n = A.shape[0]
     b = _f64(b).reshape(n)
     y = np.zeros(n)
     info = C.c_int(0)
-    _check(lib().arslam_debug_dense_llt(n, A.ctypes.data_as(_dp), b.ctypes.data_as(_dp),
-                                        y.ctypes.data_as(_dp), C.byref(info)))
+    _check(lib().arslam_debug_dense_llt_ex(C.c_long(n), A.ctypes.data_as(_dp), b.ctypes.data_as(_dp),
+                                           y.ctypes.data_as(_dp), C.byref(info), C.c_int(executor)))
     return A, y, info.value
 
 
@@ -400,7 +401,7 @@ class PlanInfo(C.Structure):
                 ("tiles_per_side", C.c_int), ("n_parts", C.c_int), ("camera_row", C.c_int),
                 ("n_levels", C.c_int), ("n_assembled_tiles", C.c_long), ("n_factor_tiles", C.c_long),
                 ("n_update_tiles", C.c_long), ("n_update_items", C.c_long), ("n_split_targets", C.c_long),
-                ("update_flops", C.c_double)]
+                ("update_flops", C.c_double), ("n_dag_tasks", C.c_long), ("dag_valid", C.c_int)]
 
 
 def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, cap_const=None,

@@ -154,6 +154,7 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--skip-zero-tiles", type=int, default=1)
     ap.add_argument("--ordering", type=int, default=2, help="0 natural, 1 RCM, 2 nested dissection")
+    ap.add_argument("--executor", type=int, default=1, help="0 level launches, 1 persistent task graph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,7 +184,7 @@ def main():
     rp = lm.ResidentProblem(**part, comm=comm, device=local_rank,
                             kernel_timing=0 if args.no_kernel_timing else 1,
                             cholesky_skip_zero_tiles=args.skip_zero_tiles,
-                            reduced_ordering=args.ordering)
+                            reduced_ordering=args.ordering, factor_executor=args.executor)
 
     def barrier():
         if world > 1:
@@ -215,8 +216,10 @@ def main():
         avg_ms = dom_ms / dom_launches
         flops_per_launch = dom_flops / dom_launches
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "k_update (reduced-system Cholesky trailing update, "
-                                               "v_mfma_f64_16x16x4_f64)",
+        kname = ("k_factor_dag (reduced-system Cholesky, persistent task graph: POTRF + TRSM + "
+                 "trailing updates on v_mfma_f64_16x16x4_f64)") if args.executor == 1 else \
+            "k_update (reduced-system Cholesky trailing update, v_mfma_f64_16x16x4_f64)"
+        roofline = {"bound": "mfma", "kernel": kname,
                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_pmc_traffic(),
                     "avg_launch_us": avg_ms * 1e3, "flops_per_launch": flops_per_launch,
@@ -247,6 +250,7 @@ def main():
             "reduced_system": {"rows": int(last["n_reduced"]), "factor_tiles": int(last["n_factor_tiles"]),
                                "etree_levels": int(last["n_levels"]),
                                "ordering": ["natural", "RCM", "nested dissection"][args.ordering],
+                               "executor": ["level launches", "persistent task graph"][args.executor],
                                "skip_zero_tiles": bool(args.skip_zero_tiles)},
             "phase_ms_per_solve": {k: last[f"t_{k}_ms"] for k in
                                    ("linearize", "schur", "cholesky", "solve", "backsub", "cost")},

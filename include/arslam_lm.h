@@ -86,6 +86,8 @@ typedef struct {
   int reduced_ordering;              /* tags in the reduced system: 0 natural, 1 reverse
                                         Cuthill-McKee, 2 nested dissection (default) */
   int kernel_timing;                 /* 1: HIP events around every launch of the dominant kernel */
+  int factor_executor;               /* reduced-system Cholesky: 0 two launches per elimination-tree
+                                        level, 1 one persistent task-graph launch (default) */
 } arslam_lm_options;
 
 /* ceres::IterationSummary subset */

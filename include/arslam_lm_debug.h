@@ -23,6 +23,9 @@ int arslam_debug_residual_jacobian(int n, const double *cam, const double *cap, 
  * n x n row-major SPD matrix A (in place: on return A holds L) and solve
  * A y = b.  *info = 0 on success, k+1 if pivot k was not positive. */
 int arslam_debug_dense_llt(long n, double *A, const double *b, double *y, int *info);
+/* the same with the factorization executor chosen (0 level launches, 1 persistent task graph);
+ * info < 0 reports a task-graph wait that timed out */
+int arslam_debug_dense_llt_ex(long n, double *A, const double *b, double *y, int *info, int executor);
 
 /* Host-only symbolic analysis of the reduced system (no device needed): the
  * row layout arslam_lm_load_soa would choose for problem p under the given
@@ -43,6 +46,8 @@ typedef struct {
   long n_update_items;     /* update work items (after splitting long k-lists) */
   long n_split_targets;
   double update_flops;     /* algorithmic flops of the trailing updates per factorization */
+  long n_dag_tasks;        /* tasks of the persistent executor's graph */
+  int dag_valid;           /* 1: run one at a time in ticket order, every wait is already met */
 } arslam_plan_info;
 
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,

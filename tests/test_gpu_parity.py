@@ -206,3 +206,20 @@ def test_cfg3_matches_golden_oracle_trace(lm):
     assert abs(s["final_cost"] - gold["final_cost"]) <= 1e-8 * gold["final_cost"]
     assert abs(cam[0] - gold["final_focal"]) <= 1e-8 * gold["final_focal"]
     assert abs(s["final_rms_px"] - gold["final_rms_px"]) <= 1e-8 * gold["final_rms_px"]
+
+
+@pytest.mark.parametrize("name", ["medium", "cfg2"])
+@pytest.mark.parametrize("ordering", [1, 2])
+def test_persistent_executor_matches_level_launches(lm, oracle, name, ordering):
+    """The persistent task-graph factorization (default) and the level-synchronous one give the
+    same LM trace (both against the oracle's tolerances)."""
+    g = synth.config_graph(name)
+    ref = oracle.solve_graph(g)
+    lev = lm.solve_graph(g, factor_executor=0, reduced_ordering=ordering)
+    dag = lm.solve_graph(g, factor_executor=1, reduced_ordering=ordering)
+    _compare_solves(g, lev, ref)
+    _compare_solves(g, dag, ref)
+    cl = [it["cost"] for it in lev[3]["iterations"]]
+    cd = [it["cost"] for it in dag[3]["iterations"]]
+    assert len(cl) == len(cd)
+    np.testing.assert_allclose(cd, cl, rtol=1e-10)
