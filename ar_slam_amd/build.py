@@ -44,7 +44,8 @@ def build(force=False, verbose=False):
     objdir = os.path.join(HERE, "_obj")
     os.makedirs(objdir, exist_ok=True)
     flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
-             "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+             "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC] + \
+        os.environ.get("ARSLAM_EXTRA_FLAGS", "").split()
     objs = []
     procs = []
     for src in SOURCES:

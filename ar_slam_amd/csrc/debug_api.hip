@@ -12,6 +12,7 @@
 #include <vector>
 
 namespace arslam {
+void debug_read_schur_stamps(unsigned long long *out);
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,
                              const double *corners, double *r, double *J, hipStream_t s);
 }
@@ -180,4 +181,11 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
   } catch (...) {
     return ARSLAM_E_INVALID_ARG;
   }
+}
+
+// diagnostic build only (-DARSLAM_SCHUR_STAMPS): accumulated per-phase cycles of k_schur
+extern "C" int arslam_debug_schur_stamps(unsigned long long out[16]) {
+  if (!out) return ARSLAM_E_INVALID_ARG;
+  arslam::debug_read_schur_stamps(out);
+  return ARSLAM_OK;
 }

@@ -478,4 +478,64 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   return L;
 }
 
+SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
+  SchurGather G;
+  G.cap_off.assign(h.nc + 1, 0);
+  struct Item {
+    long key;   // rX << 32 | rY
+    int c;
+    int px, py;
+  };
+  std::vector<Item> items;
+  std::vector<std::pair<int, int>> blk;   // (global first row, local first column) of the capture's blocks
+  for (int c = 0; c < h.nc; ++c) {
+    const int nblk = h.cap_blk_start[c + 1] - h.cap_blk_start[c];
+    const long m = 1 + 6L * nblk;
+    G.cap_off[c + 1] = G.cap_off[c] + (m + 1) * (m + 2) / 2;
+    if (h.cap_start[c + 1] == h.cap_start[c]) continue;   // no residuals: k_schur stores nothing
+    blk.clear();
+    if (L.cam_row >= 0) blk.emplace_back(L.cam_row, 0);
+    for (int u = 0; u < nblk; ++u) {
+      const int tr = L.tag_row[h.blk_tag[h.cap_blk_start[c] + u]];
+      if (tr >= 0) blk.emplace_back(tr, 1 + 6 * u);
+    }
+    if (blk.empty()) continue;
+    blk.emplace_back((int)L.nR, (int)m);   // rhs row
+    for (size_t a = 0; a < blk.size(); ++a)
+      for (size_t b = 0; b < blk.size(); ++b) {
+        const int rx = blk[a].first, ry = blk[b].first;
+        if (rx < ry || ry == L.nR) continue;   // lower blocks; the rhs only as a row
+        items.push_back({((long)rx << 32) | ry, c, blk[a].second, blk[b].second});
+      }
+  }
+  std::stable_sort(items.begin(), items.end(), [](const Item &x, const Item &y) { return x.key < y.key; });
+  G.contrib.reserve(items.size());
+  for (size_t i = 0; i < items.size(); ++i) {
+    if (i == 0 || items[i].key != items[i - 1].key) {
+      if (i) G.max_contrib = std::max(G.max_contrib, (int)(G.contrib.size() - G.dest_start.back()));
+      G.dest_row.push_back((int)(items[i].key >> 32));
+      G.dest_row.push_back((int)(items[i].key & 0xffffffffL));
+      G.dest_start.push_back((int)G.contrib.size());
+    }
+    G.contrib.push_back({G.cap_off[items[i].c], items[i].px, items[i].py});
+  }
+  if (!G.dest_start.empty())
+    G.max_contrib = std::max(G.max_contrib, (int)(G.contrib.size() - G.dest_start.back()));
+  G.dest_start.push_back((int)G.contrib.size());
+  const int nd = (int)G.dest_start.size() - 1;
+  for (int d = 0; d < nd; ++d) {
+    const int k0 = G.dest_start[d], k1 = G.dest_start[d + 1];
+    if (k1 - k0 <= kSchurChunk) {
+      G.items.insert(G.items.end(), {d, k0, k1, -1});
+      continue;
+    }
+    const int pieces = (k1 - k0 + kSchurChunk - 1) / kSchurChunk;
+    G.splits.insert(G.splits.end(), {d, G.n_pslots, pieces, 0});
+    for (int q = 0; q < pieces; ++q)
+      G.items.insert(G.items.end(), {d, k0 + q * kSchurChunk, std::min(k1, k0 + (q + 1) * kSchurChunk), G.n_pslots + q});
+    G.n_pslots += pieces;
+  }
+  return G;
+}
+
 }  // namespace arslam

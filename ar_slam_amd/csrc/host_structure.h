@@ -82,4 +82,30 @@ struct ReducedLayout {
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
                              const ReduceMaxU8 &pattern_max);
 
+// Deterministic Schur assembly.  k_schur stores capture c's local reduced
+// system packed (lower triangle, local order: f, 6 per tag, then the rhs
+// row) at slab + cap_off[c]; k_schur_gather sums, for every destination block
+// of the reduced system (global first rows rX >= rY; 1 row for f and the rhs,
+// 6 for a tag), the contributing captures' blocks in capture order and stores
+// the sum -- plain stores, no atomics, bitwise reproducible.
+struct SchurContrib {
+  long off;     // cap_off of the contributing capture
+  int px, py;   // local first columns of the destination's row and column blocks
+};
+// A destination with more than kSchurChunk contributions is summed in pieces
+// (work items writing partial sums, then one combine per split destination
+// adding the pieces in order), so no wave walks a long list serially.
+constexpr int kSchurChunk = 64;
+struct SchurGather {
+  std::vector<long> cap_off;          // [nc+1]
+  std::vector<int> dest_row;          // [2 nd] rX, rY
+  std::vector<int> dest_start;        // [nd+1] contributions of each destination
+  std::vector<SchurContrib> contrib;
+  std::vector<int> items;             // [4 ni] {destination, first, end contribution, partial slot or -1}
+  std::vector<int> splits;            // [4 ns] {destination, first partial slot, pieces, 0}
+  int n_pslots = 0;
+  int max_contrib = 0;
+};
+SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L);
+
 }  // namespace arslam

@@ -58,6 +58,18 @@ struct DevProblem {
   const int *row_slot;       // [nR]    parameter slot of a reduced row, -1 for padding rows
   const int *tile_id;        // [T*T]   compact tile index of the reduced system (see LltPlan)
   int T;                     // tiles per side
+  // deterministic Schur assembly (SchurGather): packed local systems + gather lists
+  const long *cap_off;       // [nc+1]
+  double *slab;              // [cap_off[nc]]
+  const int2 *dest_row;      // [n_dest] first rows (rX, rY) of each destination block
+  const int *dest_start;     // [n_dest+1]
+  const SchurContrib *contrib;
+  int n_dest;
+  const int4 *gather_items;  // [n_items] {destination, first, end contribution, partial slot or -1}
+  const int4 *gather_splits; // [n_splits] {destination, first partial slot, pieces, 0}
+  double *gather_part;       // [n_pslots * 36]
+  int n_items, n_splits;
+  double *jrows;             // [8 nb kRowStride] unscaled Jacobian rows + residual at the linearization point
 };
 
 // element (r, c), r >= c, of the compact-tiled reduced system

@@ -22,7 +22,28 @@
 
 namespace arslam {
 
+#ifdef ARSLAM_SCHUR_STAMPS
+__device__ unsigned long long g_schur_ph[16];
+#define SCHUR_STAMP_INIT unsigned long long _st0 = clock64()
+#define SCHUR_STAMP(k)                                                         \
+  do {                                                                         \
+    const unsigned long long _n = clock64();                                   \
+    if (threadIdx.x == 0) atomicAdd(&g_schur_ph[k], _n - _st0);                \
+    _st0 = _n;                                                                 \
+  } while (0)
+void debug_read_schur_stamps(unsigned long long *out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_schur_ph), sizeof(g_schur_ph));
+}
+#else
+#define SCHUR_STAMP_INIT do {} while (0)
+#define SCHUR_STAMP(k) do {} while (0)
+void debug_read_schur_stamps(unsigned long long *out) {
+  for (int i = 0; i < 16; ++i) out[i] = 0;
+}
+#endif
+
 namespace {
+
 
 __device__ __forceinline__ long slot_cap(const DevProblem &P, int c) { return 3 + 6L * c; }
 __device__ __forceinline__ long slot_tag(const DevProblem &P, int t) { return 3 + 6L * P.nc + 6L * t; }
@@ -34,8 +55,12 @@ __device__ __forceinline__ double lm_d2(const double *diag, long slot, double ra
 
 // Fill LDS rows [nrows][kRowStride] of capture c: 13 Jacobian entries (scaled
 // by the Jacobi scale if scale != nullptr) and the residual in column 13.
+// With gout, the unscaled rows are also stored there column-major per capture
+// (entry (row, j) at gout + 8 o0 kRowStride + j nrows + row): the Schur and
+// back-substitution passes at the same point reload them instead of
+// re-evaluating the projection.
 __device__ void fill_rows(const DevProblem &P, const double *x, const double *scale, int c,
-                          int o0, int nrows, double *rows) {
+                          int o0, int nrows, double *rows, double *gout = nullptr) {
   const double *cam = x;
   const double *cap = x + slot_cap(P, c);
   for (int row = threadIdx.x; row < nrows; row += kWave) {
@@ -61,6 +86,34 @@ __device__ void fill_rows(const DevProblem &P, const double *x, const double *sc
       for (int j = 0; j < 13; ++j) dst[j] = J[j];
     }
     dst[13] = r;
+    if (gout) {
+      double *g = gout + 8L * o0 * kRowStride + row;
+#pragma unroll
+      for (int j = 0; j < 13; ++j) g[(long)j * nrows] = J[j];
+      g[13L * nrows] = r;
+    }
+  }
+}
+
+// LDS rows of capture c from the copy fill_rows stored at the same point,
+// Jacobi-scaled.
+__device__ void load_rows(const DevProblem &P, const double *scale, int c, int o0, int nrows,
+                          double *rows) {
+  const double *sc = scale + slot_cap(P, c);
+  for (int row = threadIdx.x; row < nrows; row += kWave) {
+    const double *g = P.jrows + 8L * o0 * kRowStride + row;
+    double v[14];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) v[j] = g[(long)j * nrows];
+    const double *st = scale + slot_tag(P, P.obs_tag[o0 + (row >> 3)]);
+    double *dst = rows + (long)row * kRowStride;
+    dst[0] = v[0] * scale[0];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      dst[1 + j] = v[1 + j] * sc[j];
+      dst[7 + j] = v[7 + j] * st[j];
+    }
+    dst[13] = v[13];
   }
 }
 
@@ -146,7 +199,7 @@ __global__ __launch_bounds__(kWave) void k_linearize(DevProblem P, const double 
   const int nrows = 8 * k;
   double *rows = sm;
   double *ocost = rows + (long)nrows * kRowStride;   // [k]
-  fill_rows(P, x, nullptr, c, o0, nrows, rows);
+  fill_rows(P, x, nullptr, c, o0, nrows, rows, P.jrows);
   __syncthreads();
   // per observation: cost, tag gradient (6), tag column norms (6)
   for (int e = lane; e < 13 * k; e += kWave) {
@@ -240,13 +293,15 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
   diag[i] = fmin(fmax(d, dmin), dmax);
 }
 
-// Schur elimination of capture c into the reduced system S (compact tiles,
-// lower triangle); row nR of S accumulates the reduced right-hand side.
-__global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ x,
-                                                 const double *__restrict__ scale,
-                                                 const double *__restrict__ diag, double radius,
-                                                 double *__restrict__ S) {
+// Schur elimination of capture c (ComputeTrustRegionStep's DENSE_SCHUR
+// eliminate step, one capture = one e-block): the packed local reduced system
+//   [F'F - W' U^-1 W | F'r - W' U^-1 E'r],  U = E'E + D_c^2, W = E'F,
+// over the local f-side columns (f, then 6 per distinct tag of the capture),
+// stored for k_schur_gather.  One wave per capture.
+__global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ scale,
+                                                 const double *__restrict__ diag, double radius) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
+  SCHUR_STAMP_INIT;
   const int c = blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
   if (k == 0) return;
@@ -261,50 +316,133 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   double *W = UiE + 8;                           // 6*m
   double *Z = W + 6 * m;                         // 6*m
   double *Ftr = Z + 6 * m;                       // m (+pad)
-  int *lblk = (int *)(Ftr + m + (m & 1));        // k
-  long *gidx = (long *)(lblk + k + (k & 1));     // m
+  double *FF = Ftr + m + (m & 1);                // 28 per tag block: F_u'F_u (21, packed), F_0'F_u (6), pad
+  int *lblk = (int *)(FF + 28 * nblk);           // k
+  double *ff00 = reinterpret_cast<double *>(lblk + k + (k & 1));   // F_0'F_0
 
   for (int q = lane; q < k; q += kWave) lblk[q] = P.obs_lblk[o0 + q];
-  for (int p = lane; p < m; p += kWave) {
-    if (p == 0) {
-      gidx[p] = P.cam_row;   // f; -1 when the camera is held constant
-    } else {
-      const int tr = P.tag_row[P.blk_tag[b0 + (p - 1) / 6]];
-      gidx[p] = tr < 0 ? -1 : tr + (p - 1) % 6;
-    }
-  }
-  fill_rows(P, x, scale, c, o0, nrows, rows);
+  load_rows(P, scale, c, o0, nrows, rows);
   __syncthreads();
-  // U = E'E (21 unique) and E'r
-  if (lane < 27) {
-    if (lane < 21) {
-      int a, b;
-      upper6(lane, a, b);
-      const double s = block_dot(rows, lblk, k, 0, 1 + a, 1 + b);
-      U[6 * a + b] = s;
-      U[6 * b + a] = s;
-    } else {
-      const int a = lane - 21;
-      Etr[a] = block_dot(rows, lblk, k, 0, 1 + a, 13);
-    }
-  }
-  // W = E'F and F'r (local column 0 = f over all rows; 1+6u+j = tag block u+1)
-  for (int e = lane; e < 7 * m; e += kWave) {
-    const int a = e / m, col = e % m;   // a == 6 -> F'r
-    const int u = col == 0 ? 0 : 1 + (col - 1) / 6;
-    const int fcol = col == 0 ? 0 : 7 + (col - 1) % 6;
-    const int ecol = a < 6 ? 1 + a : 13;
-    const double s = block_dot(rows, lblk, k, u, ecol, fcol);
-    if (a < 6) W[a * m + col] = s; else Ftr[col] = s;
-  }
-  __syncthreads();
-  if (lane == 0) {
-    const long sc = slot_cap(P, c);
+  SCHUR_STAMP(0);
+  // U = E'E, E'r, the f column of W (E'F_0), F_0'r and F_0'F_0: one row per
+  // lane, xor-butterfly sums (every lane gets the same bits)
+  {
+    double prod[35];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) U[7 * a] += lm_d2(diag, sc + a, radius);
-    inv6(U, Ui);
+    for (int e = 0; e < 35; ++e) prod[e] = 0.0;
+    for (int r = lane; r < nrows; r += kWave) {
+      const double *rr = rows + (long)r * kRowStride;
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = i; j < 6; ++j) prod[e++] += rr[1 + i] * rr[1 + j];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) prod[21 + i] += rr[1 + i] * rr[13];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) prod[27 + i] += rr[1 + i] * rr[0];
+      prod[33] += rr[0] * rr[13];
+      prod[34] += rr[0] * rr[0];
+    }
+#pragma unroll
+    for (int e = 0; e < 35; ++e) prod[e] = wave_sum(prod[e]);
+    if (lane == 0) {
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = i; j < 6; ++j) {
+          U[6 * i + j] = prod[e];
+          U[6 * j + i] = prod[e];
+          ++e;
+        }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        Etr[i] = prod[21 + i];
+        W[i * m] = prod[27 + i];
+      }
+      Ftr[0] = prod[33];
+      *ff00 = prod[34];
+    }
+  }
+  // per tag block u (its observations' rows): W_u = E'F_u (36), F_u'r (6),
+  // F_u'F_u (21), F_0'F_u (6) -- 69 row dots per block
+  for (int e = lane; e < 69 * nblk; e += kWave) {
+    const int u = e / 69, t = e % 69;
+    int ci, cj;
+    if (t < 36) {
+      ci = 1 + t / 6;
+      cj = 7 + t % 6;
+    } else if (t < 42) {
+      ci = 7 + (t - 36);
+      cj = 13;
+    } else if (t < 63) {
+      int a, b;
+      upper6(t - 42, a, b);
+      ci = 7 + a;
+      cj = 7 + b;
+    } else {
+      ci = 0;
+      cj = 7 + (t - 63);
+    }
+    const double s = block_dot(rows, lblk, k, u + 1, ci, cj);
+    if (t < 36) W[(t / 6) * m + 1 + 6 * u + t % 6] = s;
+    else if (t < 42) Ftr[1 + 6 * u + (t - 36)] = s;
+    else FF[28 * u + (t - 42)] = s;
   }
   __syncthreads();
+  SCHUR_STAMP(1);
+  // (U + D_c^2)^{-1}: every lane factors U (one reciprocal per pivot), lane j
+  // solves for column j
+  {
+    const long sc = slot_cap(P, c);
+    double L[21];
+    double rd[6];
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j <= i; ++j) L[e++] = U[6 * i + j] + (i == j ? lm_d2(diag, sc + i, radius) : 0.0);
+#define LI6(i, j) L[(i) * ((i) + 1) / 2 + (j)]
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      double d = LI6(j, j);
+#pragma unroll
+      for (int p = 0; p < j; ++p) d -= LI6(j, p) * LI6(j, p);
+      const double sd = sqrt(d);
+      rd[j] = 1.0 / sd;
+      LI6(j, j) = sd;
+#pragma unroll
+      for (int i = j + 1; i < 6; ++i) {
+        double v = LI6(i, j);
+#pragma unroll
+        for (int p = 0; p < j; ++p) v -= LI6(i, p) * LI6(j, p);
+        LI6(i, j) = v * rd[j];
+      }
+    }
+    if (lane < 6) {
+      double ev[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        double v = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int p = 0; p < i; ++p) v -= LI6(i, p) * ev[p];
+        ev[i] = v * rd[i];
+      }
+#pragma unroll
+      for (int i = 5; i >= 0; --i) {
+        double v = ev[i];
+#pragma unroll
+        for (int p = i + 1; p < 6; ++p) v -= LI6(p, i) * ev[p];
+        ev[i] = v * rd[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Ui[6 * i + lane] = ev[i];
+    }
+#undef LI6
+  }
+  __syncthreads();
+  SCHUR_STAMP(2);
   // Z = Ui W ; UiE = Ui E'r
   for (int e = lane; e < 6 * m + 6; e += kWave) {
     if (e < 6 * m) {
@@ -322,37 +460,143 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
     }
   }
   __syncthreads();
-  // reduced rhs (row nR): F'r - W' Ui E'r
-  for (int p = lane; p < m; p += kWave) {
-    if (gidx[p] < 0) continue;
-    double s = 0.0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) s += W[a * m + p] * UiE[a];
-    atomicAdd(reduced_elem(S, P, P.nR, gidx[p]), Ftr[p] - s);
-  }
-  // reduced matrix: F'F - W' Ui W, local pairs p >= q
-  const int npairs = m * (m + 1) / 2;
+  SCHUR_STAMP(3);
+  // packed rows p >= q (row m is the rhs); entries of constant blocks are
+  // never gathered
+  double *out = P.slab + P.cap_off[c];
+  const int npairs = (m + 1) * (m + 2) / 2;
   for (int e = lane; e < npairs; e += kWave) {
-    int p = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-    while (p * (p + 1) / 2 > e) --p;
-    while ((p + 1) * (p + 2) / 2 <= e) ++p;
+    int p = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    p -= (p * (p + 1) / 2 > e);
+    p += ((p + 1) * (p + 2) / 2 <= e);
     const int q = e - p * (p + 1) / 2;
-    // F'F entry
-    double ff = 0.0;
-    const int up = p == 0 ? 0 : 1 + (p - 1) / 6, uq = q == 0 ? 0 : 1 + (q - 1) / 6;
-    if (up == 0 || uq == 0 || up == uq) {
-      const int u = up == 0 ? uq : up;   // rows shared by both columns
-      const int ip = p == 0 ? 0 : 7 + (p - 1) % 6, iq = q == 0 ? 0 : 7 + (q - 1) % 6;
-      ff = block_dot(rows, lblk, k, u, ip, iq);
-    }
-    double wz = 0.0;
+    double v = 0.0;
+    if (p == m) {
+      if (q < m) {
+        double s = 0.0;
 #pragma unroll
-    for (int a = 0; a < 6; ++a) wz += W[a * m + p] * Z[a * m + q];
-    const long gi = gidx[p], gj = gidx[q];
-    if (gi < 0 || gj < 0) continue;
-    const long hi = gi > gj ? gi : gj, lo = gi > gj ? gj : gi;
-    atomicAdd(reduced_elem(S, P, hi, lo), ff - wz);
+        for (int a = 0; a < 6; ++a) s += W[a * m + q] * UiE[a];
+        v = Ftr[q] - s;
+      }
+    } else {
+      double ff = 0.0;
+      const int up = p == 0 ? -1 : (p - 1) / 6, uq = q == 0 ? -1 : (q - 1) / 6;
+      if (p == 0) {
+        ff = *ff00;   // q == 0
+      } else if (q == 0) {
+        ff = FF[28 * up + 21 + (p - 1) % 6];
+      } else if (up == uq) {
+        const int ip = (p - 1) % 6, iq = (q - 1) % 6;   // iq <= ip
+        ff = FF[28 * up + iq * 6 - iq * (iq - 1) / 2 + (ip - iq)];
+      }
+      double wz = 0.0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) wz += W[a * m + p] * Z[a * m + q];
+      v = ff - wz;
+    }
+    out[e] = v;
   }
+  SCHUR_STAMP(4);
+}
+
+// Destination block geometry: E = sX sY elements (1 row for f and the rhs,
+// 6 for a tag), G = 64 / E lane groups; lane -> (element (i, j), group).
+struct GatherLane {
+  int E, G, el, grp, i, j;
+  __device__ GatherLane(const DevProblem &P, int2 rr, int lane) {
+    const int sx = (rr.x == P.nR || rr.x == P.cam_row) ? 1 : 6;
+    const int sy = rr.y == P.cam_row ? 1 : 6;
+    E = sx * sy;
+    G = kWave / E;
+    el = lane % E;
+    grp = lane / E;
+    i = el / sy;
+    j = el % sy;
+  }
+};
+
+// Lanes < E of the wave: the sum of the groups' partials, in group order.
+__device__ __forceinline__ double gather_groups(double s, const GatherLane &g, double *part, int lane) {
+  if (g.G == 1) return s;
+  part[lane] = s;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double t = 0.0;
+  if (lane < g.E)
+    for (int q = 0; q < g.G; ++q) t += part[q * g.E + lane];
+  return t;
+}
+
+// Sum of the captures' packed local systems into the reduced tiles: one wave
+// per work item (a destination block (rX, rY), or a <= 64-contribution piece
+// of one).  The wave stages the item's contribution descriptors in LDS; the
+// G lane groups stride over them with 8 slab loads in flight per lane, and
+// the groups' partials are added in group order -- a fixed summation order,
+// no atomics.  Pieces store partial sums for k_schur_combine.
+__global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__restrict__ S) {
+  __shared__ double part[4][kWave];
+  __shared__ SchurContrib cts[4][kWave];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int it = blockIdx.x * 4 + w;
+  if (it >= P.n_items) return;
+  const int4 item = P.gather_items[it];
+  const int2 rr = P.dest_row[item.x];
+  const GatherLane g(P, rr, lane);
+  const int nk = item.z - item.y;   // <= 64
+  if (lane < nk) cts[w][lane] = P.contrib[item.y + lane];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double s = 0.0;
+  if (g.grp < g.G) {
+    for (int t0 = g.grp; t0 < nk; t0 += 8 * g.G) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = min(t0 + u * g.G, nk - 1);   // clamped: always a valid address
+        const SchurContrib ct = cts[w][t];
+        const int a = ct.px + g.i, b = ct.py + g.j;
+        const int hi = a > b ? a : b, lo = a > b ? b : a;
+        v[u] = P.slab[ct.off + (long)hi * (hi + 1) / 2 + lo];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (t0 + u * g.G < nk) ? v[u] : 0.0;
+    }
+  }
+  s = gather_groups(s, g, part[w], lane);
+  if (lane >= g.E) return;
+  if (item.w >= 0) {
+    P.gather_part[(long)item.w * 36 + lane] = s;
+  } else {
+    const long r = rr.x + g.i, col = rr.y + g.j;
+    if (r >= col) *reduced_elem(S, P, r, col) = s;
+  }
+}
+
+// Split destinations: the pieces' partial sums, in piece order.
+__global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__restrict__ S) {
+  __shared__ double part[4][kWave];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sp = blockIdx.x * 4 + w;
+  if (sp >= P.n_splits) return;
+  const int4 split = P.gather_splits[sp];
+  const int2 rr = P.dest_row[split.x];
+  const GatherLane g(P, rr, lane);
+  double s = 0.0;
+  if (g.grp < g.G) {
+    for (int t0 = g.grp; t0 < split.z; t0 += 8 * g.G) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = P.gather_part[(long)(split.y + min(t0 + u * g.G, split.z - 1)) * 36 + g.el];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (t0 + u * g.G < split.z) ? v[u] : 0.0;
+    }
+  }
+  s = gather_groups(s, g, part[w], lane);
+  const long r = rr.x + g.i, col = rr.y + g.j;
+  if (lane < g.E && r >= col) *reduced_elem(S, P, r, col) = s;
 }
 
 // S[i][i] += D_f^2 for the reduced (tag + camera) rows; alignment padding and
@@ -402,7 +646,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   double *Ui = U + 36;                            // 36
   double *v = Ui + 36;                            // 8
   double *yc = v + 8;                             // 8
-  fill_rows(P, x, scale, c, o0, nrows, rows);
+  load_rows(P, scale, c, o0, nrows, rows);
   __syncthreads();
   const double yf = P.cam_row >= 0 ? yF[P.cam_row] : 0.0;
   for (int row = lane; row < nrows; row += kWave) {
@@ -712,9 +956,13 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
   if (P.nc == 0) return;
   const int maxk = P.max_obs_per_cap;
   const int m = 1 + 6 * maxk;
-  const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 8 + 13L * m + 4) +
-                     sizeof(int) * (maxk + 2) + sizeof(long) * m + 64;
-  hipLaunchKernelGGL(k_schur, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, S);
+  const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 8 + 13L * m + 4 + 28L * maxk) +
+                     sizeof(int) * (maxk + 2) + 2 * sizeof(double) + 64;
+  hipLaunchKernelGGL(k_schur, dim3(P.nc), dim3(kWave), lds, s, P, scale, diag, radius);
+  if (P.n_items)
+    hipLaunchKernelGGL(k_schur_gather, dim3((unsigned)((P.n_items + 3) / 4)), dim3(256), 0, s, P, S);
+  if (P.n_splits)
+    hipLaunchKernelGGL(k_schur_combine, dim3((unsigned)((P.n_splits + 3) / 4)), dim3(256), 0, s, P, S);
 }
 
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,

@@ -135,6 +135,13 @@ struct arslam_lm {
   DevBuf<double> d_corners, d_x0, d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_norms, d_S, d_z, d_yF;
   DevBuf<int> d_flag, d_tag_row, d_row_slot;
+  DevBuf<long> d_cap_off;
+  DevBuf<double> d_slab, d_jrows;
+  DevBuf<int2> d_dest_row;
+  DevBuf<int4> d_gather_items, d_gather_splits;
+  DevBuf<double> d_gather_part;
+  DevBuf<int> d_dest_start;
+  DevBuf<arslam::SchurContrib> d_contrib;
   arslam::LltPlan plan;
   double *x = nullptr, *xc = nullptr;
   int n_fparts = 0;
@@ -303,6 +310,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_xa.alloc(n); d_xb.alloc(n); d_xbest.alloc(n);
   d_g.alloc(n); d_colnorm.alloc(n); d_scale.alloc(n); d_diag.alloc(n);
   d_obs_tg.alloc(std::max(12L * nb, 1L));
+  d_jrows.alloc(std::max(8L * arslam::kRowStride * nb, 1L));
   d_parts.alloc((size_t)arslam::NPART * std::max(nc, 1));
   n_fparts = (int)((std::max(nR, 1L) + 255) / 256);
   d_fparts.alloc(2L * std::max(n_fparts, 1));
@@ -313,7 +321,24 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_flag.alloc(1);
   d_tag_row.alloc(tag_row.size()); d_tag_row.upload(tag_row.data(), tag_row.size(), stream);
   d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
+  int n_dest = 0, n_items = 0, n_splits = 0;
   if (has_f) {
+    const arslam::SchurGather sg = arslam::schur_gather_plan(h, L);
+    n_dest = (int)sg.dest_start.size() - 1;
+    d_cap_off.alloc(nc + 1); d_cap_off.upload(sg.cap_off.data(), nc + 1, stream);
+    d_slab.alloc(std::max(sg.cap_off[nc], 1L));
+    d_dest_row.alloc(std::max(n_dest, 1));
+    d_dest_row.upload(reinterpret_cast<const int2 *>(sg.dest_row.data()), n_dest, stream);
+    d_dest_start.alloc(n_dest + 1); d_dest_start.upload(sg.dest_start.data(), n_dest + 1, stream);
+    d_contrib.alloc(std::max<size_t>(sg.contrib.size(), 1)); d_contrib.upload(sg.contrib.data(), sg.contrib.size(), stream);
+    n_items = (int)sg.items.size() / 4;
+    n_splits = (int)sg.splits.size() / 4;
+    d_gather_items.alloc(std::max(n_items, 1));
+    d_gather_items.upload(reinterpret_cast<const int4 *>(sg.items.data()), n_items, stream);
+    d_gather_splits.alloc(std::max(n_splits, 1));
+    d_gather_splits.upload(reinterpret_cast<const int4 *>(sg.splits.data()), n_splits, stream);
+    d_gather_part.alloc(36L * std::max(sg.n_pslots, 1));
+    HIP_CHECK(hipStreamSynchronize(stream));   // sg's host buffers go out of scope
     d_S.alloc((size_t)plan.n_tiles * 4096);
     HIP_CHECK(hipMemsetAsync(d_S.p, 0, d_S.n * sizeof(double), stream));
     d_z.alloc(N);
@@ -333,6 +358,10 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   P.tag_start = d_tag_start.p; P.tag_obs = d_tag_obs.p; P.corners = d_corners.p;
   P.tag_row = d_tag_row.p; P.row_slot = d_row_slot.p;
   P.tile_id = plan.tile_id; P.T = plan.T;
+  P.cap_off = d_cap_off.p; P.slab = d_slab.p; P.dest_row = d_dest_row.p; P.dest_start = d_dest_start.p;
+  P.contrib = d_contrib.p; P.n_dest = n_dest; P.jrows = d_jrows.p;
+  P.gather_items = d_gather_items.p; P.gather_splits = d_gather_splits.p; P.gather_part = d_gather_part.p;
+  P.n_items = n_items; P.n_splits = n_splits;
   HIP_CHECK(hipStreamSynchronize(stream));
   loaded = true;
 }

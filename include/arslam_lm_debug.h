@@ -50,6 +50,10 @@ typedef struct {
   int dag_valid;           /* 1: run one at a time in ticket order, every wait is already met */
 } arslam_plan_info;
 
+/* diagnostic builds only (-DARSLAM_SCHUR_STAMPS): per-phase cycles of the
+ * Schur kernel accumulated over all its waves (zeros otherwise) */
+int arslam_debug_schur_stamps(unsigned long long out[16]);
+
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);
 

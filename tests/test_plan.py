@@ -86,3 +86,15 @@ def test_invalid_problem_rejected_on_host(L):
     bad[0] = g.n_tag
     with pytest.raises(L.LMError):
         L.debug_reduced_plan(g.camera, g.cap, g.tag, g.obs_cap, bad, g.corners)
+
+
+@pytest.mark.parametrize("name", ["medium", "cfg2", "cfg3"])
+def test_task_graph_is_deadlock_free(L, name):
+    """The persistent executor's ticket order: every wait is met by earlier tickets when run one at a
+    time, and randomised interleavings of 1..512 concurrent workers never deadlock
+    (dag_check / dag_simulate behind arslam_debug_reduced_plan)."""
+    g = synth.config_graph(name)
+    for ordering in (1, 2):
+        info, _ = _plan(L, g, ordering=ordering)
+        assert info["n_dag_tasks"] > 0
+        assert info["dag_valid"] == 1, info
