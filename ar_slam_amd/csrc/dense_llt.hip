@@ -130,6 +130,31 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
+// v of lane l of this lane's 16-lane row: one v_mov_b64_dpp row_newbcast:l.
+// l must fold to a constant (unrolled loops; the switch then disappears), and
+// the source lane must be active: call it outside divergent conditions.
+__device__ __forceinline__ double bcast16(double v, int l) {
+  switch (l) {
+    case 0: return __builtin_amdgcn_mov_dpp(v, 0x150, 0xf, 0xf, false);
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0x151, 0xf, 0xf, false);
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0x152, 0xf, 0xf, false);
+    case 3: return __builtin_amdgcn_mov_dpp(v, 0x153, 0xf, 0xf, false);
+    case 4: return __builtin_amdgcn_mov_dpp(v, 0x154, 0xf, 0xf, false);
+    case 5: return __builtin_amdgcn_mov_dpp(v, 0x155, 0xf, 0xf, false);
+    case 6: return __builtin_amdgcn_mov_dpp(v, 0x156, 0xf, 0xf, false);
+    case 7: return __builtin_amdgcn_mov_dpp(v, 0x157, 0xf, 0xf, false);
+    case 8: return __builtin_amdgcn_mov_dpp(v, 0x158, 0xf, 0xf, false);
+    case 9: return __builtin_amdgcn_mov_dpp(v, 0x159, 0xf, 0xf, false);
+    case 10: return __builtin_amdgcn_mov_dpp(v, 0x15a, 0xf, 0xf, false);
+    case 11: return __builtin_amdgcn_mov_dpp(v, 0x15b, 0xf, 0xf, false);
+    case 12: return __builtin_amdgcn_mov_dpp(v, 0x15c, 0xf, 0xf, false);
+    case 13: return __builtin_amdgcn_mov_dpp(v, 0x15d, 0xf, 0xf, false);
+    case 14: return __builtin_amdgcn_mov_dpp(v, 0x15e, 0xf, 0xf, false);
+    case 15: return __builtin_amdgcn_mov_dpp(v, 0x15f, 0xf, 0xf, false);
+    default: return v;
+  }
+}
+
 // One wave: C(16x16) -= A(16 x K) B(16 x K)^T, operands in LDS (pitch LQ).
 __device__ __forceinline__ void wave_gemm16_sub(double *C, const double *A, const double *B, int K,
                                                 int lane) {
@@ -174,59 +199,53 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
     const int b0 = 16 * p;
     STAMP(10 + 4 * p);
     if (w == 0) {
-      // 16x16 diagonal block, lane i < 16 owns row b0+i in registers.  LDL^T
-      // form: a_ic -= (a_ij / a_jj) a_cj, so only a reciprocal sits on the
-      // pivot chain (square roots are taken once at the end); every broadcast
-      // is a v_readlane from the owning lane -- no LDS round trip per pivot.
-      double x[16];
+      // 16x16 diagonal block, lane i (of each 16-lane row, redundantly) owns
+      // row b0+i in registers.  One elimination pass over [A | I] gives both
+      // factors: LDL^T with only a reciprocal on the pivot chain (x_i[c] =
+      // d_c Lu_ic, x_i[i] = d_i) and, by the same row operations on the right
+      // half, Lu^{-1}.  Every broadcast is a DPP row_newbcast from the owning
+      // lane (no LDS round trip, no SGPR hop per pivot).
+      double x[16], y[16];
       const int li = lane & 15;
       const int i = b0 + li;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) x[c] = D[i * LQ + b0 + c];
+      for (int c = 0; c < 16; ++c) {
+        x[c] = D[i * LQ + b0 + c];
+        y[c] = (c == li) ? 1.0 : 0.0;
+      }
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) {
-        const double ajj = readlane_d(x[jj], jj);
+      for (int j = 0; j < 16; ++j) {
+        const double ajj = bcast16(x[j], j);
         double r = __builtin_amdgcn_rcp(ajj);
         r = r * (2.0 - ajj * r);                    // Newton refinement of v_rcp_f64
         r = r * (2.0 - ajj * r);
-        const double f = (li > jj) ? x[jj] * r : 0.0;
+        const double f = (li > j) ? x[j] * r : 0.0;
 #pragma unroll
-        for (int c = jj + 1; c < 16; ++c) x[c] -= f * readlane_d(x[jj], c);
+        for (int c = j + 1; c < 16; ++c) x[c] -= f * bcast16(x[j], c);
+#pragma unroll
+        for (int c = 0; c <= j; ++c) y[c] -= f * bcast16(y[c], j);
       }
-      // pivots are x_i[i]; L_ic = x_i[c] / sqrt(piv_c), L_ii = sqrt(piv_i)
+      // pivots x_i[i]: L_ic = x_i[c] / sqrt(piv_c), L_ii = sqrt(piv_i);
+      // L^{-1} = D^{-1/2} Lu^{-1}: row i is y_i / sqrt(piv_i)
       double piv = 0.0;
 #pragma unroll
       for (int c = 0; c < 16; ++c) piv = (c == li) ? x[c] : piv;
       if (!(piv > 0.0) && lane < 16) *bad = 1;
       const double d = sqrt(piv), rd = 1.0 / d;
+      double *Li = LTd + p * 16 * LI;
+      double lc[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double rdc = bcast16(rd, c);   // outside any condition: a DPP read needs its source lane active
+        lc[c] = (c < li) ? x[c] * rdc : (c == li ? d : 0.0);
+      }
       if (lane < 16) {
         inv[i] = rd;
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
-          const double l = (c < li) ? x[c] * readlane_d(rd, c) : (c == li ? d : 0.0);
+          const double l = lc[c];
           D[i * LQ + b0 + c] = l;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // explicit inverse of the 16x16 diagonal block: lane c < 16 forward-
-      // substitutes column c of L_pp^{-1} (right-looking, so only one multiply
-      // and one FMA per step sit on the dependency chain)
-      {
-        double v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = (r == li) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          v[k] *= inv[b0 + k];
-#pragma unroll
-          for (int r = k + 1; r < 16; ++r) v[r] -= D[(b0 + r) * LQ + b0 + k] * v[k];
-        }
-        double *Li = LTd + p * 16 * LI;
-        if (lane < 16) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) Li[r * LI + li] = v[r];
+          Li[li * LI + c] = (c <= li) ? y[c] * rd : 0.0;
         }
       }
     }
@@ -664,7 +683,7 @@ struct DagArgs {
   int *split_cnt;
   int *flag;
   int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
-  unsigned long long *trace;  // debug: [n_tasks][4] s_memrealtime at draw / waits met / end, workgroup
+  unsigned long long *trace;  // debug: [n_tasks][8] s_memrealtime at draw / waits met / end, workgroup, sub-phases
 };
 
 __device__ __forceinline__ unsigned long long realtime() {
@@ -700,7 +719,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     if (t >= a.n_tasks) break;
     const int4 task = a.tasks[t];
     DAG_PROGRESS(2, task.x);
-    if (a.trace && tid == 0) { a.trace[4L * t] = realtime(); a.trace[4L * t + 3] = blockIdx.x; }
+    if (a.trace && tid == 0) { a.trace[8L * t] = realtime(); a.trace[8L * t + 3] = blockIdx.x; }
     if (tid == 0) {
       const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], a.wait_off[t + 1], a.flag);
       if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
@@ -708,7 +727,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     }
     __syncthreads();
     DAG_PROGRESS(1, 2);
-    if (a.trace && tid == 0) a.trace[4L * t + 1] = realtime();
+    if (a.trace && tid == 0) a.trace[8L * t + 1] = realtime();
+    // the chain tasks (POTRF, TRSM) win SIMD arbitration over co-resident updates
+    if (task.x != 2) __builtin_amdgcn_s_setprio(3);
     if (task.x == 0) {
       // ---- POTRF k: publish L_kk and its 16x16 block inverses, then (off the
       // critical path) the full inverse for the backward solve ----
@@ -736,7 +757,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), D, tid);
       }
       __syncthreads();
+      if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
       const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid);
+      if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
         int first = 0;
         while (first < T64 && D[first * LQ + first] > 0.0) ++first;
@@ -748,6 +771,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         st_wt16(ltd_g + 2 * e, *reinterpret_cast<const dbl2 *>(LTd + 2 * e));
       dag_release(tid);
       if (tid == 0) __hip_atomic_fetch_add(ready + task.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.trace && tid == 0) a.trace[8L * t + 6] = realtime();
       blocked_trinv64(D, LTd, X, tid);
       __syncthreads();
       double *Xg = a.Ld + ((long)a.T + k) * T64 * T64;
@@ -779,7 +803,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         }
       }
       __syncthreads();
+      if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
       blocked_trsm64(X, D, inv, LTd, tid);
+      if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       store_tile_wt(Ct, X, tid, false);
       dag_release(tid);
       if (tid == 0) __hip_atomic_fetch_add(ready + task.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -872,7 +898,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       }
     }
     DAG_PROGRESS(1, 4);
-    if (a.trace && tid == 0) a.trace[4L * t + 2] = realtime();
+    __builtin_amdgcn_s_setprio(0);
+    if (a.trace && tid == 0) a.trace[8L * t + 2] = realtime();
   }
   DAG_PROGRESS(1, 9);
 }

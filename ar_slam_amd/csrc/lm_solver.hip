@@ -530,9 +530,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
         static const char *trace_path = std::getenv("ARSLAM_DAG_TRACE");   // debug: dump one task timeline
         if (trace_path && !dag_traced) {
           DevBuf<unsigned long long> tr;
-          tr.alloc(4 * plan.n_dag_tasks);
+          tr.alloc(8 * plan.n_dag_tasks);
+          HIP_CHECK(hipMemsetAsync(tr.p, 0, tr.n * 8, stream));
           arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, tr.p);
-          std::vector<unsigned long long> h(4 * plan.n_dag_tasks);
+          std::vector<unsigned long long> h(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemcpyAsync(h.data(), tr.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
           HIP_CHECK(hipStreamSynchronize(stream));
           if (FILE *f = std::fopen(trace_path, "wb")) {
