@@ -37,8 +37,10 @@ for k in sorted(set(fetch) | set(write)):
     wr = w * 1024 / max(nw, 1)
     out["kernels"][k] = {"launches": max(nf, nw), "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                          "hbm_bytes_per_launch": rd + wr}
-dom = out["kernels"].get("k_update")
-if dom:
-    out["dominant"] = "k_update"
-    out["hbm_bytes_per_launch"] = dom["hbm_bytes_per_launch"]
+for name in ("k_factor_dag", "k_update"):   # persistent executor first, level launches otherwise
+    dom = out["kernels"].get(name)
+    if dom:
+        out["dominant"] = name
+        out["hbm_bytes_per_launch"] = dom["hbm_bytes_per_launch"]
+        break
 print(json.dumps(out, indent=1))
