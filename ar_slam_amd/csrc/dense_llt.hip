@@ -187,9 +187,75 @@ __device__ __forceinline__ void wave_apply_inv16(double *C, const double *Linv, 
   for (int reg = 0; reg < 4; ++reg) C[(lk + 4 * reg) * LQ + li] = acc[reg];
 }
 
-// In-LDS blocked Cholesky of the 64x64 tile D (256 threads).  Sub-panels of
-// 16 columns: unblocked 16x16 factor (16 lanes of wave 0), row solve of the
-// panel below (16 lanes per wave), MFMA rank-16 update of the trailing tile.
+// v of DPP row g (16 lanes) of this wave, lane-wise, in every row: two
+// v_permlane16_swap_b32 (within pairs of rows) then two v_permlane32_swap_b32
+// (between the halves), picking the half that holds row g.  g must fold to
+// a constant (unrolled loops).
+__device__ __forceinline__ double rowbcast(double v, int g) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo0 = (unsigned)u, hi0 = (unsigned)(u >> 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo0, lo0, false, false);   // {even rows, odd rows} replicated per pair
+  const auto b = __builtin_amdgcn_permlane16_swap(hi0, hi0, false, false);
+  const unsigned lo1 = (g & 1) ? a[1] : a[0], hi1 = (g & 1) ? b[1] : b[0];
+  const auto c = __builtin_amdgcn_permlane32_swap(lo1, lo1, false, false);   // {lower half, upper half} replicated
+  const auto d = __builtin_amdgcn_permlane32_swap(hi1, hi1, false, false);
+  const unsigned lo = (g & 2) ? c[1] : c[0], hi = (g & 2) ? d[1] : d[0];
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// 16x16 diagonal block (rows/cols b0..b0+15 of D, lower triangle) on one
+// wave: L into D (zeros above the diagonal), L^{-1} into Li (pitch LI),
+// 1/L_ii into inv.  Lane 16 g + i owns row i, columns 4g..4g+3, of both
+// halves of [A | I]; one Gaussian elimination pass turns A into U = Dg Lu^T
+// and I into Lu^{-1} (Lu unit lower, Dg the pivots), so L^T = Dg^{-1/2} U and
+// L^{-1} = Dg^{-1/2} Lu^{-1}.  Per pivot j: the row-j entries come by DPP
+// row_newbcast from lane j of the same row, the column-j entries x_i[j] by a
+// cross-row broadcast from row j/4; the only chain is rcp + two Newton steps.
+// The four rows work on different columns, so no instruction is redundant.
+__device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *Li, int *bad, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int g = lane >> 4, i = lane & 15;
+  double x[4], y[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {   // the lower triangle is the valid half: mirror it
+    const int c = 4 * g + q;
+    x[q] = c <= i ? D[(b0 + i) * LQ + b0 + c] : D[(b0 + c) * LQ + b0 + i];
+    y[q] = (c == i) ? 1.0 : 0.0;
+  }
+  double piv = 1.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double xij = rowbcast(x[j & 3], j >> 2);   // x_i[j], every row
+    const double ajj = bcast16(xij, j);
+    double r = __builtin_amdgcn_rcp(ajj);
+    r = r * (2.0 - ajj * r);                          // Newton refinement of v_rcp_f64
+    r = r * (2.0 - ajj * r);
+    piv = (i == j) ? ajj : piv;
+    const double f = (i > j) ? xij * r : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] -= f * bcast16(x[q], j);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] -= f * bcast16(y[q], j);
+  }
+  if (!(piv > 0.0)) *bad = 1;
+  const double d = sqrt(piv), rd = 1.0 / d;
+  // lane (g, i) holds U row i at columns 4g+q: L_{4g+q, i} = U_i[4g+q] / d_i
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * g + q;
+    D[(b0 + r) * LQ + b0 + i] = r > i ? x[q] * rd : (r == i ? d : 0.0);
+    Li[i * LI + r] = (r <= i) ? y[q] * rd : 0.0;
+  }
+  if (g == 0) inv[b0 + i] = rd;
+}
+
+// In-LDS blocked Cholesky of the 64x64 tile D (256 threads), right-looking
+// over 16-column panels with a one-panel lookahead: wave 0 updates the next
+// diagonal block first and factors it (diag16) while waves 1-3 apply the
+// rest of the trailing update, so the critical chain is the four diag16
+// calls plus one 16-row solve and one 16x16 update per panel.
 // Returns false (uniformly) if a pivot is not positive; inv[c] = 1 / L_cc.
 __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, int tid) {
   const int w = tid >> 6, lane = tid & 63;
@@ -199,73 +265,27 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
     const int b0 = 16 * p;
     STAMP(10 + 4 * p);
     if (w == 0) {
-      // 16x16 diagonal block, lane i (of each 16-lane row, redundantly) owns
-      // row b0+i in registers.  One elimination pass over [A | I] gives both
-      // factors: LDL^T with only a reciprocal on the pivot chain (x_i[c] =
-      // d_c Lu_ic, x_i[i] = d_i) and, by the same row operations on the right
-      // half, Lu^{-1}.  Every broadcast is a DPP row_newbcast from the owning
-      // lane (no LDS round trip, no SGPR hop per pivot).
-      double x[16], y[16];
-      const int li = lane & 15;
-      const int i = b0 + li;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        x[c] = D[i * LQ + b0 + c];
-        y[c] = (c == li) ? 1.0 : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double ajj = bcast16(x[j], j);
-        double r = __builtin_amdgcn_rcp(ajj);
-        r = r * (2.0 - ajj * r);                    // Newton refinement of v_rcp_f64
-        r = r * (2.0 - ajj * r);
-        const double f = (li > j) ? x[j] * r : 0.0;
-#pragma unroll
-        for (int c = j + 1; c < 16; ++c) x[c] -= f * bcast16(x[j], c);
-#pragma unroll
-        for (int c = 0; c <= j; ++c) y[c] -= f * bcast16(y[c], j);
-      }
-      // pivots x_i[i]: L_ic = x_i[c] / sqrt(piv_c), L_ii = sqrt(piv_i);
-      // L^{-1} = D^{-1/2} Lu^{-1}: row i is y_i / sqrt(piv_i)
-      double piv = 0.0;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) piv = (c == li) ? x[c] : piv;
-      if (!(piv > 0.0) && lane < 16) *bad = 1;
-      const double d = sqrt(piv), rd = 1.0 / d;
-      double *Li = LTd + p * 16 * LI;
-      double lc[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double rdc = bcast16(rd, c);   // outside any condition: a DPP read needs its source lane active
-        lc[c] = (c < li) ? x[c] * rdc : (c == li ? d : 0.0);
-      }
-      if (lane < 16) {
-        inv[i] = rd;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const double l = lc[c];
-          D[i * LQ + b0 + c] = l;
-          Li[li * LI + c] = (c <= li) ? y[c] * rd : 0.0;
-        }
+      if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
+      diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane);
+    } else if (p > 0) {
+      // panel p-1's update of blocks (I, C), I >= C >= p, except (p, p)
+      const int m = 4 - p, ntl = m * (m + 1) / 2;
+      for (int t = w; t < ntl; t += 3) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int C = t - I * (I + 1) / 2;
+        const int bi = 16 * (p + I), bc = 16 * (p + C);
+        wave_gemm16_sub(D + bi * LQ + bc, D + bi * LQ + b0 - 16, D + bc * LQ + b0 - 16, 16, lane);
       }
     }
     __syncthreads();
     STAMP(11 + 4 * p);
-    // rows below the diagonal block: X L_pp^T = A_panel  ->  X = A_panel L_pp^{-T}
-    if (w < 3 - p) wave_apply_inv16(D + (b0 + 16 + 16 * w) * LQ + b0, LTd + p * 16 * LI, lane);
-    __syncthreads();
-    STAMP(12 + 4 * p);
-    // trailing update of blocks p+1..3 (lower tiles I >= C) with the panel
-    const int m = 3 - p;
-    const int ntl = m * (m + 1) / 2;
-    for (int t = w; t < ntl; t += 4) {
-      int I = 0;
-      while ((I + 1) * (I + 2) / 2 <= t) ++I;
-      const int C = t - I * (I + 1) / 2;
-      const int bi = 16 * (p + 1 + I), bc = 16 * (p + 1 + C);
-      wave_gemm16_sub(D + bi * LQ + bc, D + bi * LQ + b0, D + bc * LQ + b0, 16, lane);
+    if (p < 3) {
+      // rows below the diagonal block: X L_pp^T = A_panel  ->  X = A_panel L_pp^{-T}
+      if (w < 3 - p) wave_apply_inv16(D + (b0 + 16 + 16 * w) * LQ + b0, LTd + p * 16 * LI, lane);
+      __syncthreads();
     }
-    __syncthreads();
+    STAMP(12 + 4 * p);
     STAMP(13 + 4 * p);
   }
   return *bad == 0;

@@ -218,6 +218,7 @@ struct arslam_lm {
 
   int dag_workgroups = 512;
   bool dag_traced = false;
+  int dag_trace_seen = 0;
 
   void ensure_stream() {
     if (opt.device >= 0) HIP_CHECK(hipSetDevice(opt.device));
@@ -528,7 +529,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
         const bool rec = opt.kernel_timing && upd_timing.used < upd_timing.cap;
         if (rec) HIP_CHECK(hipEventRecord(upd_timing.ev[2 * upd_timing.used], stream));
         static const char *trace_path = std::getenv("ARSLAM_DAG_TRACE");   // debug: dump one task timeline
-        if (trace_path && !dag_traced) {
+        static const int trace_skip = std::getenv("ARSLAM_DAG_TRACE_SKIP") ? std::atoi(std::getenv("ARSLAM_DAG_TRACE_SKIP")) : 0;
+        if (trace_path && !dag_traced && dag_trace_seen++ >= trace_skip) {
           DevBuf<unsigned long long> tr;
           tr.alloc(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemsetAsync(tr.p, 0, tr.n * 8, stream));
@@ -541,6 +543,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
             std::fwrite(&n, 8, 1, f);
             std::fwrite(plan.h_dag_tasks.data(), sizeof(int4), n, f);
             std::fwrite(h.data(), 8, h.size(), f);
+            const long nw = (long)plan.h_dag_waits.size();   // the dependency lists, for dag_critical.py
+            std::fwrite(&nw, 8, 1, f);
+            std::fwrite(plan.h_dag_wait_off.data(), sizeof(int), n + 1, f);
+            std::fwrite(plan.h_dag_waits.data(), sizeof(int2), nw, f);
             std::fclose(f);
           }
           dag_traced = true;
