@@ -50,6 +50,129 @@ constexpr int kSplitMin = 6;   // k-lists longer than this are split
 // chunk of an earlier level of the same target, which may be the one that
 // applies it -- has a smaller ticket; so the ticketed persistent kernel
 // cannot deadlock.
+// Ticket order of the task graph by list scheduling: a simulation of
+// kSimWorkers workgroups that, whenever one is free, start the ready task
+// with the longest remaining path to the end of the factorization (its
+// bottom level).  Tickets follow the simulated start order, so the order is
+// topological (a task starts after all of its producers finished) and tasks
+// on the elimination tree's critical chain are drawn as soon as their inputs
+// can be ready instead of behind a wave of updates that can wait.  Costs are
+// calibrated on MI355X task traces (tools/dag_critical.py), in microseconds.
+constexpr int kSimWorkers = 512;
+struct DagNode { double est; int type; int idx; int4 task; std::vector<int2> waits; };
+
+static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, long nt, const LltPlan &plan) {
+  const int n = (int)nodes.size();
+  std::vector<int> ready_prod(nt, -1);
+  std::vector<std::vector<std::pair<int, int>>> by_tile(nt);   // (seq, node) of update items
+  for (int v = 0; v < n; ++v) {
+    const int4 t = nodes[v].task;
+    if (t.x == 0 || t.x == 1) ready_prod[t.w] = v;
+    else by_tile[t.w].push_back({t.z, v});
+  }
+  auto seq_nodes = [&](int tile, int seq, std::vector<int> &out) {
+    for (const auto &sv : by_tile[tile])
+      if (sv.first == seq) out.push_back(sv.second);
+  };
+  std::vector<std::vector<int>> succ(n);
+  std::vector<int> ndep(n, 0);
+  std::vector<double> cost(n);
+  std::vector<int> pr;
+  for (int v = 0; v < n; ++v) {
+    const DagNode &nd = nodes[v];
+    pr.clear();
+    for (const int2 &w : nd.waits) {
+      if (w.x < nt) {
+        if (ready_prod[w.x] >= 0) pr.push_back(ready_prod[w.x]);
+      } else if (w.y > 0) {
+        seq_nodes(w.x - (int)nt, w.y - 1, pr);   // the level before the awaited count (earlier levels chain)
+      }
+    }
+    if (nd.task.x == 2 && nd.task.z > 0) seq_nodes(nd.task.w, nd.task.z - 1, pr);   // in-order application
+    std::sort(pr.begin(), pr.end());
+    pr.erase(std::unique(pr.begin(), pr.end()), pr.end());
+    for (int u : pr) {
+      if (u == v) continue;
+      succ[u].push_back(v);
+      ndep[v]++;
+    }
+    if (nd.task.x == 0) {
+      const int nk = nd.task.z >= 0 ? plan.h_items[nd.task.z].z - plan.h_items[nd.task.z].y : 0;
+      cost[v] = 16.0 + 4.0 * nk;
+    } else if (nd.task.x == 1) {
+      cost[v] = 6.0;
+    } else {
+      const int4 it = plan.h_items[nd.task.y];
+      cost[v] = 4.0 + 4.0 * (it.z - it.y);
+    }
+  }
+  // bottom levels (nodes are created producers-first: a reverse sweep is a valid order)
+  std::vector<int> topo;
+  topo.reserve(n);
+  {
+    std::vector<int> d = ndep;
+    std::vector<int> st;
+    for (int v = 0; v < n; ++v)
+      if (!d[v]) st.push_back(v);
+    while (!st.empty()) {
+      const int u = st.back();
+      st.pop_back();
+      topo.push_back(u);
+      for (int v : succ[u])
+        if (--d[v] == 0) st.push_back(v);
+    }
+    if ((int)topo.size() != n) throw std::runtime_error("dag_list_schedule: task graph has a cycle");
+  }
+  std::vector<double> blevel(n, 0.0);
+  for (int q = n - 1; q >= 0; --q) {
+    const int u = topo[q];
+    double m = 0.0;
+    for (int v : succ[u]) m = std::max(m, blevel[v]);
+    blevel[u] = cost[u] + m;
+  }
+  // simulation
+  auto cmp = [&](int a, int b) {   // max-heap on bottom level, then creation order
+    if (blevel[a] != blevel[b]) return blevel[a] < blevel[b];
+    return a > b;
+  };
+  std::vector<int> heap;
+  std::vector<int> d = ndep;
+  for (int v = 0; v < n; ++v)
+    if (!d[v]) heap.push_back(v);
+  std::make_heap(heap.begin(), heap.end(), cmp);
+  typedef std::pair<double, int> Ev;   // (finish time, node)
+  std::vector<Ev> events;
+  auto ev_cmp = [](const Ev &a, const Ev &b) { return a.first > b.first || (a.first == b.first && a.second > b.second); };
+  std::vector<int> order;
+  order.reserve(n);
+  int busy = 0;
+  double now = 0.0;
+  while ((int)order.size() < n || !events.empty()) {
+    while (busy < kSimWorkers && !heap.empty()) {
+      std::pop_heap(heap.begin(), heap.end(), cmp);
+      const int v = heap.back();
+      heap.pop_back();
+      order.push_back(v);
+      events.push_back({now + cost[v], v});
+      std::push_heap(events.begin(), events.end(), ev_cmp);
+      ++busy;
+    }
+    if (events.empty()) break;
+    std::pop_heap(events.begin(), events.end(), ev_cmp);
+    const Ev e = events.back();
+    events.pop_back();
+    now = e.first;
+    --busy;
+    for (int v : succ[e.second])
+      if (--d[v] == 0) {
+        heap.push_back(v);
+        std::push_heap(heap.begin(), heap.end(), cmp);
+      }
+  }
+  if ((int)order.size() != n) throw std::runtime_error("dag_list_schedule: not every task was scheduled");
+  return order;
+}
+
 void dag_build(LltPlan &plan) {
   const int T = plan.T;
   const long nt = plan.n_tiles;
@@ -68,7 +191,7 @@ void dag_build(LltPlan &plan) {
     for (int it = plan.h_item_off[l]; it < plan.h_item_off[l + 1]; ++it)
       item_seq[it] = seq_of_target[plan.h_items[it].x - t0];
   }
-  struct Node { double est; int type; int idx; int4 task; std::vector<int2> waits; };
+  typedef DagNode Node;
   std::vector<Node> nodes;
   const double c_potrf = 12.0, c_trsm = 3.0, eps = 1e-3;
   std::vector<double> potrf_done(T, 0.0), trsm_done(nt, 0.0), last_apply(nt, 0.0), last_chunk_start(nt, -1.0);
@@ -166,12 +289,7 @@ void dag_build(LltPlan &plan) {
       if (!drop[m]) kept.push_back(std::move(nodes[m]));
     nodes.swap(kept);
   }
-  std::vector<int> order(nodes.size());
-  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-    if (nodes[a].est != nodes[b].est) return nodes[a].est < nodes[b].est;
-    return nodes[a].type < nodes[b].type;
-  });
+  std::vector<int> order = dag_list_schedule(nodes, nt, plan);
   plan.h_dag_tasks.clear();
   plan.h_dag_waits.clear();
   plan.h_dag_wait_off.assign(1, 0);
