@@ -171,6 +171,22 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
       info->update_flops = plan.total_upd_flops;
       info->n_dag_tasks = plan.n_dag_tasks;
       info->dag_valid = arslam::dag_check(plan) ? 1 : 0;
+      if (const char *dump = std::getenv("ARSLAM_DAG_DUMP")) {   // debug: the task graph, for offline analysis
+        if (FILE *f = std::fopen(dump, "wb")) {
+          const long n = plan.n_dag_tasks, nw = (long)plan.h_dag_waits.size(), T = plan.T;
+          std::fwrite(&n, 8, 1, f);
+          std::fwrite(&nw, 8, 1, f);
+          std::fwrite(&T, 8, 1, f);
+          std::fwrite(plan.h_dag_tasks.data(), sizeof(int4), n, f);
+          std::fwrite(plan.h_dag_wait_off.data(), sizeof(int), n + 1, f);
+          std::fwrite(plan.h_dag_waits.data(), sizeof(int2), nw, f);
+          std::fwrite(plan.h_dag_sub.data(), sizeof(int2), n, f);
+          std::fwrite(plan.h_tile_id.data(), sizeof(int), (size_t)T * T, f);
+          std::fwrite(plan.h_items.data(), sizeof(int4), plan.h_items.size(), f);
+          std::fwrite(plan.h_targets.data(), sizeof(int2), plan.h_targets.size(), f);
+          std::fclose(f);
+        }
+      }
       for (int wk : {1, 2, 7, 64, 512})
         for (unsigned seed = 1; seed <= 3 && info->dag_valid; ++seed)
           if (!arslam::dag_simulate(plan, wk, seed)) info->dag_valid = -wk;

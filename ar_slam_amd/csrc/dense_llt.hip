@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <utility>
 
 namespace arslam {
 
@@ -203,50 +204,119 @@ __device__ __forceinline__ double rowbcast(double v, int g) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
+// One elimination step of diag16 under an explicit exec mask (constant per
+// pivot, so no per-lane selects): in the rows below the pivot,
+// x_q += nf * xj_q and R += nf * rj; then, in the pivot column's group,
+// register jq becomes nf.  The caller's exec is restored at the end, and the
+// trailing s_nop covers the wait states hipcc does not insert after an asm
+// statement (exec write -> DPP, and the outputs -> the next pivot's DPP).
+__device__ __forceinline__ void elim_step(double &x0, double &x1, double &x2, double &x3, double &R, double nf,
+                                          double y0, double y1, double y2, double y3, double rj,
+                                          unsigned long long below, unsigned long long colj, int jq) {
+  unsigned long long sv;
+#define ARSLAM_ELIM_ASM(XS)                                                                   \
+  asm volatile("s_mov_b64 %[sv], exec\n\t"                                                    \
+               "s_and_b64 exec, %[sv], %[below]\n\t"                                          \
+               "v_fma_f64 %[x0], %[nf], %[y0], %[x0]\n\t"                                     \
+               "v_fma_f64 %[x1], %[nf], %[y1], %[x1]\n\t"                                     \
+               "v_fma_f64 %[x2], %[nf], %[y2], %[x2]\n\t"                                     \
+               "v_fma_f64 %[x3], %[nf], %[y3], %[x3]\n\t"                                     \
+               "v_fma_f64 %[R], %[nf], %[rj], %[R]\n\t"                                       \
+               "s_and_b64 exec, %[sv], %[colj]\n\t"                                           \
+               "v_mov_b64 %[" XS "], %[nf]\n\t"                                               \
+               "s_mov_b64 exec, %[sv]\n\t"                                                    \
+               "s_nop 4"   /* exec write -> DPP: 5 states; VGPR write -> DPP read: 2 */        \
+               : [x0] "+v"(x0), [x1] "+v"(x1), [x2] "+v"(x2), [x3] "+v"(x3), [R] "+v"(R),      \
+                 [sv] "=&s"(sv)                                                                \
+               : [nf] "v"(nf), [y0] "v"(y0), [y1] "v"(y1), [y2] "v"(y2), [y3] "v"(y3),          \
+                 [rj] "v"(rj), [below] "s"(below), [colj] "s"(colj))
+  switch (jq) {
+    case 0: ARSLAM_ELIM_ASM("x0"); break;
+    case 1: ARSLAM_ELIM_ASM("x1"); break;
+    case 2: ARSLAM_ELIM_ASM("x2"); break;
+    default: ARSLAM_ELIM_ASM("x3"); break;
+  }
+#undef ARSLAM_ELIM_ASM
+}
+
+// Pivot J of diag16 (a template, so every broadcast lane and exec mask is a
+// compile-time constant however large the unrolled loop gets).
+template <int j>
+__device__ __forceinline__ void diag16_pivot(double (&x)[4], double &R, double &R2, double *colx, int lane) {
+  const int i = lane & 15;
+  const double ajj = bcast16(R, j);
+  const double r0 = __builtin_amdgcn_rcp(ajj);
+  const double e = __builtin_fma(-ajj, r0, 1.0);   // r0 (1 + e + e^2) = (1 - e^3) / ajj
+  const double nf0 = -R * r0;
+  const double pe = __builtin_fma(e, e, e);
+  const double nf = __builtin_fma(nf0, pe, nf0);    // -f_ij (garbage in rows i <= j: masked below)
+  double xj[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xj[q] = bcast16(x[q], j);
+  const double rj = j + 1 < 16 ? bcast16(R2, j) : 0.0;
+  R = R2;
+  // rows i > j only (exec = the lanes 16 g + i with i > j, a constant per
+  // pivot); then column j of those rows (group j / 4) becomes -f_ij
+  const unsigned long long below = 0x0001000100010001ull * ((0xffffull << (j + 1)) & 0xffffull);
+  const unsigned long long colj = below & (0xffffull << (16 * (j >> 2)));
+  elim_step(x[0], x[1], x[2], x[3], R, nf, xj[0], xj[1], xj[2], xj[3], rj, below, colj, j & 3);
+  if (j + 2 < 16) {   // column j+2 after this pivot, a pivot before it is needed
+    colx[lane] = x[(j + 2) & 3];
+    R2 = colx[16 * ((j + 2) >> 2) + i];
+  }
+}
+
+template <int... J>
+__device__ __forceinline__ void diag16_pivots(double (&x)[4], double &R, double &R2, double *colx, int lane,
+                                              std::integer_sequence<int, J...>) {
+  (diag16_pivot<J>(x, R, R2, colx, lane), ...);
+}
+
 // 16x16 diagonal block (rows/cols b0..b0+15 of D, lower triangle) on one
 // wave: L into D (zeros above the diagonal), L^{-1} into Li (pitch LI),
-// 1/L_ii into inv.  Lane 16 g + i owns row i, columns 4g..4g+3, of both
-// halves of [A | I]; one Gaussian elimination pass turns A into U = Dg Lu^T
-// and I into Lu^{-1} (Lu unit lower, Dg the pivots), so L^T = Dg^{-1/2} U and
-// L^{-1} = Dg^{-1/2} Lu^{-1}.  Per pivot j: the row-j entries come by DPP
-// row_newbcast from lane j of the same row, the column-j entries x_i[j] by a
-// cross-row broadcast from row j/4; the only chain is rcp + two Newton steps.
-// The four rows work on different columns, so no instruction is redundant.
-__device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *Li, int *bad, int lane) {
+// 1/L_ii into inv.  Lane 16 g + i owns row i, columns 4g..4g+3.  One
+// Gaussian elimination pass over A, in place: at pivot j the register of
+// column j in the rows below becomes the multiplier -f_ij, so row i ends as
+// U = Dg Lu^T (columns >= i) and Lu^{-1} (columns < i), with Lu unit lower
+// and Dg the pivots; then L^T = Dg^{-1/2} U and L^{-1} = Dg^{-1/2} Lu^{-1}.
+// Each pivot needs column j in every row; it is kept replicated one pivot
+// ahead (R: column j, R2: column j+1), and column j+2 is fetched through the
+// 64-double LDS scratch colx after pivot j's update, a pivot before it is
+// needed.  Per pivot: DPP broadcast -> v_rcp_f64 -> two-term Newton
+// correction -> multiplier -> update; about 20 VALU instructions, so the
+// block is bound by one wave's issue rate (tools/lat_bench.hip).
+__device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *Li, int *bad, int lane,
+                                       double *colx) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int g = lane >> 4, i = lane & 15;
-  double x[4], y[4];
+  double x[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {   // the lower triangle is the valid half: mirror it
     const int c = 4 * g + q;
     x[q] = c <= i ? D[(b0 + i) * LQ + b0 + c] : D[(b0 + c) * LQ + b0 + i];
-    y[q] = (c == i) ? 1.0 : 0.0;
   }
-  double piv = 1.0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const double xij = rowbcast(x[j & 3], j >> 2);   // x_i[j], every row
-    const double ajj = bcast16(xij, j);
-    double r = __builtin_amdgcn_rcp(ajj);
-    r = r * (2.0 - ajj * r);                          // Newton refinement of v_rcp_f64
-    r = r * (2.0 - ajj * r);
-    piv = (i == j) ? ajj : piv;
-    const double f = (i > j) ? xij * r : 0.0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] -= f * bcast16(x[q], j);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) y[q] -= f * bcast16(y[q], j);
-  }
+  // replicated columns 0 and 1 (lower triangle mirrored)
+  double R = D[(b0 + i) * LQ + b0];
+  double R2 = i >= 1 ? D[(b0 + i) * LQ + b0 + 1] : D[(b0 + 1) * LQ + b0];
+  diag16_pivots(x, R, R2, colx, lane, std::make_integer_sequence<int, 16>{});
+  // pivot of row i: the diagonal entry of U, held by group i / 4
+  __builtin_amdgcn_wave_barrier();
+  if (g == (i >> 2)) colx[i] = (i & 3) == 0 ? x[0] : (i & 3) == 1 ? x[1] : (i & 3) == 2 ? x[2] : x[3];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const double piv = colx[i];
   if (!(piv > 0.0)) *bad = 1;
   const double d = sqrt(piv), rd = 1.0 / d;
-  // lane (g, i) holds U row i at columns 4g+q: L_{4g+q, i} = U_i[4g+q] / d_i
+  // lane (g, i), column c = 4g+q:  L_{c,i} = U_i[c] / d_i (c > i),
+  // (L^{-1})_{i,c} = Lu^{-1}_i[c] / d_i (c < i)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int r = 4 * g + q;
-    D[(b0 + r) * LQ + b0 + i] = r > i ? x[q] * rd : (r == i ? d : 0.0);
-    Li[i * LI + r] = (r <= i) ? y[q] * rd : 0.0;
+    const int c = 4 * g + q;
+    D[(b0 + c) * LQ + b0 + i] = c > i ? x[q] * rd : (c == i ? d : 0.0);
+    Li[i * LI + c] = c < i ? x[q] * rd : (c == i ? rd : 0.0);
   }
   if (g == 0) inv[b0 + i] = rd;
 }
@@ -257,7 +327,7 @@ __device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *L
 // rest of the trailing update, so the critical chain is the four diag16
 // calls plus one 16-row solve and one 16x16 update per panel.
 // Returns false (uniformly) if a pivot is not positive; inv[c] = 1 / L_cc.
-__device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, int tid) {
+__device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, int tid, double *colx) {
   const int w = tid >> 6, lane = tid & 63;
   if (tid == 0) *bad = 0;
   __syncthreads();
@@ -266,7 +336,7 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
     STAMP(10 + 4 * p);
     if (w == 0) {
       if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
-      diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane);
+      diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane, colx);
     } else if (p > 0) {
       // panel p-1's update of blocks (I, C), I >= C >= p, except (p, p)
       const int m = 4 - p, ntl = m * (m + 1) / 2;
@@ -295,15 +365,30 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
 // blocked_potrf64 (lower part of D, inv = 1 / diag).
 __device__ void blocked_trsm64(double *X, const double *D, const double *inv, const double *LTd,
                                int tid) {
+  // row block w of X depends only on itself (and on D, LTd): the four
+  // column steps need wave-local ordering only; one barrier at the end
   const int w = tid >> 6, lane = tid & 63;
   for (int p = 0; p < 4; ++p) {
     const int b0 = 16 * p;
     if (p > 0)   // X[:, b0:b0+16] -= X[:, 0:b0] L[b0:b0+16, 0:b0]^T  (wave w: rows 16w..)
       wave_gemm16_sub(X + 16 * w * LQ + b0, X + 16 * w * LQ, D + b0 * LQ, b0, lane);
+#ifdef ARSLAM_TRSM_SYNC
     __syncthreads();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
     wave_apply_inv16(X + 16 * w * LQ + b0, LTd + p * 16 * LI, lane);
+#ifdef ARSLAM_TRSM_SYNC
     __syncthreads();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
   }
+  __syncthreads();
 }
 
 // Inverse X = L^{-1} of the 64x64 lower factor in D (after blocked_potrf64),
@@ -367,6 +452,7 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, const int
   __shared__ __attribute__((aligned(16))) double X[T64 * LQ];
   __shared__ double inv[T64];
   __shared__ __attribute__((aligned(16))) double LTd[4 * 16 * LI];   // inverses of the 16x16 diagonal blocks
+  __shared__ double colx[T64];
   __shared__ int bad;
   STAMP(0);
   if (*flag) return;
@@ -379,7 +465,7 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, const int
   if (ti != k) load_tile_wg(xt, T64, X, tid);
   __syncthreads();
   STAMP(1);
-  const bool ok = blocked_potrf64(D, inv, LTd, &bad, tid);
+  const bool ok = blocked_potrf64(D, inv, LTd, &bad, tid, colx);
   if (!ok) {
     if (ti == k && tid == 0) {
       int first = 0;
@@ -576,8 +662,11 @@ __device__ __forceinline__ double ld_wt(const double *p) {
 // atomic form).  Loads are issued in groups inside ONE asm statement that
 // also waits for them (vmcnt(0)), so the compiler never sees an asm output
 // before its data has arrived.
+// (the trailing s_nop: a VALU write of the data VGPRs right after a 128-bit
+// store may land before the store has read them, and hipcc does not pad an
+// asm statement; MI355X hazard rule, cdna_hip_programming.md §5.7)
 __device__ __forceinline__ void st_wt16(double *p, dbl2 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 // eight 16-byte sc1 loads p[k] -> v[k], waited
 __device__ __forceinline__ void ld_wt16x8(const double *const p[8], dbl2 v[8]) {
@@ -690,6 +779,7 @@ struct DagArgs {
   double *Ld;                 // [2T][4096]: L_kk then L_kk^{-1}
   double *ltd;                // [T][kLtdSize]: the 16x16 diagonal-block inverses of each L_kk
   const int4 *tasks;
+  const int2 *sub;            // [n_tasks] TRSM fused into a POTRF task: {tile id or -1, late-wait start}
   const int *wait_off;
   const int2 *waits;
   int *counters;              // ready[n_tiles] | applied[n_tiles] | ticket
@@ -724,6 +814,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 4];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);   // [0] ticket, [1] bad, [2] ok, [3] last
+#ifdef ARSLAM_COLX_SEP
+  __shared__ double colx_sep[64];
+#endif
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
   const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
@@ -740,8 +833,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     const int4 task = a.tasks[t];
     DAG_PROGRESS(2, task.x);
     if (a.trace && tid == 0) { a.trace[8L * t] = realtime(); a.trace[8L * t + 3] = blockIdx.x; }
+    const int2 sub = a.sub[t];
     if (tid == 0) {
-      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], a.wait_off[t + 1], a.flag);
+      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], sub.x >= 0 ? sub.y : a.wait_off[t + 1], a.flag);
       if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
       sh[2] = ok;
     }
@@ -778,7 +872,11 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       }
       __syncthreads();
       if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
-      const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid);
+      #ifdef ARSLAM_COLX_SEP
+      const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid, colx_sep);
+#else
+      const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid, X);   // X is free until the inverse
+#endif
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
         int first = 0;
@@ -792,6 +890,22 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       dag_release(tid);
       if (tid == 0) __hip_atomic_fetch_add(ready + task.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 6] = realtime();
+      if (sub.x >= 0) {
+        // fused TRSM of the parent's tile against the L_kk still in LDS
+        if (tid == 0) {
+          const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag);
+          if (!ok2) atomicCAS(a.flag, 0, -(3000000 + t));
+        }
+        __syncthreads();
+        double *Ct = a.S + (long)sub.x * (T64 * T64);
+        load_tile_wt(Ct, X, tid);
+        __syncthreads();
+        blocked_trsm64(X, D, inv, LTd, tid);
+        store_tile_wt(Ct, X, tid, false);
+        dag_release(tid);
+        if (tid == 0) __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
+      }
       blocked_trinv64(D, LTd, X, tid);
       __syncthreads();
       double *Xg = a.Ld + ((long)a.T + k) * T64 * T64;
@@ -1056,7 +1170,7 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
   if (P.n_dag_tasks == 0) return;
   (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2) * sizeof(int), s);
   if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
-  DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_wait_off, P.dag_waits, P.dag_counters,
+  DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
             P.upd_part, P.upd_cnt, flag, progress, trace};
   const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);

@@ -59,7 +59,18 @@ constexpr int kSplitMin = 6;   // k-lists longer than this are split
 // can be ready instead of behind a wave of updates that can wait.  Costs are
 // calibrated on MI355X task traces (tools/dag_critical.py), in microseconds.
 constexpr int kSimWorkers = 512;
-struct DagNode { double est; int type; int idx; int4 task; std::vector<int2> waits; };
+// A POTRF node may also carry the TRSM of the column's first off-diagonal
+// tile (sub = its compact tile id): 'late' waits are those of that TRSM,
+// polled after L_kk is published.
+struct DagNode {
+  double est;
+  int type;
+  int idx;
+  int4 task;
+  std::vector<int2> waits;
+  int sub = -1;
+  std::vector<int2> late;
+};
 
 static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, long nt, const LltPlan &plan) {
   const int n = (int)nodes.size();
@@ -69,6 +80,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
     const int4 t = nodes[v].task;
     if (t.x == 0 || t.x == 1) ready_prod[t.w] = v;
     else by_tile[t.w].push_back({t.z, v});
+    if (nodes[v].sub >= 0) ready_prod[nodes[v].sub] = v;
   }
   auto seq_nodes = [&](int tile, int seq, std::vector<int> &out) {
     for (const auto &sv : by_tile[tile])
@@ -81,7 +93,9 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   for (int v = 0; v < n; ++v) {
     const DagNode &nd = nodes[v];
     pr.clear();
-    for (const int2 &w : nd.waits) {
+    std::vector<int2> all(nd.waits);
+    all.insert(all.end(), nd.late.begin(), nd.late.end());
+    for (const int2 &w : all) {
       if (w.x < nt) {
         if (ready_prod[w.x] >= 0) pr.push_back(ready_prod[w.x]);
       } else if (w.y > 0) {
@@ -98,7 +112,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
     }
     if (nd.task.x == 0) {
       const int nk = nd.task.z >= 0 ? plan.h_items[nd.task.z].z - plan.h_items[nd.task.z].y : 0;
-      cost[v] = 16.0 + 4.0 * nk;
+      cost[v] = 16.0 + 4.0 * nk + (nd.sub >= 0 ? 5.0 : 0.0);
     } else if (nd.task.x == 1) {
       cost[v] = 6.0;
     } else {
@@ -289,20 +303,53 @@ void dag_build(LltPlan &plan) {
       if (!drop[m]) kept.push_back(std::move(nodes[m]));
     nodes.swap(kept);
   }
+  // Fuse the TRSM of each column's first off-diagonal tile (the elimination
+  // tree parent's row) into the column's POTRF task: on a chain of
+  // separator columns, POTRF(k) -> TRSM(parent, k) -> POTRF(parent) is the
+  // critical path, and the fused task solves the tile against the L_kk it
+  // still holds in LDS (no draw, no hand-off, no reload of L_kk).  The
+  // TRSM's own waits become the task's late waits.
+  if (!std::getenv("ARSLAM_NO_TRSM_FUSION")) {   // (debug switch)
+    std::vector<int> trsm_node(nt, -1);
+    for (size_t m = 0; m < nodes.size(); ++m)
+      if (nodes[m].type == 1) trsm_node[nodes[m].task.w] = (int)m;
+    std::vector<char> drop(nodes.size(), 0);
+    for (auto &n : nodes) {
+      if (n.type != 0) continue;
+      const int k = n.task.y;
+      int par = -1;
+      for (int i = k + 1; i < T && par < 0; ++i)
+        if (tid(i, k) >= 0) par = i;
+      if (par < 0) continue;
+      const int m = trsm_node[tid(par, k)];
+      if (m < 0) continue;
+      n.sub = tid(par, k);
+      for (const int2 &x : nodes[m].waits)
+        if (x.x != tid(k, k)) n.late.push_back(x);
+      drop[m] = 1;
+    }
+    std::vector<Node> kept;
+    for (size_t m = 0; m < nodes.size(); ++m)
+      if (!drop[m]) kept.push_back(std::move(nodes[m]));
+    nodes.swap(kept);
+  }
   std::vector<int> order = dag_list_schedule(nodes, nt, plan);
   plan.h_dag_tasks.clear();
   plan.h_dag_waits.clear();
+  plan.h_dag_sub.clear();
   plan.h_dag_wait_off.assign(1, 0);
   for (int o : order) {
     plan.h_dag_tasks.push_back(nodes[o].task);
     plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].waits.begin(), nodes[o].waits.end());
+    plan.h_dag_sub.push_back(make_int2(nodes[o].sub, (int)plan.h_dag_waits.size()));
+    plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].late.begin(), nodes[o].late.end());
     plan.h_dag_wait_off.push_back((int)plan.h_dag_waits.size());
   }
   plan.n_dag_tasks = (long)plan.h_dag_tasks.size();
   long n_potrf = 0, n_trsm = 0;
-  for (const int4 &t : plan.h_dag_tasks) {
-    n_potrf += t.x == 0;
-    n_trsm += t.x == 1;
+  for (size_t t = 0; t < plan.h_dag_tasks.size(); ++t) {
+    n_potrf += plan.h_dag_tasks[t].x == 0;
+    n_trsm += plan.h_dag_tasks[t].x == 1 || plan.h_dag_sub[t].x >= 0;
   }
   const double t3 = 64.0 * 64.0 * 64.0;
   plan.total_factor_flops = plan.total_upd_flops + n_potrf * (t3 / 3.0 + t3 / 3.0) + n_trsm * 2.0 * t3;
@@ -455,6 +502,7 @@ bool dag_check(const LltPlan &plan) {
     const int4 task = plan.h_dag_tasks[t];
     if (task.x == 0 || task.x == 1) {
       cnt[task.w] = 1;
+      if (plan.h_dag_sub[t].x >= 0) cnt[plan.h_dag_sub[t].x] = 1;
       continue;
     }
     const int sid = plan.h_items[task.y].w;
@@ -495,6 +543,7 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
         const int4 task = plan.h_dag_tasks[w.t];
         if (task.x != 2) {
           cnt[task.w] = 1;
+          if (plan.h_dag_sub[w.t].x >= 0) cnt[plan.h_dag_sub[w.t].x] = 1;
           w.phase = 0;
           ++finished;
           continue;
@@ -541,6 +590,7 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   plan.dag_tasks = upload(plan.h_dag_tasks, s);
   plan.dag_wait_off = upload(plan.h_dag_wait_off, s);
   plan.dag_waits = upload(plan.h_dag_waits, s);
+  plan.dag_sub = upload(plan.h_dag_sub, s);
   check(hipMalloc(&plan.dag_counters, (2 * (size_t)plan.n_tiles + 2) * sizeof(int)), "hipMalloc(dag_counters)");
   check(hipStreamSynchronize(s), "plan sync");
 }
@@ -556,7 +606,7 @@ void llt_plan_free(LltPlan &plan) {
                   (void *)plan.upd_cnt, (void *)plan.upd_part, (void *)plan.bs_cols, (void *)plan.bs_gather,
                   (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.tile_id, (void *)plan.ldiag,
                   (void *)plan.dag_tasks, (void *)plan.dag_wait_off, (void *)plan.dag_waits,
-                  (void *)plan.dag_counters})
+                  (void *)plan.dag_sub, (void *)plan.dag_counters})
     if (p) (void)hipFree(p);
   plan = LltPlan{};
 }

@@ -113,8 +113,12 @@ struct LltPlan {
   // persistent task-graph executor (launch_dense_llt_dag): tasks in ticket
   // order {type, a, b, c} (0 POTRF k; 1 TRSM i,k; 2 update item a, level
   // sequence b, target tile c), each with a list of {counter, value} waits;
-  // counters = [ready(n_tiles) | applied(n_tiles) | ticket]
+  // counters = [ready(n_tiles) | applied(n_tiles) | ticket].  dag_sub[t] =
+  // {tile id of the TRSM fused into POTRF task t or -1, index in dag_waits
+  // where that TRSM's late waits begin}.
   int4 *dag_tasks = nullptr;
+  int2 *dag_sub = nullptr;
+  std::vector<int2> h_dag_sub;
   int *dag_wait_off = nullptr;
   int2 *dag_waits = nullptr;
   int *dag_counters = nullptr;

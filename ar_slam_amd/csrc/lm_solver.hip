@@ -547,6 +547,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
             std::fwrite(&nw, 8, 1, f);
             std::fwrite(plan.h_dag_wait_off.data(), sizeof(int), n + 1, f);
             std::fwrite(plan.h_dag_waits.data(), sizeof(int2), nw, f);
+            std::fwrite(plan.h_dag_sub.data(), sizeof(int2), n, f);   // fused TRSM tiles
             std::fclose(f);
           }
           dag_traced = true;
@@ -557,6 +558,27 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           HIP_CHECK(hipEventRecord(upd_timing.ev[2 * upd_timing.used + 1], stream));
           upd_timing.used++;
           upd_timing.flops += plan.total_factor_flops;
+        }
+        static const char *hash_path = std::getenv("ARSLAM_FACTOR_HASH");   // debug: per-tile factor hashes
+        if (hash_path) {
+          std::vector<unsigned long long> h((size_t)plan.n_tiles * 4096), ld((size_t)plan.T * 4096);
+          HIP_CHECK(hipMemcpyAsync(h.data(), d_S.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
+          HIP_CHECK(hipMemcpyAsync(ld.data(), plan.ldiag, ld.size() * 8, hipMemcpyDeviceToHost, stream));
+          HIP_CHECK(hipStreamSynchronize(stream));
+          if (FILE *f = std::fopen(hash_path, "ab")) {
+            const long nt = plan.n_tiles, T = plan.T;
+            std::fwrite(&nt, 8, 1, f);
+            std::fwrite(&T, 8, 1, f);
+            std::vector<long> tmap(plan.h_tile_id.begin(), plan.h_tile_id.end());
+            std::fwrite(tmap.data(), 8, tmap.size(), f);
+            for (const auto *v : {&h, &ld})
+              for (size_t t = 0; t < v->size() / 4096; ++t) {
+                unsigned long long x = 1469598103934665603ull;
+                for (int e = 0; e < 4096; ++e) x = (x ^ (*v)[t * 4096 + e]) * 1099511628211ull;
+                std::fwrite(&x, 8, 1, f);
+              }
+            std::fclose(f);
+          }
         }
       } else {
         arslam::launch_dense_llt(plan, d_S.p, d_flag.p, stream, opt.kernel_timing ? &upd_timing : nullptr);

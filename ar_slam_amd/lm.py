@@ -24,7 +24,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libarslam_lm.so")
+LIB_PATH = os.environ.get("ARSLAM_LIB") or os.path.join(HERE, "libarslam_lm.so")   # (override: variant builds)
 MAX_ITERS = 1024
 COMM_ID_BYTES = 128
 

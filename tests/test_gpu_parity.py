@@ -223,3 +223,20 @@ def test_persistent_executor_matches_level_launches(lm, oracle, name, ordering):
     cd = [it["cost"] for it in dag[3]["iterations"]]
     assert len(cl) == len(cd)
     np.testing.assert_allclose(cd, cl, rtol=1e-10)
+
+
+def test_cfg3_repeated_solves_are_bit_identical(lm):
+    """The device path is deterministic (no atomics in any sum that reaches the step, fixed
+    summation orders in the task-graph factorization): repeated solves of the headline
+    workload from the same HBM-resident state give bit-identical traces and parameters.
+    A data race in the persistent executor shows up here as a differing bit."""
+    g = synth.config_graph("cfg3")
+    rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
+    ref = rp.solve()
+    tags = rp.tag.copy()
+    for _ in range(3):
+        s = rp.solve()
+        assert [i["cost"] for i in s["iterations"]] == [i["cost"] for i in ref["iterations"]]
+        assert [i["trust_region_radius"] for i in s["iterations"]] == \
+            [i["trust_region_radius"] for i in ref["iterations"]]
+        assert np.array_equal(rp.tag, tags)

@@ -25,9 +25,12 @@ tr = np.frombuffer(f.read(64 * n), np.uint64).reshape(n, 8).astype(np.int64)
 nw = int(np.frombuffer(f.read(8), np.int64)[0])
 woff = np.frombuffer(f.read(4 * (n + 1)), np.int32)
 waits = np.frombuffer(f.read(8 * nw), np.int32).reshape(nw, 2)
+rest = f.read(8 * n)
+sub = np.frombuffer(rest, np.int32).reshape(n, 2) if len(rest) == 8 * n else np.full((n, 2), -1, np.int32)
 t0 = tr[:, 0].min()
 us = lambda j: (tr[:, j] - t0) / 100.0   # s_memrealtime is 100 MHz
 draw, ready, end = us(0), us(1), us(2)
+pub_kk, pub_sub = us(6), us(7)   # POTRF: L_kk published; fused TRSM tile published
 n_tiles = int(tasks[:, 3].max()) + 1
 print(f"tasks {n}, makespan {end.max():.1f} us, workgroups {len(np.unique(tr[:, 3]))}")
 
@@ -37,21 +40,28 @@ for t in range(n):
     ty, y, z, w = tasks[t]
     if ty in (0, 1):
         ready_prod[int(w)] = t
+        if sub[t, 0] >= 0:
+            ready_prod[int(sub[t, 0])] = t
     else:
         applied_prod[int(w)].append((int(z), t))
 
 
 def producers(t):
+    """(producer task, time its awaited result was published)"""
     ps = []
     for c, v in waits[woff[t]:woff[t + 1]]:
         if c < n_tiles:
             if int(c) in ready_prod:
-                ps.append(ready_prod[int(c)])
+                u = ready_prod[int(c)]
+                if tasks[u, 0] == 0:
+                    ps.append((u, pub_sub[u] if sub[u, 0] == c else pub_kk[u]))
+                else:
+                    ps.append((u, end[u]))
         else:
-            ps += [u for s, u in applied_prod.get(int(c) - n_tiles, []) if s < v]
+            ps += [(u, end[u]) for s, u in applied_prod.get(int(c) - n_tiles, []) if s < v]
     ty, y, z, w = tasks[t]
     if ty == 2:   # in-order apply on the target
-        ps += [u for s, u in applied_prod.get(int(w), []) if s < z]
+        ps += [(u, end[u]) for s, u in applied_prod.get(int(w), []) if s < z]
     return ps
 
 
@@ -62,7 +72,7 @@ while True:
     ps = producers(t)
     if not ps:
         break
-    t = max(ps, key=lambda p: end[p])
+    t = max(ps, key=lambda p: p[1])[0]
 path.reverse()
 names = ["POTRF", "TRSM", "UPD"]
 acc = collections.defaultdict(float)
@@ -87,7 +97,7 @@ upd_on_path = [t for t in path if tasks[t, 0] == 2]
 busy = np.sum(end - ready)
 wgs = len(np.unique(tr[:, 3]))
 print(f"busy {busy:.0f} us over {wgs} workgroups = {busy / wgs / end.max():.1%} of the makespan")
-print("path (last 30):")
-for t in path[-30:]:
+print("path:")
+for t in path:
     ty, y, z, w = tasks[t]
     print(f"  {names[ty]:5s} ({y:5d},{z:5d}) draw {draw[t]:8.1f} ready {ready[t]:8.1f} end {end[t]:8.1f}")

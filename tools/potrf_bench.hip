@@ -16,6 +16,7 @@ __global__ __launch_bounds__(256) void k_bench(const double *A, int reps, unsign
   __shared__ __attribute__((aligned(16))) double D[T64 * LQ];
   __shared__ double inv[T64];
   __shared__ __attribute__((aligned(16))) double LTd[4 * 16 * LI];
+  __shared__ double colx[64];
   __shared__ int bad;
   const int tid = threadIdx.x;
   if (prio) __builtin_amdgcn_s_setprio(3);
@@ -25,7 +26,7 @@ __global__ __launch_bounds__(256) void k_bench(const double *A, int reps, unsign
       D[(e >> 6) * LQ + (e & 63)] = (e & 63) <= (e >> 6) ? A[e] : -7.0;
     __syncthreads();
     const unsigned long long t0 = realtime();
-    blocked_potrf64(D, inv, LTd, &bad, tid);
+    blocked_potrf64(D, inv, LTd, &bad, tid, colx);
     __syncthreads();
     const unsigned long long t1 = realtime();
     tot += t1 - t0;
