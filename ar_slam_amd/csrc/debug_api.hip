@@ -177,6 +177,9 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
           std::fwrite(&n, 8, 1, f);
           std::fwrite(&nw, 8, 1, f);
           std::fwrite(&T, 8, 1, f);
+          const long ni = (long)plan.h_items.size(), ntg = (long)plan.h_targets.size();
+          std::fwrite(&ni, 8, 1, f);
+          std::fwrite(&ntg, 8, 1, f);
           std::fwrite(plan.h_dag_tasks.data(), sizeof(int4), n, f);
           std::fwrite(plan.h_dag_wait_off.data(), sizeof(int), n + 1, f);
           std::fwrite(plan.h_dag_waits.data(), sizeof(int2), nw, f);
@@ -184,6 +187,8 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
           std::fwrite(plan.h_tile_id.data(), sizeof(int), (size_t)T * T, f);
           std::fwrite(plan.h_items.data(), sizeof(int4), plan.h_items.size(), f);
           std::fwrite(plan.h_targets.data(), sizeof(int2), plan.h_targets.size(), f);
+          std::fwrite(plan.h_dag_cont.data(), sizeof(int), n, f);
+          std::fwrite(plan.h_dag_maxdep.data(), sizeof(int), n, f);
           std::fclose(f);
         }
       }

@@ -630,7 +630,8 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
 //               target's earlier levels, so the summation order is fixed.
 // ---------------------------------------------------------------------------
 constexpr int kLtdSize = 4 * 16 * LI;   // 1152 doubles
-constexpr long kSpinCap = 1L << 16;   // ~0.1 s of polling: far beyond any legitimate wait
+constexpr long kSpinCap = 1L << 16;
+constexpr int kMaxOwed = 8;           // continuation targets one workgroup may owe at once   // ~0.1 s of polling: far beyond any legitimate wait
 
 // Poll a dependency counter with an atomic read-modify-write (+0): counters
 // are advanced by device-scope atomic adds, and an RMW is performed where
@@ -730,16 +731,24 @@ __device__ __forceinline__ void store_tile_wt(double *__restrict__ g, const doub
   }
 }
 
-// thread 0: spin until counter[idx] >= val for every wait; false on timeout,
+// wave 0: spin until counter[idx] >= val for every wait; false on timeout,
 // or at once when another workgroup already timed out (flag < 0), so a
-// broken graph drains in one spin cap instead of one per task
-__device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag) {
-  for (int w = w0; w < w1; ++w) {
-    const int2 cv = waits[w];
+// broken graph drains in one spin cap instead of one per task.  Lane q polls
+// wait q (64 at a time), so a task's counters are read in one round trip, not
+// one after another.
+__device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag, int lane) {
+  for (int base = w0; base < w1; base += 64) {
+    const int w = base + lane;
+    const bool mine = w < w1;
+    const int2 cv = mine ? waits[w] : make_int2(0, 0);
     long spins = 0;
-    while (ld_acquire_relaxed(counters + cv.x) < cv.y) {
+    for (;;) {
+      // (every lane re-polls each round: no loop-carried per-lane state)
+      const int got = mine ? ld_acquire_relaxed(counters + cv.x) : 0;
+      if (__builtin_amdgcn_ballot_w64(mine && got < cv.y) == 0) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(flag) < 0)) return false;
+      if (++spins > kSpinCap) return false;
+      if ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0) return false;
     }
   }
   return true;
@@ -780,6 +789,9 @@ struct DagArgs {
   double *ltd;                // [T][kLtdSize]: the 16x16 diagonal-block inverses of each L_kk
   const int4 *tasks;
   const int2 *sub;            // [n_tasks] TRSM fused into a POTRF task: {tile id or -1, late-wait start}
+  const int *cont;            // [n_tasks] POTRF task the same workgroup may continue with (or -1)
+  const int *maxdep;          // [n_tasks] continuation targets: largest ticket they wait on; else -1
+  int *claimed;               // [n_tasks] continuation targets: claimed by the predecessor or the drawer
   const int *wait_off;
   const int2 *waits;
   int *counters;              // ready[n_tiles] | applied[n_tiles] | ticket
@@ -814,19 +826,28 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 4];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);   // [0] ticket, [1] bad, [2] ok, [3] last
-#ifdef ARSLAM_COLX_SEP
-  __shared__ double colx_sep[64];
-#endif
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
   const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
   const int li = lane & 15, lk = lane >> 4;
   int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.counters + 2 * a.n_tiles;
+  // Continuation targets stay ordinary tickets with a claim flag.  The
+  // predecessor's workgroup claims its target (before publishing the tile the
+  // target waits for, so it wins whenever it claims) if every task the target
+  // waits on has been drawn -- then the target only waits on running tasks --
+  // and runs it at once, the folded tile still in LDS.  Otherwise the
+  // workgroup that drew the target claims and runs it once its waits are met.
+  int next = -1;
   for (;;) {
-    if (tid == 0) sh[0] = atomicAdd(ticket, 1);
-    __syncthreads();
-    const int t = sh[0];
-    __syncthreads();
+    const bool cont = next >= 0;
+    if (!cont) {
+      if (tid == 0) sh[0] = atomicAdd(ticket, 1);
+      __syncthreads();
+      next = sh[0];
+      __syncthreads();
+    }
+    const int t = next;
+    next = -1;
     DAG_PROGRESS(0, t);
     DAG_PROGRESS(1, 1);
     if (t >= a.n_tasks) break;
@@ -834,12 +855,17 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     DAG_PROGRESS(2, task.x);
     if (a.trace && tid == 0) { a.trace[8L * t] = realtime(); a.trace[8L * t + 3] = blockIdx.x; }
     const int2 sub = a.sub[t];
-    if (tid == 0) {
-      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], sub.x >= 0 ? sub.y : a.wait_off[t + 1], a.flag);
-      if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
-      sh[2] = ok;
+    if (w == 0) {
+      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], sub.x >= 0 ? sub.y : a.wait_off[t + 1], a.flag,
+                               lane);
+      if (lane == 0) {
+        if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
+        // a drawn continuation target: run it only if its predecessor did not claim it
+        sh[2] = (cont || a.maxdep[t] < 0 || atomicCAS(a.claimed + t, 0, 1) == 0) ? 1 : 0;
+      }
     }
     __syncthreads();
+    if (!sh[2]) continue;
     DAG_PROGRESS(1, 2);
     if (a.trace && tid == 0) a.trace[8L * t + 1] = realtime();
     // the chain tasks (POTRF, TRSM) win SIMD arbitration over co-resident updates
@@ -852,31 +878,42 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
         const int4 it = a.items[task.z];
         dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-        for (int q = it.y; q < it.z; ++q) {
+        const bool staged = false;
+        if (cont) {
+          // continuation: the fold's one column L_kj is the tile the previous
+          // task just solved, still in X
+          gemm64_nt(X, X, tid, acc);
+          if (!staged) {
+            __syncthreads();
+            load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), X, tid);
+          }
+        }
+        for (int q = cont ? it.z : it.y; q < it.z; ++q) {
           if (q > it.y) __syncthreads();
           load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, a.ks[q]), D, tid);
           __syncthreads();
           gemm64_nt(D, D, tid, acc);
         }
-        __syncthreads();
-        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), D, tid);
+        if (!cont) {
+          __syncthreads();
+          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), X, tid);
+        }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
 #pragma unroll
-          for (int reg = 0; reg < 4; ++reg) D[(rb + lk + 4 * reg) * LQ + cb + li] -= acc[q][reg];
+          for (int reg = 0; reg < 4; ++reg) {
+            const int e = (rb + lk + 4 * reg) * LQ + cb + li;
+            D[e] = (staged ? D[e] : X[e]) - acc[q][reg];
+          }
         }
       } else {
         load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), D, tid);
       }
       __syncthreads();
       if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
-      #ifdef ARSLAM_COLX_SEP
-      const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid, colx_sep);
-#else
-      const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid, X);   // X is free until the inverse
-#endif
+            const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid, X);   // X is free until the fused TRSM
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
         int first = 0;
@@ -892,20 +929,50 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       if (a.trace && tid == 0) a.trace[8L * t + 6] = realtime();
       if (sub.x >= 0) {
         // fused TRSM of the parent's tile against the L_kk still in LDS
-        if (tid == 0) {
-          const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag);
-          if (!ok2) atomicCAS(a.flag, 0, -(3000000 + t));
+        if (w == 0) {
+          const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane);
+          if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
         }
         __syncthreads();
+        const int c = a.cont[t];
         double *Ct = a.S + (long)sub.x * (T64 * T64);
         load_tile_wt(Ct, X, tid);
         __syncthreads();
         blocked_trsm64(X, D, inv, LTd, tid);
         store_tile_wt(Ct, X, tid, false);
         dag_release(tid);
-        if (tid == 0) __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+          // claim the continuation target first: its drawer waits for this
+          // tile, so it cannot have claimed it yet
+          sh[4] = (c >= 0 && ld_acquire_relaxed(ticket) > a.maxdep[c] && atomicCAS(a.claimed + c, 0, 1) == 0) ? c
+                                                                                                            : -1;
+          __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
+        __syncthreads();
+        next = sh[4];
       }
+    } else if (task.x == 3) {
+      // ---- INV k: L_kk^{-1} for the backward solve (off the critical chain) ----
+      const int k = task.y;
+      load_tile_wt(a.Ld + (long)k * T64 * T64, D, tid);
+      {
+        const double *ltd_g = a.ltd + (long)k * kLtdSize;
+        const double *p8[8];
+        dbl2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = tid + 256 * u;
+          p8[u] = ltd_g + 2 * (e < kLtdSize / 2 ? e : 0);
+        }
+        ld_wt16x8(p8, v);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int e = tid + 256 * u;
+          if (e < kLtdSize / 2) *reinterpret_cast<dbl2 *>(LTd + 2 * e) = v[u];
+        }
+      }
+      __syncthreads();
       blocked_trinv64(D, LTd, X, tid);
       __syncthreads();
       double *Xg = a.Ld + ((long)a.T + k) * T64 * T64;
@@ -1169,8 +1236,10 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
                           unsigned long long *trace) {
   if (P.n_dag_tasks == 0) return;
   (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2) * sizeof(int), s);
+  (void)hipMemsetAsync(P.dag_claimed, 0, (size_t)P.n_dag_tasks * sizeof(int), s);
   if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
-  DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_wait_off, P.dag_waits, P.dag_counters,
+  DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
+            P.dag_maxdep, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
             P.upd_part, P.upd_cnt, flag, progress, trace};
   const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);

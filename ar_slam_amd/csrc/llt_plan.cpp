@@ -79,7 +79,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   for (int v = 0; v < n; ++v) {
     const int4 t = nodes[v].task;
     if (t.x == 0 || t.x == 1) ready_prod[t.w] = v;
-    else by_tile[t.w].push_back({t.z, v});
+    else if (t.x == 2) by_tile[t.w].push_back({t.z, v});
     if (nodes[v].sub >= 0) ready_prod[nodes[v].sub] = v;
   }
   auto seq_nodes = [&](int tile, int seq, std::vector<int> &out) {
@@ -115,6 +115,8 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
       cost[v] = 16.0 + 4.0 * nk + (nd.sub >= 0 ? 5.0 : 0.0);
     } else if (nd.task.x == 1) {
       cost[v] = 6.0;
+    } else if (nd.task.x == 3) {
+      cost[v] = 5.0;
     } else {
       const int4 it = plan.h_items[nd.task.y];
       cost[v] = 4.0 + 4.0 * (it.z - it.y);
@@ -333,6 +335,18 @@ void dag_build(LltPlan &plan) {
       if (!drop[m]) kept.push_back(std::move(nodes[m]));
     nodes.swap(kept);
   }
+  // L_kk^{-1} of every column (for the backward solve) as its own task, off
+  // the chain: the POTRF task can go straight on to its parent
+  for (int k = 0; k < T; ++k) {
+    if (tid(k, k) < 0) continue;
+    Node n;
+    n.type = 3;
+    n.idx = k;
+    n.est = 0.0;
+    n.task = make_int4(3, k, 0, tid(k, k));
+    n.waits.push_back(make_int2(tid(k, k), 1));
+    nodes.push_back(std::move(n));
+  }
   std::vector<int> order = dag_list_schedule(nodes, nt, plan);
   plan.h_dag_tasks.clear();
   plan.h_dag_waits.clear();
@@ -346,6 +360,50 @@ void dag_build(LltPlan &plan) {
     plan.h_dag_wait_off.push_back((int)plan.h_dag_waits.size());
   }
   plan.n_dag_tasks = (long)plan.h_dag_tasks.size();
+  // continuation pairs: POTRF(k) with fused TRSM (par, k) -> POTRF(par) when
+  // POTRF(par)'s folded item is that one tile; maxdep = the largest ticket
+  // the target waits on (a producer of any of its counters)
+  {
+    const long n = plan.n_dag_tasks;
+    plan.h_dag_cont.assign(n, -1);
+    plan.h_dag_maxdep.assign(n, -1);
+    std::vector<int> potrf_of(T, -1), ready_tk(nt, -1);
+    std::vector<std::vector<std::pair<int, int>>> apply_tk(nt);   // (seq, ticket) of update items
+    for (long t = 0; t < n; ++t) {
+      const int4 tk = plan.h_dag_tasks[t];
+      if (tk.x == 0) potrf_of[tk.y] = (int)t;
+      if (tk.x == 0 || tk.x == 1) ready_tk[tk.w] = (int)t;
+      if (plan.h_dag_sub[t].x >= 0) ready_tk[plan.h_dag_sub[t].x] = (int)t;
+      if (tk.x == 2) apply_tk[tk.w].push_back({tk.z, (int)t});
+    }
+    for (long t = 0; t < n; ++t) {
+      const int4 tk = plan.h_dag_tasks[t];
+      const int sb = plan.h_dag_sub[t].x;
+      if (tk.x != 0 || sb < 0 || std::getenv("ARSLAM_NO_CONT")) continue;
+      int par = -1;
+      for (int i = tk.y + 1; i < T && par < 0; ++i)
+        if (tid(i, tk.y) == sb) par = i;
+      if (par < 0 || potrf_of[par] < 0) continue;
+      const int c = potrf_of[par];
+      const int4 ct = plan.h_dag_tasks[c];
+      if (ct.z < 0) continue;
+      const int4 it = plan.h_items[ct.z];
+      if (it.z - it.y != 1 || plan.h_ks[it.y] != tk.y) continue;
+      int md = -1;
+      for (int q = plan.h_dag_wait_off[c]; q < plan.h_dag_wait_off[c + 1]; ++q) {
+        const int2 w = plan.h_dag_waits[q];
+        if (w.x < nt) {
+          md = std::max(md, ready_tk[w.x]);
+        } else {
+          for (const auto &sv : apply_tk[w.x - nt])
+            if (sv.first < w.y) md = std::max(md, sv.second);
+        }
+      }
+      if (md < 0 || md >= c) continue;   // (topological order: cannot happen)
+      plan.h_dag_cont[t] = c;
+      plan.h_dag_maxdep[c] = md;
+    }
+  }
   long n_potrf = 0, n_trsm = 0;
   for (size_t t = 0; t < plan.h_dag_tasks.size(); ++t) {
     n_potrf += plan.h_dag_tasks[t].x == 0;
@@ -500,6 +558,7 @@ bool dag_check(const LltPlan &plan) {
     for (int w = plan.h_dag_wait_off[t]; w < plan.h_dag_wait_off[t + 1]; ++w)
       if (cnt[plan.h_dag_waits[w].x] < plan.h_dag_waits[w].y) return false;
     const int4 task = plan.h_dag_tasks[t];
+    if (task.x == 3) continue;
     if (task.x == 0 || task.x == 1) {
       cnt[task.w] = 1;
       if (plan.h_dag_sub[t].x >= 0) cnt[plan.h_dag_sub[t].x] = 1;
@@ -517,21 +576,45 @@ bool dag_check(const LltPlan &plan) {
 // persistent executor's protocol (draw ticket, static waits, run, split
 // arrival, level-ordered application).  Returns false on a deadlock.
 bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
-  const long nt = plan.n_tiles;
+  const long nt = plan.n_tiles, n = plan.n_dag_tasks;
   std::vector<int> cnt(2 * nt + 1, 0), arrived(plan.h_split.size(), 0);
-  struct W { long t = -1; int phase = 0; };   // 0 draw, 1 wait, 2 apply-wait
+  const bool has_cont = !plan.h_dag_cont.empty();
+  auto maxdep = [&](long t) { return has_cont ? plan.h_dag_maxdep[t] : -1; };
+  std::vector<char> claimed(n, 0);
+  // the persistent kernel's protocol (k_factor_dag): phases 0 pick, 1 wait,
+  // 2 apply-wait.  A finished POTRF claims its continuation target if every
+  // task the target waits on has been drawn, and runs it next; a drawn target
+  // runs only if its predecessor did not claim it.
+  struct W { long t = -1; int phase = 0; long next = -1; bool cont = false; };
   std::vector<W> ws(n_workers);
-  long next = 0, finished = 0;
+  long ticket = 0, finished = 0;
   unsigned rng = seed ? seed : 1u;
   auto rnd = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
-  while (finished < plan.n_dag_tasks) {
+  auto done = [&](W &w) {
+    ++finished;
+    const int c = has_cont ? plan.h_dag_cont[w.t] : -1;
+    w.next = -1;
+    if (c >= 0 && ticket > maxdep(c) && !claimed[c]) {
+      claimed[c] = 1;
+      w.next = c;
+    }
+    w.phase = 0;
+  };
+  while (finished < n) {
     bool progressed = false;
     const int start = (int)(rnd() % (unsigned)n_workers);
     for (int m = 0; m < n_workers && !progressed; ++m) {
       W &w = ws[(start + m) % n_workers];
       if (w.phase == 0) {
-        if (next >= plan.n_dag_tasks) continue;
-        w.t = next++;
+        if (w.next >= 0) {
+          w.t = w.next;
+          w.next = -1;
+          w.cont = true;
+        } else {
+          if (ticket >= n) continue;
+          w.t = ticket++;
+          w.cont = false;
+        }
         w.phase = 1;
         progressed = true;
       } else if (w.phase == 1) {
@@ -540,28 +623,30 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
           ok = cnt[plan.h_dag_waits[q].x] >= plan.h_dag_waits[q].y;
         if (!ok) continue;
         progressed = true;
+        if (!w.cont && maxdep(w.t) >= 0) {
+          if (claimed[w.t]) {   // its predecessor runs it
+            w.phase = 0;
+            continue;
+          }
+          claimed[w.t] = 1;
+        }
         const int4 task = plan.h_dag_tasks[w.t];
+        if (task.x == 3) { done(w); continue; }
         if (task.x != 2) {
           cnt[task.w] = 1;
           if (plan.h_dag_sub[w.t].x >= 0) cnt[plan.h_dag_sub[w.t].x] = 1;
-          w.phase = 0;
-          ++finished;
+          done(w);
           continue;
         }
         const int sid = plan.h_items[task.y].w;
-        if (sid >= 0 && ++arrived[sid >> 8] < plan.h_split[sid >> 8].x) {
-          w.phase = 0;
-          ++finished;
-          continue;
-        }
+        if (sid >= 0 && ++arrived[sid >> 8] < plan.h_split[sid >> 8].x) { done(w); continue; }
         w.phase = 2;
       } else {
         const int4 task = plan.h_dag_tasks[w.t];
         if (cnt[nt + task.w] < task.z) continue;
         cnt[nt + task.w]++;
         progressed = true;
-        w.phase = 0;
-        ++finished;
+        done(w);
       }
     }
     if (!progressed) return false;
@@ -591,6 +676,9 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   plan.dag_wait_off = upload(plan.h_dag_wait_off, s);
   plan.dag_waits = upload(plan.h_dag_waits, s);
   plan.dag_sub = upload(plan.h_dag_sub, s);
+  plan.dag_cont = upload(plan.h_dag_cont, s);
+  plan.dag_maxdep = upload(plan.h_dag_maxdep, s);
+  check(hipMalloc(&plan.dag_claimed, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int)), "hipMalloc(dag_claimed)");
   check(hipMalloc(&plan.dag_counters, (2 * (size_t)plan.n_tiles + 2) * sizeof(int)), "hipMalloc(dag_counters)");
   check(hipStreamSynchronize(s), "plan sync");
 }
@@ -606,7 +694,8 @@ void llt_plan_free(LltPlan &plan) {
                   (void *)plan.upd_cnt, (void *)plan.upd_part, (void *)plan.bs_cols, (void *)plan.bs_gather,
                   (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.tile_id, (void *)plan.ldiag,
                   (void *)plan.dag_tasks, (void *)plan.dag_wait_off, (void *)plan.dag_waits,
-                  (void *)plan.dag_sub, (void *)plan.dag_counters})
+                  (void *)plan.dag_sub, (void *)plan.dag_cont, (void *)plan.dag_maxdep, (void *)plan.dag_claimed,
+                  (void *)plan.dag_counters})
     if (p) (void)hipFree(p);
   plan = LltPlan{};
 }

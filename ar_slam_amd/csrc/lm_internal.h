@@ -119,6 +119,12 @@ struct LltPlan {
   int4 *dag_tasks = nullptr;
   int2 *dag_sub = nullptr;
   std::vector<int2> h_dag_sub;
+  // dag_cont[t]: the POTRF task the workgroup finishing POTRF task t may run
+  // next (the parent column, whose fold is exactly the tile t solved) or -1;
+  // dag_maxdep[t]: for such targets the largest ticket t waits on, else -1;
+  // dag_claimed[t]: taken by the predecessor's workgroup or by the drawer
+  int *dag_cont = nullptr, *dag_maxdep = nullptr, *dag_claimed = nullptr;
+  std::vector<int> h_dag_cont, h_dag_maxdep;
   int *dag_wait_off = nullptr;
   int2 *dag_waits = nullptr;
   int *dag_counters = nullptr;

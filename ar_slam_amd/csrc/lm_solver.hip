@@ -612,6 +612,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     timing_collect();
 
     const bool lin_fail = flag != 0;
+    if (lin_fail && std::getenv("ARSLAM_DEBUG_FLAG"))   // debug: factorization failure code
+      std::fprintf(stderr, "arslam: factorization flag %d at iteration %d\n", flag, it.iteration);
     const bool ybad = red[arslam::P_YBAD] != 0.0 || red[arslam::NPART + 1] != 0.0;
     const double model_cost_change = red[arslam::P_MODEL];
     const bool valid = !lin_fail && !ybad && model_cost_change > 0.0;

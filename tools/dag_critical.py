@@ -74,7 +74,7 @@ while True:
         break
     t = max(ps, key=lambda p: p[1])[0]
 path.reverse()
-names = ["POTRF", "TRSM", "UPD"]
+names = ["POTRF", "TRSM", "UPD", "INV"]
 acc = collections.defaultdict(float)
 prev_end = draw[path[0]]
 for t in path:

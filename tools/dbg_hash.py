@@ -12,7 +12,10 @@ os.environ["ARSLAM_FACTOR_HASH"] = path
 from ar_slam_amd import lm, synth
 g = synth.config_graph(sys.argv[1] if len(sys.argv) > 1 else "cfg3")
 rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
-runs = [rp.solve() for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 4)]
+runs = []
+for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 4):
+    runs.append(rp.solve())
+    print("solve", len(runs), runs[-1]["num_linear_solves"], runs[-1]["termination"], flush=True)
 raw = np.fromfile(path, np.uint64)
 recs, o = [], 0
 while o < raw.size:
