@@ -124,7 +124,8 @@ extern "C" int arslam_debug_dense_llt_ex(long n, double *A, const double *b, dou
   }
   if (executor == 1) arslam::launch_dense_llt_dag(plan, d_S, d_flag, 0, grid);
   else arslam::launch_dense_llt(plan, d_S, d_flag, 0);
-  arslam::launch_dense_back_solve(plan, d_S, n, d_z, d_y, d_flag, 0);
+  if (executor == 1) arslam::launch_dense_back_solve_dag(plan, d_S, n, d_y, d_flag, 0, grid);
+  else arslam::launch_dense_back_solve(plan, d_S, n, d_z, d_y, d_flag, 0);
   arslam::launch_scatter_diag(plan, d_S, 0);
   DBG_CHECK(hipGetLastError());
   DBG_CHECK(hipDeviceSynchronize());

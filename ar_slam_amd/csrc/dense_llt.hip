@@ -630,8 +630,7 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
 //               target's earlier levels, so the summation order is fixed.
 // ---------------------------------------------------------------------------
 constexpr int kLtdSize = 4 * 16 * LI;   // 1152 doubles
-constexpr long kSpinCap = 1L << 16;
-constexpr int kMaxOwed = 8;           // continuation targets one workgroup may owe at once   // ~0.1 s of polling: far beyond any legitimate wait
+constexpr long kSpinCap = 1L << 16;   // ~0.1 s of polling: far beyond any legitimate wait
 
 // Poll a dependency counter with an atomic read-modify-write (+0): counters
 // are advanced by device-scope atomic adds, and an RMW is performed where
@@ -1193,6 +1192,100 @@ __global__ __launch_bounds__(256) void k_bs_solve(const double *__restrict__ Xin
   if (w == 0 && row0 + lane < nR) yF[row0 + lane] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// Persistent backward solve L^T y = z (the launch-per-level pair above as one
+// launch).  Ticket b takes column bs_cols[b]; the columns are root level
+// first, so every ancestor a column waits for holds an earlier ticket and was
+// drawn by a running workgroup (deadlock-free for any grid).  A column task:
+//   z_k      from the rhs row (as k_init_z);
+//   gathers  nearest ancestor LAST (ancestors finish root-first, so all but
+//            the parent's partial are summed while the parent is still being
+//            solved): L_ik is prefetched into registers before the wait on
+//            done[i], y_i is an sc1 load (written this launch), and the
+//            partials are summed in this fixed order, so every rank of a
+//            sharded solve computes the same bits;
+//   solve    y_k = L_kk^{-T}(z_k - acc) with the prefetched inverse X_kk;
+//            wave 0 stores y_k write-through, drains, bumps done[k].
+__global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S, const int *__restrict__ tid_map,
+                                                    int T, const double *__restrict__ Ld, long nR,
+                                                    const int *__restrict__ cols, const int2 *__restrict__ gather,
+                                                    const int *__restrict__ gbeg, int ncols, double *yF,
+                                                    int *counters, int *flag) {
+  __shared__ double red[4][T64];
+  __shared__ double ys[T64];
+  __shared__ int sh[2];
+  if (*flag) return;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  int *done = counters, *ticket = counters + T;
+  const double *Xinv = Ld + (long)T * T64 * T64;
+  const long kr = nR / T64;
+  for (;;) {
+    if (tid == 0) sh[0] = atomicAdd(ticket, 1);
+    __syncthreads();
+    const int b = sh[0];
+    if (b >= ncols) break;
+    const int k = cols[b];
+    const long row0 = (long)k * T64;
+    // the inverse's rows 16w..16w+15 for lane's column, in flight during the gathers
+    const double *X = Xinv + (long)k * T64 * T64;
+    double xv[16];
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) xv[rr] = X[(16 * w + rr) * T64 + lane];
+    double acc = 0.0;   // wave 0: lane's row of sum_i L_ik^T y_i
+    bool ok = true;
+    for (int g = gbeg[b + 1] - 1; g >= gbeg[b]; --g) {
+      const int i = gather[g].x;
+      const long ri = (long)i * T64;
+      const double *Lik = tile_ptr(S, tid_map, T, i, k);
+      double lv[16];   // rows w, w+4, ..., lane's column
+#pragma unroll
+      for (int m = 0; m < 16; ++m) lv[m] = Lik[(w + 4 * m) * T64 + lane];
+      if (w == 0) {
+        if (lane == 0) {
+          long spins = 0;
+          while (ld_acquire_relaxed(done + i) < 1) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(flag) != 0)) {
+              atomicCAS(flag, 0, -(4000000 + b));
+              ok = false;
+              break;
+            }
+          }
+          sh[1] = ok;
+        }
+        asm volatile("" ::: "memory");   // y_i is loaded after the wait
+        ys[lane] = (ri + lane < nR) ? ld_wt(yF + ri + lane) : 0.0;
+      }
+      __syncthreads();
+      if (!sh[1]) break;
+      double s = 0.0;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) s += lv[m] * ys[w + 4 * m];
+      red[w][lane] = s;
+      __syncthreads();
+      if (w == 0) acc += ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    }
+    if (w == 0) {
+      double z = 0.0;
+      if (row0 + lane < nR) {
+        if (k == kr) z = Ld[kr * T64 * T64 + (nR - kr * T64) * T64 + lane];
+        else z = tile_ptr(S, tid_map, T, (int)kr, k)[(nR - kr * T64) * T64 + lane];
+      }
+      ys[lane] = (row0 + lane < nR) ? z - acc : 0.0;
+    }
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) s += xv[rr] * ys[16 * w + rr];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0) {
+      if (row0 + lane < nR) st_wt(yF + row0 + lane, ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(done + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // tests only: copy the diagonal factors L_kk into their S tiles
 __global__ void k_scatter_diag(double *__restrict__ S, const int *__restrict__ tid_map, int T,
                                const double *__restrict__ Ld) {
@@ -1244,6 +1337,16 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
             P.upd_part, P.upd_cnt, flag, progress, trace};
   const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
+}
+
+void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, double *yF, int *flag,
+                                 hipStream_t s, int n_workgroups) {
+  const int ncols = (int)P.h_bcols.size();
+  if (ncols == 0) return;
+  (void)hipMemsetAsync(P.bs_counters, 0, ((size_t)P.T + 1) * sizeof(int), s);
+  const int grid = std::min(n_workgroups, ncols);
+  hipLaunchKernelGGL(k_bsolve_dag, dim3((unsigned)grid), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag, nR, P.bs_cols,
+                     P.bs_gather, P.bs_gbeg, ncols, yF, P.bs_counters, flag);
 }
 
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,

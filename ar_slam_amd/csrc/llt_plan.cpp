@@ -669,6 +669,7 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   plan.bs_gather = upload(plan.h_gather, s);
   plan.bs_gbeg = upload(plan.h_gbeg, s);
   check(hipMalloc(&plan.bs_part, std::max<size_t>(plan.h_gather.size(), 1) * 64 * sizeof(double)), "hipMalloc(bs_part)");
+  check(hipMalloc(&plan.bs_counters, ((size_t)T + 1) * sizeof(int)), "hipMalloc(bs_counters)");
   plan.tile_id = upload(plan.h_tile_id, s);
   // L_kk, L_kk^{-1}, and the 16x16 block inverses (4 x 16 x 18) of each column
   check(hipMalloc(&plan.ldiag, ((size_t)2 * T * 64 * 64 + (size_t)T * 1152) * sizeof(double)), "hipMalloc(ldiag)");
@@ -692,7 +693,7 @@ void llt_plan_free(LltPlan &plan) {
   for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
                   (void *)plan.upd_ks, (void *)plan.upd_items, (void *)plan.upd_split,
                   (void *)plan.upd_cnt, (void *)plan.upd_part, (void *)plan.bs_cols, (void *)plan.bs_gather,
-                  (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.tile_id, (void *)plan.ldiag,
+                  (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.bs_counters, (void *)plan.tile_id, (void *)plan.ldiag,
                   (void *)plan.dag_tasks, (void *)plan.dag_wait_off, (void *)plan.dag_waits,
                   (void *)plan.dag_sub, (void *)plan.dag_cont, (void *)plan.dag_maxdep, (void *)plan.dag_claimed,
                   (void *)plan.dag_counters})

@@ -100,6 +100,7 @@ struct LltPlan {
   int2 *bs_gather = nullptr;    // (i,k) tiles gathered by each backward level, root level first
   int *bs_gbeg = nullptr;       // [ncols+1] gather range of each backward column (bs_cols order)
   double *bs_part = nullptr;    // [n_gather*64] per-gather partial sums L_ik^T y_i (summed in order)
+  int *bs_counters = nullptr;   // [T+1] persistent backward solve: done[column] | ticket
   int *tile_id = nullptr;       // [T*T] compact index of tile (i,j), -1 if structurally zero
   std::vector<int> h_tile_id;
   long n_tiles = 0;             // tiles of the factor (compact storage = n_tiles * 4096 doubles)
@@ -204,6 +205,10 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
                           int *progress = nullptr, unsigned long long *trace = nullptr);
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s);
+// The same backward solve as one persistent launch (columns in root-first
+// ticket order, per-column completion counters).
+void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, double *yF, int *flag,
+                                 hipStream_t s, int n_workgroups);
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s);
 // copy the diagonal factors L_kk into S (tests only: S then holds the whole factor)
 void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s);

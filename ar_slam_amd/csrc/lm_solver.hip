@@ -585,7 +585,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       }
       timers[PH_CHOL].stop(stream);
       timers[PH_SOLVE].start(stream);
-      arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
+      if (opt.factor_executor == 1)
+        arslam::launch_dense_back_solve_dag(plan, d_S.p, nR, d_yF.p, d_flag.p, stream, dag_workgroups);
+      else
+        arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
       timers[PH_SOLVE].stop(stream);
     }
     timers[PH_BACK].start(stream);

@@ -66,10 +66,13 @@ def producers(t):
 
 
 path = []
+seen = set()
 t = int(np.argmax(end))
 while True:
     path.append(t)
-    ps = producers(t)
+    seen.add(t)
+    # a claimed POTRF publishes the tile it was claimed for: never walk back into the path itself
+    ps = [p for p in producers(t) if p[0] not in seen]
     if not ps:
         break
     t = max(ps, key=lambda p: p[1])[0]
