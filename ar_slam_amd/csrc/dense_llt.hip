@@ -877,15 +877,22 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
         const int4 it = a.items[task.z];
         dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-        const bool staged = false;
+        // A_kk (final: the task's waits are met) straight into the MFMA
+        // accumulator layout, sc1 loads in flight during the fold's GEMMs
+        double akk[16];
+        {
+          const double *Akk = tile_ptr(a.S, a.tid_map, a.T, k, k);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) akk[4 * q + reg] = ld_wt(Akk + (rb + lk + 4 * reg) * T64 + cb + li);
+          }
+        }
         if (cont) {
           // continuation: the fold's one column L_kj is the tile the previous
           // task just solved, still in X
           gemm64_nt(X, X, tid, acc);
-          if (!staged) {
-            __syncthreads();
-            load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), X, tid);
-          }
         }
         for (int q = cont ? it.z : it.y; q < it.z; ++q) {
           if (q > it.y) __syncthreads();
@@ -893,19 +900,12 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           __syncthreads();
           gemm64_nt(D, D, tid, acc);
         }
-        if (!cont) {
-          __syncthreads();
-          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), X, tid);
-        }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
 #pragma unroll
-          for (int reg = 0; reg < 4; ++reg) {
-            const int e = (rb + lk + 4 * reg) * LQ + cb + li;
-            D[e] = (staged ? D[e] : X[e]) - acc[q][reg];
-          }
+          for (int reg = 0; reg < 4; ++reg) D[(rb + lk + 4 * reg) * LQ + cb + li] = akk[4 * q + reg] - acc[q][reg];
         }
       } else {
         load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), D, tid);

@@ -42,7 +42,7 @@ for t in range(n):
         ready_prod[int(w)] = t
         if sub[t, 0] >= 0:
             ready_prod[int(sub[t, 0])] = t
-    else:
+    elif ty == 2:   # (INV tasks publish nothing another task waits for)
         applied_prod[int(w)].append((int(z), t))
 
 
