@@ -484,14 +484,14 @@ SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
   struct Item {
     long key;   // rX << 32 | rY
     int c;
-    int px, py;
+    int px, py, nblk;
   };
   std::vector<Item> items;
   std::vector<std::pair<int, int>> blk;   // (global first row, local first column) of the capture's blocks
   for (int c = 0; c < h.nc; ++c) {
     const int nblk = h.cap_blk_start[c + 1] - h.cap_blk_start[c];
     const long m = 1 + 6L * nblk;
-    G.cap_off[c + 1] = G.cap_off[c] + (m + 1) * (m + 2) / 2;
+    G.cap_off[c + 1] = G.cap_off[c] + schur_slab_size(nblk);
     if (h.cap_start[c + 1] == h.cap_start[c]) continue;   // no residuals: k_schur stores nothing
     blk.clear();
     if (L.cam_row >= 0) blk.emplace_back(L.cam_row, 0);
@@ -505,7 +505,7 @@ SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
       for (size_t b = 0; b < blk.size(); ++b) {
         const int rx = blk[a].first, ry = blk[b].first;
         if (rx < ry || ry == L.nR) continue;   // lower blocks; the rhs only as a row
-        items.push_back({((long)rx << 32) | ry, c, blk[a].second, blk[b].second});
+        items.push_back({((long)rx << 32) | ry, c, blk[a].second, blk[b].second, nblk});
       }
   }
   std::stable_sort(items.begin(), items.end(), [](const Item &x, const Item &y) { return x.key < y.key; });
@@ -517,7 +517,10 @@ SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
       G.dest_row.push_back((int)(items[i].key & 0xffffffffL));
       G.dest_start.push_back((int)G.contrib.size());
     }
-    G.contrib.push_back({G.cap_off[items[i].c], items[i].px, items[i].py});
+    const Item &t = items[i];
+    const int m = 1 + 6 * t.nblk, U = schur_blk(t.px, m), V = schur_blk(t.py, m);
+    if (U >= V) G.contrib.push_back({G.cap_off[t.c] + schur_block_off(U, V, t.nblk), 0, schur_blk_size(V, t.nblk)});
+    else G.contrib.push_back({G.cap_off[t.c] + schur_block_off(V, U, t.nblk), 1, schur_blk_size(U, t.nblk)});
   }
   if (!G.dest_start.empty())
     G.max_contrib = std::max(G.max_contrib, (int)(G.contrib.size() - G.dest_start.back()));

@@ -83,15 +83,34 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
                              const ReduceMaxU8 &pattern_max);
 
 // Deterministic Schur assembly.  k_schur stores capture c's local reduced
-// system packed (lower triangle, local order: f, 6 per tag, then the rhs
-// row) at slab + cap_off[c]; k_schur_gather sums, for every destination block
-// of the reduced system (global first rows rX >= rY; 1 row for f and the rhs,
-// 6 for a tag), the contributing captures' blocks in capture order and stores
-// the sum -- plain stores, no atomics, bitwise reproducible.
+// system at slab + cap_off[c] block-packed: local blocks U = 0 (f, 1 row),
+// 1..nblk (a tag, 6 rows), nblk+1 (the rhs row); the lower block pairs
+// (U >= V) in row-block order, each block contiguous and row-major, so the
+// gather of one destination block reads one contiguous run per capture
+// (schur_block_off).  k_schur_gather sums, for every destination block of the
+// reduced system (global first rows rX >= rY; 1 row for f and the rhs, 6 for
+// a tag), the contributing captures' blocks in capture order and stores the
+// sum -- plain stores, no atomics, bitwise reproducible.
+#if defined(__HIPCC__)
+#define ARSLAM_HD __host__ __device__
+#else
+#define ARSLAM_HD
+#endif
 struct SchurContrib {
-  long off;     // cap_off of the contributing capture
-  int px, py;   // local first columns of the destination's row and column blocks
+  long off;     // first element of the contributing local block in the slab
+  int tr, ld;   // tr: the block is stored transposed (local U < V); ld: its row length
 };
+// local block of local column x (m = 1 + 6 nblk: the rhs row)
+ARSLAM_HD inline int schur_blk(int x, int m) { return x == 0 ? 0 : (x == m ? 1 + (m - 1) / 6 : 1 + (x - 1) / 6); }
+ARSLAM_HD inline int schur_blk_size(int U, int nblk) { return (U == 0 || U == nblk + 1) ? 1 : 6; }
+ARSLAM_HD inline int schur_blk_start(int U, int nblk) { return U == 0 ? 0 : (U <= nblk ? 1 + 6 * (U - 1) : 1 + 6 * nblk); }
+// first element of block (U, V), U >= V: row blocks before U, then the blocks
+// (U, V') with V' < V (their columns = the local start of V)
+ARSLAM_HD inline long schur_block_off(int U, int V, int nblk) {
+  const long R = U == 0 ? 0 : 1 + 6L * (U - 1) + 18L * U * (U - 1);
+  return R + (long)schur_blk_size(U, nblk) * schur_blk_start(V, nblk);
+}
+ARSLAM_HD inline long schur_slab_size(int nblk) { return 3 + 12L * nblk + 18L * nblk * (nblk + 1); }
 // A destination with more than kSchurChunk contributions is summed in pieces
 // (work items writing partial sums, then one combine per split destination
 // adding the pieces in order), so no wave walks a long list serially.

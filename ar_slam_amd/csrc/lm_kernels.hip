@@ -312,10 +312,8 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   double *U = rows + (long)nrows * kRowStride;   // 36
   double *Ui = U + 36;                           // 36
   double *Etr = Ui + 36;                         // 8
-  double *UiE = Etr + 8;                         // 8
-  double *W = UiE + 8;                           // 6*m
-  double *Z = W + 6 * m;                         // 6*m
-  double *Ftr = Z + 6 * m;                       // m (+pad)
+  double *W = Etr + 8;                           // 6*m
+  double *Ftr = W + 6 * m;                       // m (+pad)
   double *FF = Ftr + m + (m & 1);                // 28 per tag block: F_u'F_u (21, packed), F_0'F_u (6), pad
   int *lblk = (int *)(FF + 28 * nblk);           // k
   double *ff00 = reinterpret_cast<double *>(lblk + k + (k & 1));   // F_0'F_0
@@ -443,58 +441,76 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   }
   __syncthreads();
   SCHUR_STAMP(2);
-  // Z = Ui W ; UiE = Ui E'r
-  for (int e = lane; e < 6 * m + 6; e += kWave) {
-    if (e < 6 * m) {
-      const int a = e / m, col = e % m;
-      double s = 0.0;
-#pragma unroll
-      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * W[b * m + col];
-      Z[a * m + col] = s;
-    } else {
-      const int a = e - 6 * m;
-      double s = 0.0;
-#pragma unroll
-      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * Etr[b];
-      UiE[a] = s;
-    }
-  }
-  __syncthreads();
   SCHUR_STAMP(3);
-  // packed rows p >= q (row m is the rhs); entries of constant blocks are
-  // never gathered
+  // block-packed rows (row m is the rhs; entries of constant blocks are never
+  // gathered; schur_block_off): lane q owns column q, z = (U + D_c^2)^{-1}
+  // W[:, q] in registers; row p is wave-uniform, so its W column (the rhs
+  // row: E'r) is an LDS broadcast.  One block row U at a time is staged in
+  // LDS (over the dead Jacobian rows) in its final layout, then copied out
+  // with contiguous stores.
+  //   (p, q) = F_p'F_q - W_p' z_q,   (m, q) = F_q'r - (E'r)' z_q
   double *out = P.slab + P.cap_off[c];
-  const int npairs = (m + 1) * (m + 2) / 2;
-  for (int e = lane; e < npairs; e += kWave) {
-    int p = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
-    p -= (p * (p + 1) / 2 > e);
-    p += ((p + 1) * (p + 2) / 2 <= e);
-    const int q = e - p * (p + 1) / 2;
-    double v = 0.0;
-    if (p == m) {
-      if (q < m) {
+  double *stage = rows;   // <= 6 (m + 1) doubles
+  auto make_z = [&](int q, double z[6]) {
+    if (q < m) {
+      double wq[6];
+#pragma unroll
+      for (int b = 0; b < 6; ++b) wq[b] = W[b * m + q];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
         double s = 0.0;
 #pragma unroll
-        for (int a = 0; a < 6; ++a) s += W[a * m + q] * UiE[a];
-        v = Ftr[q] - s;
+        for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * wq[b];
+        z[a] = s;
       }
     } else {
-      double ff = 0.0;
-      const int up = p == 0 ? -1 : (p - 1) / 6, uq = q == 0 ? -1 : (q - 1) / 6;
-      if (p == 0) {
-        ff = *ff00;   // q == 0
-      } else if (q == 0) {
-        ff = FF[28 * up + 21 + (p - 1) % 6];
-      } else if (up == uq) {
-        const int ip = (p - 1) % 6, iq = (q - 1) % 6;   // iq <= ip
-        ff = FF[28 * up + iq * 6 - iq * (iq - 1) / 2 + (ip - iq)];
-      }
-      double wz = 0.0;
 #pragma unroll
-      for (int a = 0; a < 6; ++a) wz += W[a * m + p] * Z[a * m + q];
-      v = ff - wz;
+      for (int a = 0; a < 6; ++a) z[a] = 0.0;
     }
-    out[e] = v;
+  };
+  const bool one_chunk = m + 1 <= kWave;
+  double z[6];
+  if (one_chunk) make_z(lane, z);
+  for (int U = 0; U <= nblk + 1; ++U) {
+    const int sU = schur_blk_size(U, nblk), p0U = schur_blk_start(U, nblk), ncol = p0U + sU;
+    for (int q0 = 0; q0 < ncol; q0 += kWave) {
+      const int q = q0 + lane;
+      if (!one_chunk) make_z(q, z);
+      const int V = schur_blk(min(q, m), m), sV = schur_blk_size(V, nblk), q0V = schur_blk_start(V, nblk);
+      const int uq = V - 1, iq = q - q0V;   // tag block and row inside it (V in 1..nblk)
+      for (int i = 0; i < sU; ++i) {
+        const int p = p0U + i;
+        const double *wp = p < m ? W + p : Etr;
+        const int st = p < m ? m : 1;
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) s += wp[a * st] * z[a];
+        double ff = 0.0;
+        if (p == m) {
+          ff = q < m ? Ftr[q] : 0.0;
+        } else if (p == 0) {
+          ff = *ff00;   // q == 0
+        } else {
+          const int up = U - 1;
+          if (q == 0) {
+            ff = FF[28 * up + 21 + i];
+          } else if (uq == up) {   // F_u'F_u packed upper (a <= b)
+            const int lo = min(i, iq), hi = max(i, iq);
+            ff = FF[28 * up + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+          }
+        }
+        if (q < ncol) stage[sU * q0V + i * sV + (q - q0V)] = ff - s;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double *dst = out + schur_block_off(U, 0, nblk);
+    const int nreg = sU * ncol;
+    for (int e = lane; e < nreg; e += kWave) dst[e] = stage[e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   SCHUR_STAMP(4);
 }
@@ -556,9 +572,7 @@ __global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__re
       for (int u = 0; u < 8; ++u) {
         const int t = min(t0 + u * g.G, nk - 1);   // clamped: always a valid address
         const SchurContrib ct = cts[w][t];
-        const int a = ct.px + g.i, b = ct.py + g.j;
-        const int hi = a > b ? a : b, lo = a > b ? b : a;
-        v[u] = P.slab[ct.off + (long)hi * (hi + 1) / 2 + lo];
+        v[u] = P.slab[ct.off + (ct.tr ? g.j * ct.ld + g.i : g.i * ct.ld + g.j)];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += (t0 + u * g.G < nk) ? v[u] : 0.0;
@@ -956,7 +970,7 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
   if (P.nc == 0) return;
   const int maxk = P.max_obs_per_cap;
   const int m = 1 + 6 * maxk;
-  const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 8 + 13L * m + 4 + 28L * maxk) +
+  const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 7L * m + 4 + 28L * maxk) +
                      sizeof(int) * (maxk + 2) + 2 * sizeof(double) + 64;
   hipLaunchKernelGGL(k_schur, dim3(P.nc), dim3(kWave), lds, s, P, scale, diag, radius);
   if (P.n_items)
