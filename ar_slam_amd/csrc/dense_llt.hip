@@ -1300,6 +1300,30 @@ void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s) {
   hipLaunchKernelGGL(k_scatter_diag, dim3((unsigned)P.T), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag);
 }
 
+namespace {
+// One launch zeroing the persistent executors' counters (and the step's
+// failure flag) instead of a fill launch per array.
+__global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c, long nc, int *d, long nd) {
+  const long n = na + nb + nc + nd;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    if (e < na) a[e] = 0;
+    else if (e < na + nb) b[e - na] = 0;
+    else if (e < na + nb + nc) c[e - na - nb] = 0;
+    else d[e - na - nb - nc] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 0;
+}
+}  // namespace
+
+void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s) {
+  const long na = P.n_dag_tasks ? 2 * P.n_tiles + 2 : 0, nb = P.n_dag_tasks, nc = P.n_split,
+             nd = P.h_bcols.empty() ? 0 : (long)P.T + 1;
+  const long n = na + nb + nc + nd;
+  const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 1024));
+  hipLaunchKernelGGL(k_exec_reset, dim3(grid), dim3(256), 0, s, flag, P.dag_counters, na, P.dag_claimed, nb,
+                     P.upd_cnt, nc, P.bs_counters, nd);
+}
+
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s) {
   if (P.n_tiles) (void)hipMemsetAsync(S, 0, (size_t)P.n_tiles * T64 * T64 * sizeof(double), s);
 }
@@ -1326,11 +1350,13 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
 }
 
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
-                          unsigned long long *trace) {
+                          unsigned long long *trace, bool reset) {
   if (P.n_dag_tasks == 0) return;
-  (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2) * sizeof(int), s);
-  (void)hipMemsetAsync(P.dag_claimed, 0, (size_t)P.n_dag_tasks * sizeof(int), s);
-  if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
+  if (reset) {
+    (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2) * sizeof(int), s);
+    (void)hipMemsetAsync(P.dag_claimed, 0, (size_t)P.n_dag_tasks * sizeof(int), s);
+    if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
+  }
   DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
             P.dag_maxdep, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
@@ -1340,10 +1366,10 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
 }
 
 void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, double *yF, int *flag,
-                                 hipStream_t s, int n_workgroups) {
+                                 hipStream_t s, int n_workgroups, bool reset) {
   const int ncols = (int)P.h_bcols.size();
   if (ncols == 0) return;
-  (void)hipMemsetAsync(P.bs_counters, 0, ((size_t)P.T + 1) * sizeof(int), s);
+  if (reset) (void)hipMemsetAsync(P.bs_counters, 0, ((size_t)P.T + 1) * sizeof(int), s);
   const int grid = std::min(n_workgroups, ncols);
   hipLaunchKernelGGL(k_bsolve_dag, dim3((unsigned)grid), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag, nR, P.bs_cols,
                      P.bs_gather, P.bs_gbeg, ncols, yF, P.bs_counters, flag);

@@ -201,14 +201,17 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
                       LaunchTiming *timing = nullptr);
 // The same factorization as one persistent launch over the plan's task graph
 // (tickets in a topological order, dependency counters in global memory).
+// (reset = false: the counters were zeroed by launch_exec_reset)
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups,
-                          int *progress = nullptr, unsigned long long *trace = nullptr);
+                          int *progress = nullptr, unsigned long long *trace = nullptr, bool reset = true);
+// *flag and every counter of the two persistent executors to zero, one launch
+void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s);
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s);
 // The same backward solve as one persistent launch (columns in root-first
 // ticket order, per-column completion counters).
 void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, double *yF, int *flag,
-                                 hipStream_t s, int n_workgroups);
+                                 hipStream_t s, int n_workgroups, bool reset = true);
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s);
 // copy the diagonal factors L_kk into S (tests only: S then holds the whole factor)
 void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s);

@@ -73,6 +73,17 @@ struct DevBuf {
   ~DevBuf() { release(); }
 };
 
+// page-locked host words: a D2H copy into them stays asynchronous
+struct PinnedBuf {
+  double *p = nullptr;
+  void alloc(size_t count) {
+    if (!p) HIP_CHECK(hipHostMalloc(&p, count * sizeof(double), hipHostMallocDefault));
+  }
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
 struct Timer {
   hipEvent_t a = nullptr, b = nullptr;
   double acc_ms = 0.0;
@@ -232,6 +243,10 @@ struct arslam_lm {
 
   void load(const arslam_soa_problem *p);
   void linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
+  // linearize split at the host read: enqueue (results copied to h_lin), collect after a sync
+  void linearize_launch();
+  void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
+  PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [4..9] slot norms
   void solve(arslam_lm_summary *s);
   void write_back(const double *d_src);
 };
@@ -369,8 +384,8 @@ void arslam_lm::load(const arslam_soa_problem *p) {
 
 // Evaluate residuals/Jacobian at x: cost, gradient (unscaled), column norms
 // and the norms the minimizer reads.  Ceres EvaluateGradientAndJacobian.
-void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
-                          double *xnorm) {
+void arslam_lm::linearize_launch() {
+  h_lin.alloc(16);
   timers[PH_LIN].start(stream);
   arslam::launch_linearize(P, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
   arslam::launch_tag_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, stream);
@@ -383,30 +398,36 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
   }
   arslam::launch_camera_slots(P, d_red.p, d_g.p, d_colnorm.p, stream);
   arslam::launch_slot_norms(P, d_g.p, x, d_norms.p, stream);
-  timers[PH_LIN].stop(stream);
-  double red[4], norms[6];
-  HIP_CHECK(hipMemcpyAsync(red, d_red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, stream));
-  HIP_CHECK(hipMemcpyAsync(norms, d_norms.p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
-  HIP_CHECK(hipStreamSynchronize(stream));
   if (nranks > 1) {
     // capture slots are disjoint across ranks, tag/camera slots replicated:
-    // norms[0..2] cover captures, norms[3..5] the rest
-    double cap_part[3] = {norms[0], norms[1], norms[2]};
-    DevBuf<double> tmp;
-    tmp.alloc(3);
-    tmp.upload(cap_part, 3, stream);
-    allreduce(tmp.p, 1, ARSLAM_OP_MAX);
-    allreduce(tmp.p + 1, 2, ARSLAM_OP_SUM);
-    HIP_CHECK(hipMemcpyAsync(cap_part, tmp.p, 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
-    norms[0] = cap_part[0]; norms[1] = cap_part[1]; norms[2] = cap_part[2];
+    // norms[0..2] cover captures (max, sum, sum), norms[3..5] the rest
+    allreduce(d_norms.p, 1, ARSLAM_OP_MAX);
+    allreduce(d_norms.p + 1, 2, ARSLAM_OP_SUM);
   }
+  timers[PH_LIN].stop(stream);
+  HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipMemcpyAsync(h_lin.p + 4, d_norms.p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
+}
+
+// (after a stream sync that covers linearize_launch)
+void arslam_lm::linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
+                                  double *xnorm) {
+  const double *red = h_lin.p, *norms = h_lin.p + 4;
   *x_cost = red[arslam::P_COST];
   *fixed_cost = red[arslam::P_FIXED];
   *gmax = std::max(norms[0], norms[3]);
   *gnorm = std::sqrt(norms[1] + norms[4]);
   *xnorm = std::sqrt(norms[2] + norms[5]);
   timers[PH_LIN].collect();
+}
+
+// Evaluate residuals/Jacobian at x: cost, gradient (unscaled), column norms
+// and the norms the minimizer reads.  Ceres EvaluateGradientAndJacobian.
+void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
+                          double *xnorm) {
+  linearize_launch();
+  HIP_CHECK(hipStreamSynchronize(stream));
+  linearize_collect(x_cost, fixed_cost, gmax, gnorm, xnorm);
 }
 
 void arslam_lm::write_back(const double *d_src) {
@@ -477,7 +498,21 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   it.step_is_successful = 1;
   double t_iter = t_start;
 
-  for (;;) {
+  // A successful step's re-linearization is only enqueued (lin_pending): the
+  // next step's kernels follow it in the stream, and its results are read at
+  // that step's one host sync, where the finalization below runs first.  If
+  // it then stops the minimizer, the speculative step is dropped uncounted.
+  bool lin_pending = false;
+  double prev_gmax = 0.0, prev_gnorm = 0.0;
+  auto finalize = [&]() -> bool {   // true: the minimizer stops
+    if (lin_pending) {
+      double fc;
+      linearize_collect(&x_cost, &fc, &gmax, &gnorm, &x_norm);
+      it.cost = x_cost + fixed_cost;
+      it.gradient_max_norm = gmax;
+      it.gradient_norm = gnorm;
+      lin_pending = false;
+    }
     // ---- FinalizeIterationAndCheckIfMinimizerCanContinue ----
     if (it.step_is_successful) {
       if (it.iteration > 0) s->num_successful_steps++;
@@ -497,25 +532,38 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     if (s->n_iters <= ARSLAM_LM_MAX_ITERS) s->iters[s->n_iters++] = it;
     if (o.minimizer_progress_to_stdout && root) print_row(it);
     if (it.iteration >= o.max_num_iterations) {
-      s->termination = ARSLAM_NO_CONVERGENCE; s->rule = ARSLAM_RULE_MAX_ITERS; break;
+      s->termination = ARSLAM_NO_CONVERGENCE; s->rule = ARSLAM_RULE_MAX_ITERS; return true;
     }
     if (it.step_is_successful && it.gradient_max_norm <= o.gradient_tolerance) {
-      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_GRADIENT; break;
+      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_GRADIENT; return true;
     }
     if (radius <= o.min_trust_region_radius) {
-      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_MIN_RADIUS; break;
+      s->termination = ARSLAM_CONVERGENCE; s->rule = ARSLAM_RULE_MIN_RADIUS; return true;
     }
-    const double prev_gmax = it.gradient_max_norm, prev_gnorm = it.gradient_norm;
+    prev_gmax = it.gradient_max_norm;
+    prev_gnorm = it.gradient_norm;
     const int next_iter = it.iteration + 1;
     it = arslam_lm_iteration{};
     it.iteration = next_iter;
+    return false;
+  };
+
+  for (;;) {
+    // the stop rules that do not read the pending linearization: decided now
+    // (after reading it), so no step is computed past them
+    const bool stop_rule = it.iteration >= o.max_num_iterations || radius <= o.min_trust_region_radius;
+    if (lin_pending && stop_rule) HIP_CHECK(hipStreamSynchronize(stream));
+    const bool deferred = lin_pending && !stop_rule;
+    if (!deferred && finalize()) break;
 
     // ---- ComputeTrustRegionStep: LM diagonal, DENSE_SCHUR solve ----
     s->num_linear_solves++;
     if (!reuse_diag)
       arslam::launch_lm_diag(P, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal, d_diag.p, stream);
     reuse_diag = true;
-    HIP_CHECK(hipMemsetAsync(d_flag.p, 0, sizeof(int), stream));
+    const bool exec_dag = has_f && opt.factor_executor == 1;
+    if (exec_dag) arslam::launch_exec_reset(plan, d_flag.p, stream);   // flag + executor counters, one launch
+    else HIP_CHECK(hipMemsetAsync(d_flag.p, 0, sizeof(int), stream));
     if (has_f) {
       timers[PH_SCHUR].start(stream);
       arslam::launch_zero_tiles(plan, d_S.p, stream);
@@ -534,7 +582,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           DevBuf<unsigned long long> tr;
           tr.alloc(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemsetAsync(tr.p, 0, tr.n * 8, stream));
-          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, tr.p);
+          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, tr.p, false);
           std::vector<unsigned long long> h(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemcpyAsync(h.data(), tr.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
           HIP_CHECK(hipStreamSynchronize(stream));
@@ -552,7 +600,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           }
           dag_traced = true;
         } else {
-          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups);
+          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false);
         }
         if (rec) {
           HIP_CHECK(hipEventRecord(upd_timing.ev[2 * upd_timing.used + 1], stream));
@@ -586,7 +634,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       timers[PH_CHOL].stop(stream);
       timers[PH_SOLVE].start(stream);
       if (opt.factor_executor == 1)
-        arslam::launch_dense_back_solve_dag(plan, d_S.p, nR, d_yF.p, d_flag.p, stream, dag_workgroups);
+        arslam::launch_dense_back_solve_dag(plan, d_S.p, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false);
       else
         arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
       timers[PH_SOLVE].stop(stream);
@@ -613,6 +661,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     HIP_CHECK(hipStreamSynchronize(stream));
     for (int ph = PH_SCHUR; ph < PH_N; ++ph) timers[ph].collect();
     timing_collect();
+    if (deferred && finalize()) {
+      s->num_linear_solves--;   // the speculative step is not part of the trace
+      break;
+    }
 
     const bool lin_fail = flag != 0;
     if (lin_fail && std::getenv("ARSLAM_DEBUG_FLAG"))   // debug: factorization failure code
@@ -654,11 +706,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
                                                      : (x_cost - candidate_cost) / model_cost_change;
     if (it.relative_decrease > o.min_relative_decrease) {
       std::swap(x, xc);
-      double fc;
-      linearize(&x_cost, &fc, &gmax, &gnorm, &x_norm);
-      it.cost = x_cost + fixed_cost;
-      it.gradient_max_norm = gmax;
-      it.gradient_norm = gnorm;
+      linearize_launch();   // read at the next step's sync (finalize)
+      lin_pending = true;
       it.step_is_successful = 1;
       const double q = 2.0 * it.relative_decrease - 1.0;
       radius = radius / std::max(1.0 / 3.0, 1.0 - q * q * q);
