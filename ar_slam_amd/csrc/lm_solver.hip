@@ -237,6 +237,7 @@ struct arslam_lm {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       dag_workgroups = 2 * cus;   // two 73 KB-LDS workgroups per CU
+    if (const char *g = std::getenv("ARSLAM_DAG_GRID")) dag_workgroups = std::max(1, std::atoi(g));   // debug
     if (!stream) HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &t : timers) t.init();
   }
