@@ -70,6 +70,7 @@ struct DevProblem {
   double *gather_part;       // [n_pslots * 36]
   int n_items, n_splits;
   double *jrows;             // [8 nb kRowStride] unscaled Jacobian rows + residual at the linearization point
+  double *cap_ui;            // [36 nc] (U_c + D_c^2)^{-1} of the current step (k_schur -> k_backsub)
 };
 
 // element (r, c), r >= c, of the compact-tiled reduced system
@@ -170,7 +171,8 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
                          hipStream_t s);
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                    double radius, const double *yF, double *xc, double *parts, hipStream_t s);
+                    double radius, const double *yF, double *xc, double *parts, hipStream_t s,
+                    bool reuse_ui = false);
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,
                      double *xc, double *fparts, hipStream_t s);
 void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_t s);

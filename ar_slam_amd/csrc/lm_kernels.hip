@@ -440,6 +440,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
 #undef LI6
   }
   __syncthreads();
+  if (lane < 36) P.cap_ui[36L * c + lane] = Ui[lane];   // reused by k_backsub
   SCHUR_STAMP(2);
   SCHUR_STAMP(3);
   // block-packed rows (row m is the rhs; entries of constant blocks are never
@@ -639,7 +640,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
                                                    const double *__restrict__ diag, double radius,
                                                    const double *__restrict__ yF,
                                                    double *__restrict__ xc,
-                                                   double *__restrict__ parts) {
+                                                   double *__restrict__ parts, int reuse_ui) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int c = blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
@@ -674,34 +675,55 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
     qv[row] = q;
   }
   __syncthreads();
-  if (lane < 27) {
-    double s = 0.0;
-    if (lane < 21) {
-      int a, b;
-      upper6(lane, a, b);
-      for (int r = 0; r < nrows; ++r) s += rows[(long)r * kRowStride + 1 + a] * rows[(long)r * kRowStride + 1 + b];
-      U[6 * a + b] = s;
-      U[6 * b + a] = s;
-    } else {
-      const int a = lane - 21;
+  if (reuse_ui) {
+    // (U_c + D_c^2)^{-1} as k_schur formed it for this step
+    if (lane < 36) Ui[lane] = P.cap_ui[36L * c + lane];
+    if (lane >= 32 && lane < 38) {
+      const int a = lane - 32;
+      double s = 0.0;
       for (int r = 0; r < nrows; ++r) {
         const double *rr = rows + (long)r * kRowStride;
         s += rr[1 + a] * (rr[13] - qv[r]);   // E'(b - F z)
       }
       v[a] = s;
     }
-  }
-  __syncthreads();
-  if (lane == 0) {
-#pragma unroll
-    for (int a = 0; a < 6; ++a) U[7 * a] += lm_d2(diag, sc + a, radius);
-    inv6(U, Ui);
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
+    __syncthreads();
+    if (lane < 6) {
       double s = 0.0;
 #pragma unroll
-      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * v[b];
-      yc[a] = s;
+      for (int b = 0; b < 6; ++b) s += Ui[6 * lane + b] * v[b];
+      yc[lane] = s;
+    }
+  } else {
+    if (lane < 27) {
+      double s = 0.0;
+      if (lane < 21) {
+        int a, b;
+        upper6(lane, a, b);
+        for (int r = 0; r < nrows; ++r) s += rows[(long)r * kRowStride + 1 + a] * rows[(long)r * kRowStride + 1 + b];
+        U[6 * a + b] = s;
+        U[6 * b + a] = s;
+      } else {
+        const int a = lane - 21;
+        for (int r = 0; r < nrows; ++r) {
+          const double *rr = rows + (long)r * kRowStride;
+          s += rr[1 + a] * (rr[13] - qv[r]);   // E'(b - F z)
+        }
+        v[a] = s;
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) U[7 * a] += lm_d2(diag, sc + a, radius);
+      inv6(U, Ui);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        double s = 0.0;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * v[b];
+        yc[a] = s;
+      }
     }
   }
   __syncthreads();
@@ -986,11 +1008,12 @@ void launch_prep_reduced(const DevProblem &P, const double *diag, double radius,
 }
 
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                    double radius, const double *yF, double *xc, double *parts, hipStream_t s) {
+                    double radius, const double *yF, double *xc, double *parts, hipStream_t s,
+                    bool reuse_ui) {
   if (P.nc == 0) return;
   const int maxk = P.max_obs_per_cap;
   const size_t lds = lds_rows(maxk) + sizeof(double) * (8L * maxk + 36 + 36 + 16);
-  hipLaunchKernelGGL(k_backsub, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts);
+  hipLaunchKernelGGL(k_backsub, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts, reuse_ui ? 1 : 0);
 }
 
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,

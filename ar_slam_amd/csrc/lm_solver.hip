@@ -147,7 +147,7 @@ struct arslam_lm {
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_norms, d_S, d_z, d_yF;
   DevBuf<int> d_flag, d_tag_row, d_row_slot;
   DevBuf<long> d_cap_off;
-  DevBuf<double> d_slab, d_jrows;
+  DevBuf<double> d_slab, d_jrows, d_cap_ui;
   DevBuf<int2> d_dest_row;
   DevBuf<int4> d_gather_items, d_gather_splits;
   DevBuf<double> d_gather_part;
@@ -328,6 +328,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_g.alloc(n); d_colnorm.alloc(n); d_scale.alloc(n); d_diag.alloc(n);
   d_obs_tg.alloc(std::max(12L * nb, 1L));
   d_jrows.alloc(std::max(8L * arslam::kRowStride * nb, 1L));
+  d_cap_ui.alloc(std::max(36L * nc, 1L));
   d_parts.alloc((size_t)arslam::NPART * std::max(nc, 1));
   n_fparts = (int)((std::max(nR, 1L) + 255) / 256);
   d_fparts.alloc(2L * std::max(n_fparts, 1));
@@ -376,7 +377,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   P.tag_row = d_tag_row.p; P.row_slot = d_row_slot.p;
   P.tile_id = plan.tile_id; P.T = plan.T;
   P.cap_off = d_cap_off.p; P.slab = d_slab.p; P.dest_row = d_dest_row.p; P.dest_start = d_dest_start.p;
-  P.contrib = d_contrib.p; P.n_dest = n_dest; P.jrows = d_jrows.p;
+  P.contrib = d_contrib.p; P.n_dest = n_dest; P.jrows = d_jrows.p; P.cap_ui = d_cap_ui.p;
   P.gather_items = d_gather_items.p; P.gather_splits = d_gather_splits.p; P.gather_part = d_gather_part.p;
   P.n_items = n_items; P.n_splits = n_splits;
   HIP_CHECK(hipStreamSynchronize(stream));
@@ -642,7 +643,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     }
     timers[PH_BACK].start(stream);
     HIP_CHECK(hipMemcpyAsync(xc, x, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
-    arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream);
+    arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream, has_f);
     arslam::launch_update_f(P, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
     timers[PH_BACK].stop(stream);
     timers[PH_COST].start(stream);
