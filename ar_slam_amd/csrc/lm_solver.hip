@@ -196,6 +196,7 @@ struct arslam_lm {
   ~arslam_lm() {
     for (auto &t : timers) t.destroy();
     for (auto e : upd_events) (void)hipEventDestroy(e);
+    if (ev_sync) (void)hipEventDestroy(ev_sync);
     arslam::llt_plan_free(plan);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
@@ -248,6 +249,18 @@ struct arslam_lm {
   void linearize_launch();
   void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
   PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [4..9] slot norms
+  PinnedBuf h_step;  // [0..NPART+1] the step's reduced scalars, [15] the factorization flag (int bits)
+  hipEvent_t ev_sync = nullptr;
+  // Wait for the stream by polling an event: the LM loop's one host round
+  // trip per step, without the blocking-sync wake-up latency.
+  void spin_sync() {
+    if (!ev_sync) HIP_CHECK(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(ev_sync, stream));
+    hipError_t e;
+    while ((e = hipEventQuery(ev_sync)) == hipErrorNotReady) {
+    }
+    HIP_CHECK(e);
+  }
   void solve(arslam_lm_summary *s);
   void write_back(const double *d_src);
 };
@@ -428,7 +441,7 @@ void arslam_lm::linearize_collect(double *x_cost, double *fixed_cost, double *gm
 void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
                           double *xnorm) {
   linearize_launch();
-  HIP_CHECK(hipStreamSynchronize(stream));
+  spin_sync();
   linearize_collect(x_cost, fixed_cost, gmax, gnorm, xnorm);
 }
 
@@ -554,7 +567,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     // the stop rules that do not read the pending linearization: decided now
     // (after reading it), so no step is computed past them
     const bool stop_rule = it.iteration >= o.max_num_iterations || radius <= o.min_trust_region_radius;
-    if (lin_pending && stop_rule) HIP_CHECK(hipStreamSynchronize(stream));
+    if (lin_pending && stop_rule) spin_sync();
     const bool deferred = lin_pending && !stop_rule;
     if (!deferred && finalize()) break;
 
@@ -656,11 +669,13 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       allreduce(d_red.p + arslam::P_YBAD, 2, ARSLAM_OP_MAX);
     }
     timers[PH_COST].stop(stream);
-    double red[16];
+    h_step.alloc(16);
+    HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 2) * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipMemcpyAsync(h_step.p + 15, d_flag.p, sizeof(int), hipMemcpyDeviceToHost, stream));
+    spin_sync();
+    const double *red = h_step.p;
     int flag = 0;
-    HIP_CHECK(hipMemcpyAsync(red, d_red.p, (arslam::NPART + 2) * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipMemcpyAsync(&flag, d_flag.p, sizeof(int), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
+    std::memcpy(&flag, h_step.p + 15, sizeof(int));
     for (int ph = PH_SCHUR; ph < PH_N; ++ph) timers[ph].collect();
     timing_collect();
     if (deferred && finalize()) {
