@@ -76,8 +76,12 @@ struct DevBuf {
 // page-locked host words: a D2H copy into them stays asynchronous
 struct PinnedBuf {
   double *p = nullptr;
-  void alloc(size_t count) {
-    if (!p) HIP_CHECK(hipHostMalloc(&p, count * sizeof(double), hipHostMallocDefault));
+  size_t cap = 0;
+  void alloc(size_t count) {   // grows only; keeps the buffer across solves
+    if (count <= cap) return;
+    if (p) (void)hipHostFree(p);
+    HIP_CHECK(hipHostMalloc(&p, count * sizeof(double), hipHostMallocDefault));
+    cap = count;
   }
   ~PinnedBuf() {
     if (p) (void)hipHostFree(p);
@@ -249,6 +253,7 @@ struct arslam_lm {
   void linearize_launch();
   void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
   PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [4..9] slot norms
+  PinnedBuf h_x;     // [n] parameter download (write_back)
   PinnedBuf h_step;  // [0..NPART+1] the step's reduced scalars, [15] the factorization flag (int bits)
   hipEvent_t ev_sync = nullptr;
   // Wait for the stream by polling an event: the LM loop's one host round
@@ -446,12 +451,13 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
 }
 
 void arslam_lm::write_back(const double *d_src) {
-  std::vector<double> h(n);
-  HIP_CHECK(hipMemcpyAsync(h.data(), d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
-  HIP_CHECK(hipStreamSynchronize(stream));
-  std::memcpy(soa.camera, h.data(), 3 * sizeof(double));
-  if (nc) std::memcpy(soa.cap, h.data() + 3, 6L * nc * sizeof(double));
-  if (nt) std::memcpy(soa.tag, h.data() + 3 + 6L * nc, 6L * nt * sizeof(double));
+  h_x.alloc(n);   // page-locked: the parameter download is one DMA, no staging
+  HIP_CHECK(hipMemcpyAsync(h_x.p, d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+  spin_sync();
+  const double *h = h_x.p;
+  std::memcpy(soa.camera, h, 3 * sizeof(double));
+  if (nc) std::memcpy(soa.cap, h + 3, 6L * nc * sizeof(double));
+  if (nt) std::memcpy(soa.tag, h + 3 + 6L * nc, 6L * nt * sizeof(double));
 }
 
 namespace {
