@@ -186,9 +186,11 @@ __device__ __forceinline__ double block_dot(const double *rows, const int *lblk,
 // Kernels
 // ---------------------------------------------------------------------------
 
+// (4 waves per SIMD instead of the 3 its 143 VGPRs allow: a 28-byte spill,
+// 84 -> 71 us on cfg3; 5 waves spills 148 bytes and is slower)
 // Linearize at x: per-observation tag gradient/column norms, per-capture
 // gradient/column norms, cost and camera partials.  Unscaled Jacobian.
-__global__ __launch_bounds__(kWave) void k_linearize(DevProblem P, const double *__restrict__ x,
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_linearize(DevProblem P, const double *__restrict__ x,
                                                      double *__restrict__ g,
                                                      double *__restrict__ colnorm,
                                                      double *__restrict__ obs_tg,
