@@ -481,28 +481,40 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
       if (!one_chunk) make_z(q, z);
       const int V = schur_blk(min(q, m), m), sV = schur_blk_size(V, nblk), q0V = schur_blk_start(V, nblk);
       const int uq = V - 1, iq = q - q0V;   // tag block and row inside it (V in 1..nblk)
-      for (int i = 0; i < sU; ++i) {
-        const int p = p0U + i;
-        const double *wp = p < m ? W + p : Etr;
-        const int st = p < m ? m : 1;
-        double s = 0.0;
+      if (sU == 6) {
+        // a tag block row: the 36 W entries of its six rows read up front
+        // (independent broadcasts), then six rows of six FMAs
+        const int up = U - 1;
+        double wv[6][6];
 #pragma unroll
-        for (int a = 0; a < 6; ++a) s += wp[a * st] * z[a];
-        double ff = 0.0;
-        if (p == m) {
-          ff = q < m ? Ftr[q] : 0.0;
-        } else if (p == 0) {
-          ff = *ff00;   // q == 0
-        } else {
-          const int up = U - 1;
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+          for (int a = 0; a < 6; ++a) wv[i][a] = W[a * m + p0U + i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          double s = 0.0;
+#pragma unroll
+          for (int a = 0; a < 6; ++a) s += wv[i][a] * z[a];
+          double ff = 0.0;
           if (q == 0) {
             ff = FF[28 * up + 21 + i];
           } else if (uq == up) {   // F_u'F_u packed upper (a <= b)
             const int lo = min(i, iq), hi = max(i, iq);
             ff = FF[28 * up + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
           }
+          if (q < ncol) stage[6 * q0V + i * sV + (q - q0V)] = ff - s;
         }
-        if (q < ncol) stage[sU * q0V + i * sV + (q - q0V)] = ff - s;
+      } else {   // the f row (p = 0) or the rhs row (p = m)
+        const int p = p0U;
+        const double *wp = p < m ? W + p : Etr;
+        const int st = p < m ? m : 1;
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) s += wp[a * st] * z[a];
+        double ff = 0.0;
+        if (p == m) ff = q < m ? Ftr[q] : 0.0;
+        else ff = *ff00;   // p == 0: only q == 0 is stored
+        if (q < ncol) stage[q0V + (q - q0V)] = ff - s;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
