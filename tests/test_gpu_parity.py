@@ -39,23 +39,27 @@ def test_residual_jacobian_matches_oracle(lm, oracle):
         assert np.max(np.abs(J[i] - Jo) / scale) < 1e-12
 
 
+@pytest.mark.parametrize("executor", [0, 1])
 @pytest.mark.parametrize("n", [5, 64, 200, 777])
-def test_dense_llt_matches_numpy(lm, n):
+def test_dense_llt_matches_numpy(lm, n, executor):
+    """Tiled Cholesky + forward/backward solve of a dense SPD matrix: level launches (0) and the
+    persistent factorization + persistent backward solve (1)."""
     rng = np.random.default_rng(n)
     B = rng.normal(size=(n, n))
     A = B @ B.T + n * np.eye(n)
     b = rng.normal(size=n)
-    L, y, info = lm.debug_dense_llt(A, b)
+    L, y, info = lm.debug_dense_llt(A, b, executor=executor)
     assert info == 0
     Lref = np.linalg.cholesky(A)
     np.testing.assert_allclose(L, Lref, rtol=1e-10, atol=1e-10 * np.abs(Lref).max())
     np.testing.assert_allclose(A @ y, b, rtol=1e-9, atol=1e-9 * np.abs(b).max())
 
 
-def test_dense_llt_reports_indefinite(lm):
+@pytest.mark.parametrize("executor", [0, 1])
+def test_dense_llt_reports_indefinite(lm, executor):
     A = np.eye(100)
     A[70, 70] = -1.0
-    _, _, info = lm.debug_dense_llt(A, np.ones(100))
+    _, _, info = lm.debug_dense_llt(A, np.ones(100), executor=executor)
     assert info == 71
 
 
