@@ -92,14 +92,18 @@ struct Timer {
   hipEvent_t a = nullptr, b = nullptr;
   double acc_ms = 0.0;
   bool pending = false;
+  bool on = true;   // options.phase_timing
   void init() {
     if (!a) {
       HIP_CHECK(hipEventCreate(&a));
       HIP_CHECK(hipEventCreate(&b));
     }
   }
-  void start(hipStream_t s) { HIP_CHECK(hipEventRecord(a, s)); }
+  void start(hipStream_t s) {
+    if (on) HIP_CHECK(hipEventRecord(a, s));
+  }
   void stop(hipStream_t s) {
+    if (!on) return;
     HIP_CHECK(hipEventRecord(b, s));
     pending = true;
   }
@@ -480,7 +484,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   const arslam_lm_options &o = opt;
   const double t_start = now_s();
   std::memset(s, 0, sizeof(*s));
-  for (auto &t : timers) t.acc_ms = 0.0;
+  for (auto &t : timers) {
+    t.acc_ms = 0.0;
+    t.on = o.phase_timing != 0;
+  }
   dom_ms = dom_flops = 0.0;
   dom_launches = 0;
   s->n_obs = nb;
@@ -829,6 +836,7 @@ int arslam_lm_options_init(arslam_lm_options *o) {
   o->reduced_ordering = 2;
   o->kernel_timing = 0;
   o->factor_executor = 1;
+  o->phase_timing = 1;
   return ARSLAM_OK;
 }
 

@@ -82,7 +82,8 @@ class Options(C.Structure):
                 ("minimizer_progress_to_stdout", C.c_int),
                 ("update_state_every_iteration", C.c_int),
                 ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int),
-                ("reduced_ordering", C.c_int), ("kernel_timing", C.c_int), ("factor_executor", C.c_int)]
+                ("reduced_ordering", C.c_int), ("kernel_timing", C.c_int), ("factor_executor", C.c_int),
+                ("phase_timing", C.c_int)]
 
 
 class Iteration(C.Structure):

@@ -88,6 +88,9 @@ typedef struct {
   int kernel_timing;                 /* 1: HIP events around every launch of the dominant kernel */
   int factor_executor;               /* reduced-system Cholesky: 0 two launches per elimination-tree
                                         level, 1 one persistent task-graph launch (default) */
+  int phase_timing;                  /* 1 (default): HIP events around each phase of the step
+                                        (summary t_*_ms); 0: none (each event record costs a few
+                                        microseconds of GPU time between kernels) */
 } arslam_lm_options;
 
 /* ceres::IterationSummary subset */
