@@ -327,7 +327,12 @@ __device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *L
 // rest of the trailing update, so the critical chain is the four diag16
 // calls plus one 16-row solve and one 16x16 update per panel.
 // Returns false (uniformly) if a pivot is not positive; inv[c] = 1 / L_cc.
-__device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, int tid, double *colx) {
+// idle(w, lane) runs on waves 1-3 while wave 0 factors the first diagonal
+// block (they have no trailing update yet): the persistent executor fetches
+// its fused TRSM's tile there.
+template <class Idle>
+__device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *bad, int tid, double *colx,
+                                     Idle &&idle) {
   const int w = tid >> 6, lane = tid & 63;
   if (tid == 0) *bad = 0;
   __syncthreads();
@@ -337,7 +342,9 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
     if (w == 0) {
       if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
       diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane, colx);
-    } else if (p > 0) {
+    } else if (p == 0) {
+      idle(w, lane);
+    } else {
       // panel p-1's update of blocks (I, C), I >= C >= p, except (p, p)
       const int m = 4 - p, ntl = m * (m + 1) / 2;
       for (int t = w; t < ntl; t += 3) {
@@ -359,6 +366,10 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
     STAMP(13 + 4 * p);
   }
   return *bad == 0;
+}
+
+__device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, int tid, double *colx) {
+  return blocked_potrf64_idle(D, inv, LTd, bad, tid, colx, [](int, int) {});
 }
 
 // In-LDS blocked solve X L^T = A for a 64x64 tile X (256 threads), L from
@@ -822,9 +833,11 @@ __device__ __forceinline__ unsigned long long realtime() {
 
 __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
-  __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 4];
+  __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 4 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
-  int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);   // [0] ticket, [1] bad, [2] ok, [3] last
+  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [5] fused TRSM tile prefetched
+  int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
+  double *colx = LTd + 4 * 16 * LI + 4;   // POTRF pivot scratch (X stays free for the prefetch)
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
   const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
@@ -912,7 +925,37 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       }
       __syncthreads();
       if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
-            const bool ok = blocked_potrf64(D, inv, LTd, sh + 1, tid, X);   // X is free until the fused TRSM
+      // The fused TRSM's tile: wave 1 fetches it into X while wave 0 factors
+      // the first diagonal block, if its late waits are already met (sh[5]);
+      // otherwise it is waited for and loaded after L_kk is published.
+      const double *pf_src = sub.x >= 0 ? a.S + (long)sub.x * (T64 * T64) : nullptr;
+      const int pw0 = sub.y, pw1 = a.wait_off[t + 1];
+      const bool ok = blocked_potrf64_idle(D, inv, LTd, sh + 1, tid, colx, [&](int wv, int ln) {
+        if (wv != 1) return;
+        bool met = false;
+        if (pf_src && pw1 - pw0 <= 64) {
+          const int q = pw0 + ln;
+          const int2 cv = q < pw1 ? a.waits[q] : make_int2(0, 0);
+          const int got = q < pw1 ? ld_acquire_relaxed(a.counters + cv.x) : 0;
+          met = __builtin_amdgcn_ballot_w64(q < pw1 && got < cv.y) == 0;
+        }
+        if (met) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const double *p8[8];
+            dbl2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * ((g * 8 + u) * 64 + ln);
+            ld_wt16x8(p8, v);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int e = (g * 8 + u) * 64 + ln, r = e >> 5, c2 = (e & 31) * 2;
+              *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
+            }
+          }
+        }
+        if (ln == 0) sh[5] = met ? 1 : 0;
+      });
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
         int first = 0;
@@ -928,14 +971,17 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       if (a.trace && tid == 0) a.trace[8L * t + 6] = realtime();
       if (sub.x >= 0) {
         // fused TRSM of the parent's tile against the L_kk still in LDS
-        if (w == 0) {
-          const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane);
-          if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
+        const bool pref = sh[5] != 0;   // (written inside the POTRF, barriers since)
+        if (!pref) {
+          if (w == 0) {
+            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane);
+            if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
+          }
+          __syncthreads();
         }
-        __syncthreads();
         const int c = a.cont[t];
         double *Ct = a.S + (long)sub.x * (T64 * T64);
-        load_tile_wt(Ct, X, tid);
+        if (!pref) load_tile_wt(Ct, X, tid);
         __syncthreads();
         blocked_trsm64(X, D, inv, LTd, tid);
         store_tile_wt(Ct, X, tid, false);
