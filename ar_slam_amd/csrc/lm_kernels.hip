@@ -858,7 +858,8 @@ __global__ __launch_bounds__(kWave) void k_cost(DevProblem P, const double *__re
 // assignment, fixed tree); 8 loads in flight per thread.
 __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
                                                        const double *__restrict__ fparts,
-                                                       int nfparts, double *__restrict__ out) {
+                                                       int nfparts, double *__restrict__ out,
+                                                       const int *__restrict__ flag) {
   __shared__ double red[1024];
   const int t = threadIdx.x;
   const int p = blockIdx.x;
@@ -884,6 +885,7 @@ __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict_
     __syncthreads();
   }
   if (t == 0) out[p] = red[0];
+  if (flag && p == 0 && t == 0) out[NPART + 2] = (double)*flag;   // rides along the step's one D2H
 }
 
 // Norms over free parameter slots, split into capture slots (out[0..2]) and
@@ -1043,8 +1045,8 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 }
 
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out);
+                         hipStream_t s, const int *flag) {
+  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag);
 }
 
 void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out, hipStream_t s) {

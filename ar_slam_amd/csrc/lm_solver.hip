@@ -152,7 +152,8 @@ struct arslam_lm {
   DevBuf<int> d_cap_start, d_obs_tag, d_obs_lblk, d_cap_blk_start, d_blk_tag, d_tag_start, d_tag_obs;
   DevBuf<unsigned char> d_obs_active, d_slot_free;
   DevBuf<double> d_corners, d_x0, d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
-  DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_norms, d_S, d_z, d_yF;
+  DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_S, d_z, d_yF;
+  double *d_norms_p = nullptr;   // inside d_red
   DevBuf<int> d_flag, d_tag_row, d_row_slot;
   DevBuf<long> d_cap_off;
   DevBuf<double> d_slab, d_jrows, d_cap_ui;
@@ -256,9 +257,9 @@ struct arslam_lm {
   // linearize split at the host read: enqueue (results copied to h_lin), collect after a sync
   void linearize_launch();
   void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
-  PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [4..9] slot norms
+  PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [16..21] slot norms
   PinnedBuf h_x;     // [n] parameter download (write_back)
-  PinnedBuf h_step;  // [0..NPART+1] the step's reduced scalars, [15] the factorization flag (int bits)
+  PinnedBuf h_step;  // [0..NPART+1] the step's reduced scalars, [NPART+2] the factorization flag
   hipEvent_t ev_sync = nullptr;
   // Wait for the stream by polling an event: the LM loop's one host round
   // trip per step, without the blocking-sync wake-up latency.
@@ -356,8 +357,8 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_fparts.alloc(2L * std::max(n_fparts, 1));
   // stays zero when there are no reduced rows (k_update_f is then not launched)
   HIP_CHECK(hipMemsetAsync(d_fparts.p, 0, d_fparts.n * sizeof(double), stream));
-  d_red.alloc(16);
-  d_norms.alloc(8 + 6 * 64);   // results + k_slot_norms block partials
+  d_red.alloc(16 + 8 + 6 * 64);   // LM scalars | slot norms: results + k_slot_norms block partials
+  d_norms_p = d_red.p + 16;       // (one D2H carries both after a linearization)
   d_flag.alloc(1);
   d_tag_row.alloc(tag_row.size()); d_tag_row.upload(tag_row.data(), tag_row.size(), stream);
   d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
@@ -409,7 +410,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
 // Evaluate residuals/Jacobian at x: cost, gradient (unscaled), column norms
 // and the norms the minimizer reads.  Ceres EvaluateGradientAndJacobian.
 void arslam_lm::linearize_launch() {
-  h_lin.alloc(16);
+  h_lin.alloc(32);
   timers[PH_LIN].start(stream);
   arslam::launch_linearize(P, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
   arslam::launch_tag_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, stream);
@@ -421,22 +422,21 @@ void arslam_lm::linearize_launch() {
     allreduce(d_red.p, 4, ARSLAM_OP_SUM);   // cost, fixed, g_f, col_f
   }
   arslam::launch_camera_slots(P, d_red.p, d_g.p, d_colnorm.p, stream);
-  arslam::launch_slot_norms(P, d_g.p, x, d_norms.p, stream);
+  arslam::launch_slot_norms(P, d_g.p, x, d_norms_p, stream);
   if (nranks > 1) {
     // capture slots are disjoint across ranks, tag/camera slots replicated:
     // norms[0..2] cover captures (max, sum, sum), norms[3..5] the rest
-    allreduce(d_norms.p, 1, ARSLAM_OP_MAX);
-    allreduce(d_norms.p + 1, 2, ARSLAM_OP_SUM);
+    allreduce(d_norms_p, 1, ARSLAM_OP_MAX);
+    allreduce(d_norms_p + 1, 2, ARSLAM_OP_SUM);
   }
   timers[PH_LIN].stop(stream);
-  HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, stream));
-  HIP_CHECK(hipMemcpyAsync(h_lin.p + 4, d_norms.p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 22 * sizeof(double), hipMemcpyDeviceToHost, stream));
 }
 
 // (after a stream sync that covers linearize_launch)
 void arslam_lm::linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
                                   double *xnorm) {
-  const double *red = h_lin.p, *norms = h_lin.p + 4;
+  const double *red = h_lin.p, *norms = h_lin.p + 16;
   *x_cost = red[arslam::P_COST];
   *fixed_cost = red[arslam::P_FIXED];
   *gmax = std::max(norms[0], norms[3]);
@@ -674,7 +674,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     timers[PH_BACK].stop(stream);
     timers[PH_COST].start(stream);
     arslam::launch_cost(P, xc, d_parts.p, stream);
-    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream);
+    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p);
     if (nranks > 1) {
       // model change, capture step^2, candidate cost, fixed; flags by max
       allreduce(d_red.p + arslam::P_COST, 2, ARSLAM_OP_SUM);
@@ -683,12 +683,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     }
     timers[PH_COST].stop(stream);
     h_step.alloc(16);
-    HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 2) * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipMemcpyAsync(h_step.p + 15, d_flag.p, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 3) * sizeof(double), hipMemcpyDeviceToHost, stream));
     spin_sync();
     const double *red = h_step.p;
-    int flag = 0;
-    std::memcpy(&flag, h_step.p + 15, sizeof(int));
+    const int flag = (int)red[arslam::NPART + 2];   // the factorization flag (k_reduce_parts)
     for (int ph = PH_SCHUR; ph < PH_N; ++ph) timers[ph].collect();
     timing_collect();
     if (deferred && finalize()) {
