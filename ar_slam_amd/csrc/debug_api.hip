@@ -15,6 +15,7 @@ namespace arslam {
 void debug_read_schur_stamps(unsigned long long *out);
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,
                              const double *corners, double *r, double *J, hipStream_t s);
+void debug_angle_axis(int n, const double *w, const double *p, double *out, int *branch, hipStream_t s);
 }
 
 namespace {
@@ -51,6 +52,26 @@ extern "C" int arslam_debug_residual_jacobian(int n, const double *cam, const do
   (void)hipFree(d_in);
   (void)hipFree(d_r);
   (void)hipFree(d_J);
+  return ARSLAM_OK;
+}
+
+extern "C" int arslam_debug_angle_axis_rotate(int n, const double *w, const double *p, double *out,
+                                              int *branch) {
+  if (n < 0 || (n && (!w || !p || !out || !branch))) return ARSLAM_E_INVALID_ARG;
+  if (n == 0) return ARSLAM_OK;
+  double *d = nullptr;
+  int *d_b = nullptr;
+  DBG_CHECK(hipMalloc(&d, (size_t)n * 9 * sizeof(double)));
+  DBG_CHECK(hipMalloc(&d_b, (size_t)n * sizeof(int)));
+  DBG_CHECK(hipMemcpy(d, w, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice));
+  DBG_CHECK(hipMemcpy(d + 3L * n, p, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice));
+  arslam::debug_angle_axis(n, d, d + 3L * n, d + 6L * n, d_b, 0);
+  DBG_CHECK(hipGetLastError());
+  DBG_CHECK(hipDeviceSynchronize());
+  DBG_CHECK(hipMemcpy(out, d + 6L * n, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToHost));
+  DBG_CHECK(hipMemcpy(branch, d_b, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  (void)hipFree(d_b);
   return ARSLAM_OK;
 }
 

@@ -177,9 +177,11 @@ void launch_update_f(const DevProblem &P, const double *x, const double *scale, 
                      double *xc, double *fparts, hipStream_t s);
 void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_t s);
 // reduce per-capture partials [NPART][nc] (+ f-slot partials) into out[NPART]
-// (flag: also out[NPART + 2] = *flag)
+// (flag: also out[NPART + 2] = indefinite (flag > 0), out[NPART + 3] = executor
+// fault (flag < 0), out[NPART + 4] = the raw flag)
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts,
                          double *out, hipStream_t s, const int *flag = nullptr);
+void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, hipStream_t s);
 void launch_camera_slots(const DevProblem &P, const double *red, double *g, double *colnorm,
                          hipStream_t s);
 // norms over free parameter slots: out[0..2] = max|g|, sum g^2, sum x^2 over capture slots,

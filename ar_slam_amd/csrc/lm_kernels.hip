@@ -885,7 +885,12 @@ __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict_
     __syncthreads();
   }
   if (t == 0) out[p] = red[0];
-  if (flag && p == 0 && t == 0) out[NPART + 2] = (double)*flag;   // rides along the step's one D2H
+  if (flag && p == 0 && t == 0) {   // rides along the step's one D2H
+    const int f = *flag;
+    out[NPART + 2] = f > 0 ? 1.0 : 0.0;   // indefinite reduced system: an invalid LM step (max over ranks)
+    out[NPART + 3] = f < 0 ? 1.0 : 0.0;   // executor fault: an error, never a step (max over ranks)
+    out[NPART + 4] = (double)f;           // this rank's raw code, for the error message
+  }
 }
 
 // Norms over free parameter slots, split into capture slots (out[0..2]) and
@@ -968,6 +973,24 @@ __global__ void k_debug_rj(int n, const double *__restrict__ cam, const double *
   out[1] = 0.0;
   out[2] = 0.0;
   for (int j = 0; j < 12; ++j) out[3 + j] = j13[1 + j];
+}
+
+// AngleAxisRotatePoint of n (w, p) pairs with the branch each one took
+// (1: theta^2 > DBL_EPSILON, Rodrigues; 0: x + w x p) -- parity of the
+// small-angle branch, ar_slam_util.cpp:145,155.
+__global__ void k_debug_aa(int n, const double *__restrict__ w, const double *__restrict__ p,
+                           double *__restrict__ out, int *__restrict__ branch) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const AngleAxis a = aa_prepare(w + 3L * i);
+  aa_rotate(a, p + 3L * i, out + 3L * i);
+  branch[i] = a.big ? 1 : 0;
+}
+
+// test hook: S[row,row] = v after the LM diagonal was added (a forced
+// indefinite reduced system, arslam_lm_debug_force_indefinite)
+__global__ void k_debug_set_diag(DevProblem P, double *S, long row, double v) {
+  if (threadIdx.x == 0) *reduced_elem(S, P, row, row) = v;
 }
 
 size_t lds_rows(int maxk) { return (size_t)8 * maxk * kRowStride * sizeof(double); }
@@ -1066,6 +1089,14 @@ void debug_residual_jacobian(int n, const double *cam, const double *cap, const 
   const long m = 8L * n;
   hipLaunchKernelGGL(k_debug_rj, dim3((unsigned)((m + 127) / 128)), dim3(128), 0, s, n, cam, cap, tag,
                      corners, r, J);
+}
+
+void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, hipStream_t s) {
+  hipLaunchKernelGGL(k_debug_set_diag, dim3(1), dim3(64), 0, s, P, S, row, v);
+}
+
+void debug_angle_axis(int n, const double *w, const double *p, double *out, int *branch, hipStream_t s) {
+  hipLaunchKernelGGL(k_debug_aa, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, n, w, p, out, branch);
 }
 
 }  // namespace arslam

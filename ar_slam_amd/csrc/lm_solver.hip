@@ -8,6 +8,7 @@
 // problem, the parameters and the reduced system stay resident in HBM.
 #include "lm_internal.h"
 #include "arslam_lm.h"
+#include "arslam_lm_debug.h"
 
 #include <rccl/rccl.h>
 
@@ -47,6 +48,20 @@ using Error = arslam::ApiError;
 
 void fail_if(bool cond, int code, const std::string &msg) {
   if (cond) throw Error(code, msg);
+}
+
+// decode the persistent executors' negative flags (dense_llt.hip)
+std::string executor_fault_message(int code, int rank, int iteration) {
+  std::string what;
+  const int c = -code;
+  if (code == 0) what = "on another rank";
+  else if (c >= 4000000) what = "backward-solve column " + std::to_string(c - 4000000) + ": dependency wait timed out";
+  else if (c >= 3000000) what = "ticket " + std::to_string(c - 3000000) + ": fused TRSM late wait timed out";
+  else if (c >= 2000000) what = "ticket " + std::to_string(c - 2000000) + ": in-order update wait timed out";
+  else if (c >= 1000000) what = "ticket " + std::to_string(c - 1000000) + ": dependency wait timed out";
+  else what = "code " + std::to_string(code);
+  return "reduced-system executor fault (rank " + std::to_string(rank) + ", LM iteration " +
+         std::to_string(iteration) + "): " + what;
 }
 
 double now_s() {
@@ -164,6 +179,7 @@ struct arslam_lm {
   DevBuf<arslam::SchurContrib> d_contrib;
   arslam::LltPlan plan;
   double *x = nullptr, *xc = nullptr;
+  unsigned long long dbg_indefinite_mask = 0;   // arslam_lm_debug_force_indefinite
   int n_fparts = 0;
 
   Timer timers[PH_N];
@@ -259,7 +275,7 @@ struct arslam_lm {
   void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
   PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [16..21] slot norms
   PinnedBuf h_x;     // [n] parameter download (write_back)
-  PinnedBuf h_step;  // [0..NPART+1] the step's reduced scalars, [NPART+2] the factorization flag
+  PinnedBuf h_step;  // [0..NPART+1] the step's reduced scalars, [NPART+2..4] the factorization flags
   hipEvent_t ev_sync = nullptr;
   // Wait for the stream by polling an event: the LM loop's one host round
   // trip per step, without the blocking-sync wake-up latency.
@@ -598,6 +614,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream);
       if (nranks > 1) allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ARSLAM_OP_SUM);
       arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
+      if (dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull)   // test hook
+        arslam::debug_set_reduced_diag(P, d_S.p, P.cam_row >= 0 ? P.cam_row : nR - 1, -1.0, stream);
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
       timing_begin();
@@ -680,13 +698,18 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       allreduce(d_red.p + arslam::P_COST, 2, ARSLAM_OP_SUM);
       allreduce(d_red.p + arslam::P_MODEL, 2, ARSLAM_OP_SUM);
       allreduce(d_red.p + arslam::P_YBAD, 2, ARSLAM_OP_MAX);
+      // f-side non-finite step, indefinite, executor fault: every rank takes the same branch
+      allreduce(d_red.p + arslam::NPART + 1, 3, ARSLAM_OP_MAX);
     }
     timers[PH_COST].stop(stream);
     h_step.alloc(16);
-    HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 3) * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 5) * sizeof(double), hipMemcpyDeviceToHost, stream));
     spin_sync();
     const double *red = h_step.p;
-    const int flag = (int)red[arslam::NPART + 2];   // the factorization flag (k_reduce_parts)
+    // A stuck dependency wait of a persistent executor is a device fault, not
+    // an indefinite system: fail loudly instead of shrinking the radius.
+    if (red[arslam::NPART + 3] != 0.0)
+      throw Error(ARSLAM_E_DEVICE, executor_fault_message((int)red[arslam::NPART + 4], rank, it.iteration));
     for (int ph = PH_SCHUR; ph < PH_N; ++ph) timers[ph].collect();
     timing_collect();
     if (deferred && finalize()) {
@@ -694,9 +717,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       break;
     }
 
-    const bool lin_fail = flag != 0;
-    if (lin_fail && std::getenv("ARSLAM_DEBUG_FLAG"))   // debug: factorization failure code
-      std::fprintf(stderr, "arslam: factorization flag %d at iteration %d\n", flag, it.iteration);
+    const bool lin_fail = red[arslam::NPART + 2] != 0.0;   // LLT failure: Ceres' invalid step
     const bool ybad = red[arslam::P_YBAD] != 0.0 || red[arslam::NPART + 1] != 0.0;
     const double model_cost_change = red[arslam::P_MODEL];
     const bool valid = !lin_fail && !ybad && model_cost_change > 0.0;
@@ -1045,6 +1066,30 @@ int arslam_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int arslam_lm_debug_force_indefinite(arslam_lm *h, unsigned long long step_mask) {
+  if (!h) return ARSLAM_E_INVALID_ARG;
+  h->dbg_indefinite_mask = step_mask;
+  return ARSLAM_OK;
+}
+
+int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken) {
+  if (!h || ticket < 0) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    fail_if(!h->loaded || !h->has_f || h->opt.factor_executor != 1, ARSLAM_E_STATE,
+            "break_dependency needs a loaded problem on the persistent executor");
+    arslam::LltPlan &pl = h->plan;
+    long t = ticket;
+    while (t < pl.n_dag_tasks && pl.h_dag_wait_off[t] == pl.h_dag_wait_off[t + 1]) ++t;
+    fail_if(t >= pl.n_dag_tasks, ARSLAM_E_INVALID_ARG, "no task at or after this ticket waits on anything");
+    const int w = pl.h_dag_wait_off[t];
+    pl.h_dag_waits[w].y += 1 << 28;   // a count no task ever reaches
+    HIP_CHECK(hipMemcpyAsync(pl.dag_waits + w, &pl.h_dag_waits[w], sizeof(int2), hipMemcpyHostToDevice,
+                             h->stream));
+    HIP_CHECK(hipStreamSynchronize(h->stream));
+    if (broken) *broken = t;
+  });
 }
 
 const char *arslam_lm_last_error(void) { return g_last_error.c_str(); }

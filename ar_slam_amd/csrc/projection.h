@@ -27,10 +27,18 @@ struct AngleAxis {
   bool big;
 };
 
+// theta^2 exactly as rotation.h evaluates it on x86-64 (three rounded
+// products, two rounded sums, no FMA): the branch test theta^2 > DBL_EPSILON
+// must pick the same side as the reference for draws within an ulp of it.
+__device__ __forceinline__ double aa_theta2(const double *w) {
+#pragma clang fp contract(off)
+  return w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+}
+
 __device__ __forceinline__ AngleAxis aa_prepare(const double *w) {
   AngleAxis a;
   a.w[0] = w[0]; a.w[1] = w[1]; a.w[2] = w[2];
-  a.th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  a.th2 = aa_theta2(w);
   a.big = a.th2 > DBL_EPSILON;
   if (a.big) {
     a.th = sqrt(a.th2);

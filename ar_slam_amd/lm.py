@@ -33,7 +33,7 @@ RULES = {0: "none", 1: "gradient_tolerance", 2: "parameter_tolerance", 3: "funct
          4: "min_trust_region_radius", 5: "max_num_iterations", 6: "invalid_steps",
          7: "evaluation_failed"}
 ERRORS = {-1: "INVALID_ARG", -2: "UNSUPPORTED", -3: "NO_DEVICE", -4: "HIP", -5: "OUT_OF_MEMORY",
-          -6: "COMM", -7: "STATE"}
+          -6: "COMM", -7: "STATE", -8: "DEVICE"}
 
 # Every symbol include/arslam_lm.h declares (checked by the CPU tests).
 EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
@@ -44,6 +44,8 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm", "arslam_lm_set_comm_callback",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
+           "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
+           "arslam_lm_debug_break_dependency",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
@@ -187,6 +189,9 @@ def lib():
     L.arslam_lm_version.restype = C.c_char_p
     L.arslam_debug_residual_jacobian.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp, _dp]
     L.arslam_debug_dense_llt.argtypes = [C.c_long, _dp, _dp, _dp, C.POINTER(C.c_int)]
+    L.arslam_debug_angle_axis_rotate.argtypes = [C.c_int, _dp, _dp, _dp, _ip]
+    L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
+    L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
     _lib = L
     return L
 
@@ -272,6 +277,11 @@ class _Handle:
         _check(lib().arslam_lm_get_options(self._h, C.byref(o)))
         return o
 
+    def debug_force_indefinite(self, step_mask):
+        """Test hook: linear solves whose bit min(i,63) is set in step_mask see an indefinite
+        reduced system (camera diagonal -1), i.e. an invalid LM step."""
+        _check(lib().arslam_lm_debug_force_indefinite(self._h, C.c_ulonglong(step_mask & (2**64 - 1))))
+
     def set_comm(self, rank, nranks, uid):
         """Join the ranks' exchange: ``uid`` is an RCCL unique id (bytes, one GPU per
         rank) or a host all-reduce ``fn(array, op)`` reducing a numpy array in place
@@ -314,6 +324,12 @@ class ResidentProblem(_Handle):
         s = Summary()
         _check(lib().arslam_lm_solve_loaded(self._h, C.byref(s)))
         return s.to_dict()
+
+    def debug_break_dependency(self, ticket):
+        """Test hook: make one dependency wait of the factorization task graph unreachable."""
+        out = C.c_long(-1)
+        _check(lib().arslam_lm_debug_break_dependency(self._h, ticket, C.byref(out)))
+        return out.value
 
     @property
     def camera(self):
@@ -383,6 +399,18 @@ def debug_residual_jacobian(cam, cap, tag, corners):
                                                 tag.ctypes.data_as(_dp), corners.ctypes.data_as(_dp),
                                                 r.ctypes.data_as(_dp), J.ctypes.data_as(_dp)))
     return r, J
+
+
+def debug_angle_axis_rotate(w, p):
+    """Device AngleAxisRotatePoint of n points: (out (n,3), branch (n,) 1 = Rodrigues, 0 = small angle)."""
+    w = _f64(w, (-1, 3))
+    p = _f64(p, (-1, 3))
+    n = w.shape[0]
+    out = np.zeros((n, 3))
+    br = np.zeros(n, np.int32)
+    _check(lib().arslam_debug_angle_axis_rotate(n, w.ctypes.data_as(_dp), p.ctypes.data_as(_dp),
+                                                out.ctypes.data_as(_dp), br.ctypes.data_as(_ip)))
+    return out, br
 
 
 def debug_dense_llt(A, b, executor=0):

@@ -45,7 +45,8 @@ enum {
   ARSLAM_E_HIP = -4,
   ARSLAM_E_OUT_OF_MEMORY = -5,
   ARSLAM_E_COMM = -6,
-  ARSLAM_E_STATE = -7
+  ARSLAM_E_STATE = -7,
+  ARSLAM_E_DEVICE = -8          /* a device executor fault (a dependency wait that never completed) */
 };
 
 /* which side of the camera/tag graph the Schur complement eliminates */

@@ -19,6 +19,12 @@ extern "C" {
 int arslam_debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,
                                    const double *corners, double *r, double *J);
 
+/* ceres::AngleAxisRotatePoint (rotation.h; called at ar_slam_util.cpp:145,155)
+ * of n points p[n*3] by angle-axis w[n*3] on the device -> out[n*3], and the
+ * branch each took: branch[i] = 1 if theta^2 > DBL_EPSILON (Rodrigues), 0 for
+ * the first-order form x + w x p. */
+int arslam_debug_angle_axis_rotate(int n, const double *w, const double *p, double *out, int *branch);
+
 /* Dense reduced-system solve on the device: factor the lower triangle of the
  * n x n row-major SPD matrix A (in place: on return A holds L) and solve
  * A y = b.  *info = 0 on success, k+1 if pivot k was not positive. */
@@ -53,6 +59,20 @@ typedef struct {
 /* diagnostic builds only (-DARSLAM_SCHUR_STAMPS): per-phase cycles of the
  * Schur kernel accumulated over all its waves (zeros otherwise) */
 int arslam_debug_schur_stamps(unsigned long long out[16]);
+
+/* Test hooks on a solver handle.
+ * force_indefinite: at every linear solve i (0-based) whose bit
+ * min(i, 63) is set in step_mask, the reduced system's first camera row
+ * (the last row if the camera is constant) gets diagonal -1 after the LM
+ * diagonal is added, so the Cholesky reports a failed pivot and the LM step
+ * is invalid (Ceres' LinearSolver FAILURE path).  0 turns it off.
+ * break_dependency: on a problem loaded by arslam_lm_load_soa with the
+ * persistent executor, raise the first wait of the first task at or after
+ * `ticket` that has one beyond any count it can reach; the next solve must
+ * then fail with ARSLAM_E_DEVICE.  *broken = the task changed.  Load again
+ * to repair. */
+int arslam_lm_debug_force_indefinite(arslam_lm *h, unsigned long long step_mask);
+int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken);
 
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);

@@ -52,6 +52,7 @@ void or_default_options(or_options *o) {
   o->elimination = OR_ELIM_CAPTURES;
   o->num_threads = 1;
   o->progress = 0;
+  o->debug_indefinite_mask = 0;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -330,6 +331,7 @@ typedef struct {
   double *y;          /* solution of (Jt'Jt + D^2) y = Jt' r */
   double *delta;
   int nthreads;
+  int dbg_indefinite;   /* test hook for this linear solve (or_options.debug_indefinite_mask) */
 } lm_t;
 
 static inline long slot_cam(void) { return 0; }
@@ -567,6 +569,7 @@ static int solve_schur(lm_t *L, const double *D2) {
   for (int t = 0; t < L->nt; ++t)
     for (int j = 0; j < 6; ++j) L->S[(fidx_tag(t) + j) * (ld + 1)] += D2[slot_tag(L, t) + j];
   for (int j = 0; j < 3; ++j) L->S[(fidx_cam(L) + j) * (ld + 1)] += D2[slot_cam() + j];
+  if (L->dbg_indefinite) L->S[fidx_cam(L) * (ld + 1)] = -1.0;   /* test hook */
 
   if (or_llt_lower(L->S, nF, ld, L->nthreads) != 0) return 1;
   double *yF = malloc(sizeof(double) * nF);
@@ -634,6 +637,7 @@ static int solve_full(lm_t *L, const double *D2) {
     }
   }
   for (long s = 0; s < n; ++s) L->S[s * (n + 1)] += D2[s];
+  if (L->dbg_indefinite) L->S[slot_cam() * (n + 1)] = -1.0;   /* test hook */
   if (or_llt_lower(L->S, n, n, L->nthreads) != 0) return 1;
   memcpy(L->y, L->rhs, n * sizeof(double));
   llt_solve(L->S, n, n, L->y);
@@ -804,6 +808,7 @@ int or_solve(or_problem *p, const or_options *o, or_summary *s, const or_comm *c
       D2[k] = dk * dk;
     }
     s->num_linear_solves++;
+    L.dbg_indefinite = (int)((o->debug_indefinite_mask >> (s->num_linear_solves - 1 < 63 ? s->num_linear_solves - 1 : 63)) & 1ull);
     int lin_fail = (o->elimination == OR_ELIM_NONE) ? solve_full(&L, D2) : solve_schur(&L, D2);
     reuse_diag = 1;
     double model_cost_change = 0.0;

@@ -61,6 +61,11 @@ typedef struct {
   int elimination;                     /* OR_ELIM_CAPTURES | OR_ELIM_NONE */
   int num_threads;                     /* OpenMP threads for the dense LLT (1 = reference) */
   int progress;                        /* print the Ceres progress table */
+  /* test hook (not a Ceres option): at linear solve i (0-based) with bit
+   * min(i,63) set, the reduced system's first camera row gets diagonal -1
+   * after D_f^2 is added, so its LLT fails and the step is invalid -- the
+   * same hook as the device's arslam_lm_debug_force_indefinite. */
+  unsigned long long debug_indefinite_mask;
 } or_options;
 
 typedef struct {

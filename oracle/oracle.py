@@ -44,7 +44,8 @@ class Options(C.Structure):
                 ("min_lm_diagonal", C.c_double), ("max_lm_diagonal", C.c_double),
                 ("max_num_consecutive_invalid_steps", C.c_int),
                 ("jacobi_scaling", C.c_int), ("elimination", C.c_int),
-                ("num_threads", C.c_int), ("progress", C.c_int)]
+                ("num_threads", C.c_int), ("progress", C.c_int),
+                ("debug_indefinite_mask", C.c_ulonglong)]
 
 
 class Iter(C.Structure):

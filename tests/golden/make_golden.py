@@ -7,7 +7,9 @@ fixtures are oracle outputs on seeded synthetic inputs:
                          cross-checked in tests against torch-fp64 autograd;
   * lm_<cfg>.json     -- LM traces (cost, radius, rho, step per iteration),
                          termination and final state summaries.
-Usage: python tests/golden/make_golden.py [cfg ...]   (default: tiny small medium cfg2)
+  * lm_ctl_<name>.json -- Ceres control-flow traces (CONTROL below): rejected
+                         and invalid steps, every termination rule;
+Usage: python tests/golden/make_golden.py [cfg ... | control | ctl_<name> ... | loc | kat]   (default: tiny small medium cfg2)
 """
 import json
 import os
@@ -47,6 +49,62 @@ def jacobian_kat(n=256, seed=5):
                         corners=corners, r=r, J=J)
 
 
+# Ceres control-flow traces: each names a graph (config
+# + generator overrides) and solver options chosen so that one branch of the
+# trust-region loop fires -- rejected steps (hard initial states, f0 = 3000,
+# the reference default ar_slam_util.hpp:69), each termination rule, invalid
+# steps through the forced-indefinite test hook, and FAILURE after more than
+# max_num_consecutive_invalid_steps of them.
+HARD = dict(init_trans_sigma=0.15, init_rot_sigma=0.25, f_init=3000.0)
+HARD_M = dict(init_trans_sigma=0.12, init_rot_sigma=0.22, f_init=3000.0)
+ALL_STEPS = 2 ** 64 - 1
+CONTROL = {
+    "tiny_reject": ("tiny", HARD, {}),
+    "small_reject": ("small", HARD, {}),
+    "medium_reject": ("medium", HARD_M, {}),
+    "cfg2_reject": ("cfg2", HARD_M, {}),
+    "small_min_radius": ("small", HARD, {"min_trust_region_radius": 100.0}),
+    "small_max_iters": ("small", {}, {"max_num_iterations": 3}),
+    "small_parameter": ("small", {}, {"function_tolerance": 0.0}),
+    "medium_parameter": ("medium", {}, {"function_tolerance": 0.0}),
+    "small_gradient": ("small", {}, {"function_tolerance": 0.0, "parameter_tolerance": 0.0,
+                                     "gradient_tolerance": 1e-4}),
+    "medium_gradient": ("medium", {}, {"function_tolerance": 0.0, "parameter_tolerance": 0.0,
+                                       "gradient_tolerance": 1e-4}),
+    "small_invalid": ("small", {}, {"debug_indefinite_mask": 0b110}),
+    "medium_invalid": ("medium", {}, {"debug_indefinite_mask": 0b1010}),
+    "tiny_failure": ("tiny", {}, {"debug_indefinite_mask": ALL_STEPS}),
+    "small_failure": ("small", {}, {"debug_indefinite_mask": ALL_STEPS}),
+}
+
+
+def control_trace(name, threads=8):
+    cfg, gkw, opts = CONTROL[name]
+    g = synth.config_graph(cfg, **gkw)
+    cam, cap, tag, s = O.solve_graph(g, num_threads=threads, **opts)
+    its = s["iterations"]
+    out = {"control": name, "config": cfg, "graph": gkw, "options": opts,
+           "n_cap": g.n_cap, "n_tag": g.n_tag, "n_obs": g.n_obs,
+           "termination": s["termination"], "rule": s["rule"],
+           "num_linear_solves": s["num_linear_solves"],
+           "num_successful_steps": s["num_successful_steps"],
+           "num_unsuccessful_steps": s["num_unsuccessful_steps"],
+           "initial_cost": s["initial_cost"], "final_cost": s["final_cost"], "final_focal": cam[0]}
+    for k in ("cost", "cost_change", "trust_region_radius", "relative_decrease", "step_norm",
+              "gradient_max_norm", "step_is_valid", "step_is_successful"):
+        out[k] = [it[k] for it in its]
+    # The same solve with no Schur elimination (the oracle's full normal
+    # equations): a second exact arithmetic, whose distance from the Schur
+    # trace measures how strongly this trajectory amplifies rounding.  The GPU
+    # test allows the device a multiple of it (and never less than 1e-9).
+    _, _, _, alt = O.solve_graph(g, num_threads=threads, elimination=1, **opts)
+    assert [it["step_is_successful"] for it in alt["iterations"]] == out["step_is_successful"], name
+    out["alt_cost"] = [it["cost"] for it in alt["iterations"]]
+    out["alt_trust_region_radius"] = [it["trust_region_radius"] for it in alt["iterations"]]
+    with open(os.path.join(HERE, f"lm_ctl_{name}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def lm_trace(name, threads=8):
     g = synth.config_graph(name)
     cam, cap, tag, s = O.solve_graph(g, num_threads=threads)
@@ -84,6 +142,11 @@ def localize_golden(n_query=4096):
 
 if __name__ == "__main__":
     names = sys.argv[1:] or ["tiny", "small", "medium", "cfg2"]
+    ctl = list(CONTROL) if "control" in names else [n[4:] for n in names if n.startswith("ctl_")]
+    for n in ctl:
+        control_trace(n)
+        print("wrote control", n)
+    names = [n for n in names if n != "control" and not n.startswith("ctl_")]
     if "loc" in names:
         localize_golden()
         print("wrote loc")

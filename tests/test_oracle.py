@@ -114,6 +114,48 @@ def test_golden_lm_traces(oracle, name):
     assert cam[0] == pytest.approx(gold["final_focal"], rel=1e-12)
 
 
+CONTROL_EXPECT = {   # the branch of Ceres' trust-region loop each control trace pins
+    "tiny_reject": ("CONVERGENCE", "function_tolerance"),
+    "small_reject": ("CONVERGENCE", "function_tolerance"),
+    "medium_reject": ("CONVERGENCE", "function_tolerance"),
+    "cfg2_reject": ("CONVERGENCE", "function_tolerance"),
+    "small_min_radius": ("CONVERGENCE", "min_trust_region_radius"),
+    "small_max_iters": ("NO_CONVERGENCE", "max_num_iterations"),
+    "small_parameter": ("CONVERGENCE", "parameter_tolerance"),
+    "medium_parameter": ("CONVERGENCE", "parameter_tolerance"),
+    "small_gradient": ("CONVERGENCE", "gradient_tolerance"),
+    "medium_gradient": ("CONVERGENCE", "gradient_tolerance"),
+    "small_invalid": ("CONVERGENCE", "function_tolerance"),
+    "medium_invalid": ("CONVERGENCE", "function_tolerance"),
+    "tiny_failure": ("FAILURE", "invalid_steps"),
+    "small_failure": ("FAILURE", "invalid_steps"),
+}
+
+
+@pytest.mark.parametrize("name", [n for n in CONTROL_EXPECT if not n.startswith("cfg2")])
+def test_golden_control_traces(oracle, name):
+    """The oracle reproduces its committed control-flow traces, and each trace exercises the
+    branch it is named for (rejected steps, invalid steps, each termination rule)."""
+    with open(os.path.join(GOLDEN, f"lm_ctl_{name}.json")) as f:
+        gold = json.load(f)
+    assert (gold["termination"], gold["rule"]) == CONTROL_EXPECT[name]
+    if "reject" in name or "min_radius" in name:
+        assert 0 in gold["step_is_successful"][1:] and all(gold["step_is_valid"])
+    if "invalid" in name or "failure" in name:
+        assert 0 in gold["step_is_valid"]
+    if "failure" in name:   # Ceres aborts on the (max_num_consecutive_invalid_steps + 1)-th
+        assert gold["step_is_valid"][-5:] == [0] * 5
+    g = synth.config_graph(gold["config"], **gold["graph"])
+    cam, cap, tag, s = oracle.solve_graph(g, **gold["options"])
+    assert (s["termination"], s["rule"]) == (gold["termination"], gold["rule"])
+    its = s["iterations"]
+    assert [it["step_is_successful"] for it in its] == gold["step_is_successful"]
+    assert [it["step_is_valid"] for it in its] == gold["step_is_valid"]
+    np.testing.assert_allclose([it["cost"] for it in its], gold["cost"], rtol=1e-12)
+    np.testing.assert_allclose([it["trust_region_radius"] for it in its], gold["trust_region_radius"],
+                               rtol=1e-12)
+
+
 @pytest.mark.parametrize("name", ["tiny", "small"])
 def test_schur_step_equals_full_normal_equations(oracle, name):
     """Eliminating captures (DENSE_SCHUR) gives the LM step of the full system."""
