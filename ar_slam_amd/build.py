@@ -14,7 +14,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "libarslam_lm.so")
+LIB = os.environ.get("ARSLAM_LIB") or os.path.join(HERE, "libarslam_lm.so")   # (override: variant builds)
 SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "debug_api.hip", "llt_plan.cpp",
            "host_structure.cpp", "localize.hip"]
 HOST = os.path.join(HERE, "host")
@@ -39,9 +39,23 @@ def _stale():
 
 
 def build(force=False, verbose=False):
+    """Compile libarslam_lm.so if any source is newer.  Safe under concurrent callers (torchrun
+    ranks): one process builds behind an exclusive file lock while the others wait, and the
+    library is written to a private path and renamed into place, so a reader never maps a
+    half-written file."""
     if not force and not _stale():
         return LIB
-    objdir = os.path.join(HERE, "_obj")
+    import fcntl
+    with open(os.path.join(HERE, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not force and not _stale():   # another process built it while we waited
+            return LIB
+        return _build_locked(verbose)
+
+
+def _build_locked(verbose):
+    extra = os.environ.get("ARSLAM_EXTRA_FLAGS", "")
+    objdir = os.path.join(HERE, "_obj" + ("_" + "".join(c for c in extra if c.isalnum()) if extra else ""))
     os.makedirs(objdir, exist_ok=True)
     flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC] + \
@@ -72,9 +86,11 @@ def build(force=False, verbose=False):
             print(out.decode())
     if errs:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", LIB] + objs + \
+    tmp = f"{LIB}.tmp{os.getpid()}"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", tmp] + objs + \
           ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
     return LIB
 
 

@@ -207,30 +207,43 @@ __device__ __forceinline__ double rowbcast(double v, int g) {
 // One elimination step of diag16 under an explicit exec mask (constant per
 // pivot, so no per-lane selects): in the rows below the pivot,
 // x_q += nf * xj_q and R += nf * rj; then, in the pivot column's group,
-// register jq becomes nf.  The caller's exec is restored at the end, and the
-// trailing s_nop covers the wait states hipcc does not insert after an asm
-// statement (exec write -> DPP, and the outputs -> the next pivot's DPP).
+// register jq becomes nf.  The masks are 32-bit immediates per exec half
+// (both halves of `below` are equal), so no SGPR pair holds a 64-bit mask
+// constant across the unrolled pivots (those used to be spilled to VGPR lanes
+// and reloaded with v_readlane inside the chain).  The caller's exec is
+// restored at the end, and the trailing s_nop covers the wait states hipcc
+// does not insert after an asm statement (exec write -> DPP, and the outputs
+// -> the next pivot's DPP).
+template <int j>
 __device__ __forceinline__ void elim_step(double &x0, double &x1, double &x2, double &x3, double &R, double nf,
-                                          double y0, double y1, double y2, double y3, double rj,
-                                          unsigned long long below, unsigned long long colj, int jq) {
-  unsigned long long sv;
+                                          double y0, double y1, double y2, double y3, double rj) {
+  constexpr unsigned m = (0xffffu << (j + 1)) & 0xffffu;   // rows i > j of one 16-lane group
+  constexpr unsigned BL = m | (m << 16);                    // `below`, per exec half
+  constexpr int g = j >> 2;                                 // the group holding column j
+  constexpr unsigned CL = g == 0 ? m : g == 1 ? (m << 16) : 0u;
+  constexpr unsigned CH = g == 2 ? m : g == 3 ? (m << 16) : 0u;
+  unsigned sl, sh;
 #define ARSLAM_ELIM_ASM(XS)                                                                   \
-  asm volatile("s_mov_b64 %[sv], exec\n\t"                                                    \
-               "s_and_b64 exec, %[sv], %[below]\n\t"                                          \
+  asm volatile("s_mov_b32 %[sl], exec_lo\n\t"                                                 \
+               "s_mov_b32 %[sh], exec_hi\n\t"                                                 \
+               "s_and_b32 exec_lo, %[sl], %[bl]\n\t"                                          \
+               "s_and_b32 exec_hi, %[sh], %[bl]\n\t"                                          \
                "v_fma_f64 %[x0], %[nf], %[y0], %[x0]\n\t"                                     \
                "v_fma_f64 %[x1], %[nf], %[y1], %[x1]\n\t"                                     \
                "v_fma_f64 %[x2], %[nf], %[y2], %[x2]\n\t"                                     \
                "v_fma_f64 %[x3], %[nf], %[y3], %[x3]\n\t"                                     \
                "v_fma_f64 %[R], %[nf], %[rj], %[R]\n\t"                                       \
-               "s_and_b64 exec, %[sv], %[colj]\n\t"                                           \
+               "s_and_b32 exec_lo, %[sl], %[cl]\n\t"                                          \
+               "s_and_b32 exec_hi, %[sh], %[ch]\n\t"                                          \
                "v_mov_b64 %[" XS "], %[nf]\n\t"                                               \
-               "s_mov_b64 exec, %[sv]\n\t"                                                    \
+               "s_mov_b32 exec_lo, %[sl]\n\t"                                                 \
+               "s_mov_b32 exec_hi, %[sh]\n\t"                                                 \
                "s_nop 4"   /* exec write -> DPP: 5 states; VGPR write -> DPP read: 2 */        \
                : [x0] "+v"(x0), [x1] "+v"(x1), [x2] "+v"(x2), [x3] "+v"(x3), [R] "+v"(R),      \
-                 [sv] "=&s"(sv)                                                                \
+                 [sl] "=&s"(sl), [sh] "=&s"(sh)                                                \
                : [nf] "v"(nf), [y0] "v"(y0), [y1] "v"(y1), [y2] "v"(y2), [y3] "v"(y3),          \
-                 [rj] "v"(rj), [below] "s"(below), [colj] "s"(colj))
-  switch (jq) {
+                 [rj] "v"(rj), [bl] "i"(BL), [cl] "i"(CL), [ch] "i"(CH))
+  switch (j & 3) {
     case 0: ARSLAM_ELIM_ASM("x0"); break;
     case 1: ARSLAM_ELIM_ASM("x1"); break;
     case 2: ARSLAM_ELIM_ASM("x2"); break;
@@ -257,9 +270,7 @@ __device__ __forceinline__ void diag16_pivot(double (&x)[4], double &R, double &
   R = R2;
   // rows i > j only (exec = the lanes 16 g + i with i > j, a constant per
   // pivot); then column j of those rows (group j / 4) becomes -f_ij
-  const unsigned long long below = 0x0001000100010001ull * ((0xffffull << (j + 1)) & 0xffffull);
-  const unsigned long long colj = below & (0xffffull << (16 * (j >> 2)));
-  elim_step(x[0], x[1], x[2], x[3], R, nf, xj[0], xj[1], xj[2], xj[3], rj, below, colj, j & 3);
+  elim_step<j>(x[0], x[1], x[2], x[3], R, nf, xj[0], xj[1], xj[2], xj[3], rj);
   if (j + 2 < 16) {   // column j+2 after this pivot, a pivot before it is needed
     colx[lane] = x[(j + 2) & 3];
     R2 = colx[16 * ((j + 2) >> 2) + i];
@@ -838,10 +849,6 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [5] fused TRSM tile prefetched
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
   double *colx = LTd + 4 * 16 * LI + 4;   // POTRF pivot scratch (X stays free for the prefetch)
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, lane = tid & 63;
-  const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
-  const int li = lane & 15, lk = lane >> 4;
   int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.counters + 2 * a.n_tiles;
   // Continuation targets stay ordinary tickets with a claim flag.  The
   // predecessor's workgroup claims its target (before publishing the tile the
@@ -851,6 +858,14 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // workgroup that drew the target claims and runs it once its waits are met.
   int next = -1;
   for (;;) {
+    // thread coordinates re-derived per task from a laundered threadIdx: the
+    // per-lane LDS/tile addresses of every task type are then computed where
+    // they are used instead of being hoisted out of the loop and spilled
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int w = tid >> 6, lane = tid & 63;
+    const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
+    const int li = lane & 15, lk = lane >> 4;
     const bool cont = next >= 0;
     if (!cont) {
       if (tid == 0) sh[0] = atomicAdd(ticket, 1);
@@ -940,12 +955,14 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           met = __builtin_amdgcn_ballot_w64(q < pw1 && got < cv.y) == 0;
         }
         if (met) {
+          int lnl = ln;   // laundered: the 32 prefetch addresses are formed here, not hoisted and spilled
+          asm volatile("" : "+v"(lnl));
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const double *p8[8];
             dbl2 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * ((g * 8 + u) * 64 + ln);
+            for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * ((g * 8 + u) * 64 + lnl);
             ld_wt16x8(p8, v);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -1147,7 +1164,10 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     __builtin_amdgcn_s_setprio(0);
     if (a.trace && tid == 0) a.trace[8L * t + 2] = realtime();
   }
-  DAG_PROGRESS(1, 9);
+  {
+    const int tid = threadIdx.x;
+    DAG_PROGRESS(1, 9);
+  }
 }
 
 // z[j] = L[nR][j], the forward-substituted right-hand side: from S for the

@@ -6,6 +6,8 @@
 #include "host_structure.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -50,6 +52,20 @@ int peripheral(int start, const std::vector<std::vector<int>> &adj, const std::v
     best = far;
   }
   return best;
+}
+
+double nd_beta() {   // (ARSLAM_ND_BETA: tuning knob, debug)
+  static const double b = std::getenv("ARSLAM_ND_BETA") ? std::atof(std::getenv("ARSLAM_ND_BETA")) : 0.6;
+  return b;
+}
+
+// Elimination-tree height, in tile columns, of a dissection step: the
+// separator's tiles plus the larger child's height, which grows about as
+// sqrt(size) on these planar co-visibility graphs (cfg3: ~1 tile column per
+// sqrt(tag) at the root); balance only breaks ties.
+double height_score(long ssz, long na, long nb) {
+  return std::ceil(6.0 * ssz / kTileRows) + nd_beta() * std::sqrt((double)std::max(na, nb)) +
+         1e-6 * std::labs(na - nb);
 }
 
 struct Dissector {
@@ -101,10 +117,83 @@ struct Dissector {
     return true;
   }
 
+  // Minimum vertex cover of the cut's bipartite graph (side-1 boundary nodes
+  // x side-2 boundary nodes, the cut edges), by augmenting paths and König's
+  // construction: the smallest vertex separator that removes every cut edge
+  // while keeping the remaining nodes on their sides.  On the co-visibility
+  // graph (edges span up to ~3 tag spacings) it is often well below either
+  // one-sided boundary.  cover[u] = 1 for the chosen nodes of comp.
+  int konig_cover(const std::vector<int> &comp, const std::vector<int> &side, int tag,
+                  std::vector<char> &cover) {
+    std::vector<int> left, right;
+    for (int u : comp) {
+      bool bd = false;
+      for (int v : adj[u])
+        if (mark[v] == tag && side[v] != side[u]) { bd = true; break; }
+      if (bd) (side[u] == 1 ? left : right).push_back(u);
+    }
+    std::vector<int> idx(0);
+    // local numbering: left 0..nl-1, right nl..
+    const int nl = (int)left.size(), nr = (int)right.size();
+    for (int i = 0; i < nl; ++i) lev[left[i]] = i;
+    for (int i = 0; i < nr; ++i) lev[right[i]] = nl + i;
+    std::vector<std::vector<int>> g(nl);
+    for (int i = 0; i < nl; ++i)
+      for (int v : adj[left[i]])
+        if (mark[v] == tag && side[v] == 2) g[i].push_back(lev[v] - nl);
+    std::vector<int> mate_l(nl, -1), mate_r(nr, -1), seen(nr, -1);
+    // Kuhn's augmenting paths (iterative DFS), greedy initial matching
+    for (int i = 0; i < nl; ++i)
+      for (int r : g[i])
+        if (mate_r[r] < 0) { mate_l[i] = r; mate_r[r] = i; break; }
+    std::vector<std::pair<int, int>> st;
+    std::vector<int> par_r(nr, -1);
+    for (int i0 = 0; i0 < nl; ++i0) {
+      if (mate_l[i0] >= 0) continue;
+      st.assign(1, {i0, 0});
+      int found = -1;
+      while (!st.empty() && found < 0) {
+        auto &[i, k] = st.back();
+        if (k >= (int)g[i].size()) { st.pop_back(); continue; }
+        const int r = g[i][k++];
+        if (seen[r] == i0) continue;
+        seen[r] = i0;
+        par_r[r] = i;
+        if (mate_r[r] < 0) found = r;
+        else st.push_back({mate_r[r], 0});
+      }
+      for (int r = found; r >= 0;) {   // flip the path
+        const int i = par_r[r], nxt = mate_l[i];
+        mate_l[i] = r;
+        mate_r[r] = i;
+        r = nxt;
+      }
+    }
+    // König: Z = reachable from unmatched left nodes by alternating paths
+    std::vector<char> zl(nl, 0), zr(nr, 0);
+    std::vector<int> q;
+    for (int i = 0; i < nl; ++i)
+      if (mate_l[i] < 0) { zl[i] = 1; q.push_back(i); }
+    for (size_t h = 0; h < q.size(); ++h)
+      for (int r : g[q[h]])
+        if (!zr[r] && mate_l[q[h]] != r) {
+          zr[r] = 1;
+          const int i = mate_r[r];
+          if (i >= 0 && !zl[i]) { zl[i] = 1; q.push_back(i); }
+        }
+    int n = 0;
+    for (int i = 0; i < nl; ++i) if (!zl[i]) { cover[left[i]] = 1; ++n; }
+    for (int r = 0; r < nr; ++r) if (zr[r]) { cover[right[r]] = 1; ++n; }
+    for (int u : left) lev[u] = -1;
+    for (int u : right) lev[u] = -1;
+    (void)idx;
+    return n;
+  }
+
   // Geometric separator: cut the component by a plane normal to one of its
   // principal axes at a quantile of the projections; the separator is the
-  // smaller one-sided boundary of the cut edges.  The best (smallest, then
-  // most balanced) of several cuts is kept.
+  // minimum vertex cover of the cut edges (konig_cover).  The best
+  // (smallest, then most balanced) of several cuts is kept.
   bool geometric_separator(std::vector<int> &comp, int tag, std::vector<int> &A, std::vector<int> &B,
                            std::vector<int> &S) {
     const int m = (int)comp.size();
@@ -134,8 +223,9 @@ struct Dissector {
         for (int b = 0; b < 3; ++b) D[3 * a + b] -= lam * v[a] * v[b];
     }
     std::vector<int> side(adj.size(), 0);
+    std::vector<char> cover(adj.size(), 0);
     std::vector<std::pair<double, int>> pr(m);
-    long best_score = -1;
+    double best_score = -1;
     std::vector<int> best_side;
     for (int k = 0; k < 2; ++k) {
       for (int i = 0; i < m; ++i) {
@@ -147,30 +237,20 @@ struct Dissector {
         const int cut = m * qi / 20;
         if (cut < 1 || cut >= m) continue;
         for (int i = 0; i < m; ++i) side[pr[i].second] = i < cut ? 1 : 2;
-        // one-sided boundaries
-        int sa = 0, sb = 0;
-        for (int u : comp) {
-          bool bd = false;
-          for (int v : adj[u])
-            if (mark[v] == tag && side[v] != side[u]) { bd = true; break; }
-          if (bd) (side[u] == 1 ? sa : sb)++;
-        }
-        const int sep_side = sa <= sb ? 1 : 2;
-        const int ssz = std::min(sa, sb);
-        const int na = cut - (sep_side == 1 ? ssz : 0), nbb = m - cut - (sep_side == 2 ? ssz : 0);
+        for (int u : comp) cover[u] = 0;
+        const int ssz = konig_cover(comp, side, tag, cover);
+        int na = 0, nbb = 0;
+        for (int u : comp)
+          if (!cover[u]) (side[u] == 1 ? na : nbb)++;
         if (std::min(na, nbb) < m / 5) continue;
-        const long score = (long)ssz * 4 * m + std::abs(na - nbb);
+        // elimination-tree height in tile columns: the separator's tiles plus
+        // the larger child's height, which grows about as sqrt(size) on these
+        // planar graphs (cfg3's tree: ~1 tile column per sqrt(tag))
+        const double score = height_score(ssz, na, nbb);
         if (best_score < 0 || score < best_score) {
           best_score = score;
           best_side.assign(m, 0);
-          for (int i = 0; i < m; ++i) {
-            const int u = comp[i];
-            bool bd = false;
-            if (side[u] == sep_side)
-              for (int v : adj[u])
-                if (mark[v] == tag && side[v] != side[u]) { bd = true; break; }
-            best_side[i] = bd ? 0 : side[u];
-          }
+          for (int i = 0; i < m; ++i) best_side[i] = cover[comp[i]] ? 0 : side[comp[i]];
         }
       }
     }
@@ -190,7 +270,9 @@ struct Dissector {
     if (!xyz.empty()) {
       ok = geometric_separator(comp, tag, A, B, S);
       std::vector<int> A2, B2, S2;
-      if (level_separator(comp, tag, A2, B2, S2) && (!ok || S2.size() < S.size())) {
+      if (level_separator(comp, tag, A2, B2, S2) &&
+          (!ok || height_score((long)S2.size(), (long)A2.size(), (long)B2.size()) <
+                      height_score((long)S.size(), (long)A.size(), (long)B.size()))) {
         A.swap(A2); B.swap(B2); S.swap(S2);
         ok = true;
       }
@@ -202,6 +284,8 @@ struct Dissector {
       return;
     }
     absorb(A, B, S, tag);
+    static const bool dbg = std::getenv("ARSLAM_ND_DEBUG") != nullptr;   // debug: the dissection tree
+    if (dbg) std::fprintf(stderr, "nd: comp %zu -> A %zu B %zu S %zu\n", comp.size(), A.size(), B.size(), S.size());
     const int ta = ++next_tag, tb = ++next_tag, ts = ++next_tag;
     for (int u : A) mark[u] = ta;
     for (int u : B) mark[u] = tb;
@@ -413,7 +497,7 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
       for (int a = 0; a < 3; ++a) xyz[3L * t + a] = h.x0[3 + 6L * nc + 6L * t + a];
     // leaves of up to 32 tags (192 rows = 3 whole tiles): a smaller dissection
     // would not shorten the elimination tree, only add padding and parts
-    parts = nd_parts(nt, adj, 32, xyz);
+    parts = nd_parts(nt, adj, std::getenv("ARSLAM_ND_LEAF") ? std::atoi(std::getenv("ARSLAM_ND_LEAF")) : 32, xyz);
   } else {
     std::vector<int> order;
     if (ordering == 1 && nt > 1) order = rcm_order(nt, adj);

@@ -75,9 +75,8 @@ def bench_localize(args, world, rank):
     (algorithmic bytes: per query-iteration 2 passes over the observation
     records (72 B each) and the tag poses they gather (48 B each), plus the
     pose) ride along."""
-    from ar_slam_amd import build, lm, synth
+    from ar_slam_amd import lm, synth
     import torch
-    build.build()
     b = synth.make_localize_batch(n_query=4096)
     loc = lm.Localizer(b, device=0 if world == 1 else int(os.environ.get("LOCAL_RANK", "0")))
     _, res, _ = loc.solve()
@@ -160,6 +159,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # build (if stale) before anything touches the GPU; ranks serialize on the build lock
+    from ar_slam_amd import build
+    build.build()
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -171,8 +173,7 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    from ar_slam_amd import build, lm, synth
-    build.build()
+    from ar_slam_amd import lm, synth
     g = synth.config_graph(args.config)
     part = shard_graph(g, rank, world) if world > 1 else dict(
         camera=g.camera, cap=g.cap, tag=g.tag, obs_cap=g.obs_cap, obs_tag=g.obs_tag, corners=g.corners)
