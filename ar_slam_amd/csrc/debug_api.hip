@@ -191,6 +191,8 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
       info->n_update_items = (long)plan.h_items.size();
       info->n_split_targets = (long)plan.h_split.size();
       info->update_flops = plan.total_upd_flops;
+      info->factor_flops = plan.total_factor_flops;
+      info->scalar_flops = L.scalar_flops;
       info->n_dag_tasks = plan.n_dag_tasks;
       info->dag_valid = arslam::dag_check(plan) ? 1 : 0;
       if (const char *dump = std::getenv("ARSLAM_DAG_DUMP")) {   // debug: the task graph, for offline analysis

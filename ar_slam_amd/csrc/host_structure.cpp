@@ -6,6 +6,7 @@
 #include "host_structure.h"
 
 #include <algorithm>
+#include <iterator>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -227,14 +228,20 @@ struct Dissector {
     std::vector<std::pair<double, int>> pr(m);
     double best_score = -1;
     std::vector<int> best_side;
-    for (int k = 0; k < 2; ++k) {
+    static const int n_dir = std::getenv("ARSLAM_ND_DIRS") ? std::atoi(std::getenv("ARSLAM_ND_DIRS")) : 6;
+    static const int n_q = std::getenv("ARSLAM_ND_QSTEPS") ? std::atoi(std::getenv("ARSLAM_ND_QSTEPS")) : 20;
+    for (int k = 0; k < n_dir; ++k) {
+      // cut directions in the plane of the two principal axes
+      const double ang = M_PI * k / n_dir, ca = std::cos(ang), sa = std::sin(ang);
+      double dir[3];
+      for (int a = 0; a < 3; ++a) dir[a] = ca * axes[0][a] + sa * axes[1][a];
       for (int i = 0; i < m; ++i) {
         const int u = comp[i];
-        pr[i] = {axes[k][0] * xyz[3L * u] + axes[k][1] * xyz[3L * u + 1] + axes[k][2] * xyz[3L * u + 2], u};
+        pr[i] = {dir[0] * xyz[3L * u] + dir[1] * xyz[3L * u + 1] + dir[2] * xyz[3L * u + 2], u};
       }
       std::sort(pr.begin(), pr.end());
-      for (int qi = 6; qi <= 14; ++qi) {   // cut at quantiles 0.30 .. 0.70
-        const int cut = m * qi / 20;
+      for (int qi = 3 * n_q / 10; qi <= 7 * n_q / 10; ++qi) {   // cut at quantiles 0.30 .. 0.70
+        const int cut = m * qi / n_q;
         if (cut < 1 || cut >= m) continue;
         for (int i = 0; i < m; ++i) side[pr[i].second] = i < cut ? 1 : 2;
         for (int u : comp) cover[u] = 0;
@@ -369,6 +376,45 @@ std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>
 }
 
 
+double scalar_cholesky_flops(const std::vector<std::vector<int>> &adj, const std::vector<int> &tag_row,
+                             bool camera) {
+  // tags in elimination order; symbolic factorization on the tag graph: the
+  // higher-ordered neighbour set of a tag (its fill included) is merged into
+  // its elimination-tree parent, the lowest of them
+  std::vector<int> order;
+  for (int t = 0; t < (int)tag_row.size(); ++t)
+    if (tag_row[t] >= 0) order.push_back(t);
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return tag_row[a] < tag_row[b]; });
+  std::vector<int> pos(tag_row.size(), -1);
+  for (int i = 0; i < (int)order.size(); ++i) pos[order[i]] = i;
+  const int n = (int)order.size();
+  std::vector<std::vector<int>> up(n);   // higher-ordered neighbours (positions), sorted
+  for (int i = 0; i < n; ++i) {
+    for (int v : adj[order[i]])
+      if (v < (int)pos.size() && pos[v] > i) up[i].push_back(pos[v]);
+    std::sort(up[i].begin(), up[i].end());
+    up[i].erase(std::unique(up[i].begin(), up[i].end()), up[i].end());
+  }
+  const double ncam = camera ? 3.0 : 0.0;
+  double flops = 0.0;
+  auto col = [&](double c) { flops += c * (c + 1.0) + c + 1.0; };
+  std::vector<int> merged;
+  for (int i = 0; i < n; ++i) {
+    const double f = (double)up[i].size();
+    for (int k = 0; k < 6; ++k) col((5 - k) + 6.0 * f + ncam);
+    if (!up[i].empty()) {
+      const int parent = up[i][0];
+      merged.clear();
+      std::set_union(up[parent].begin(), up[parent].end(), up[i].begin() + 1, up[i].end(),
+                     std::back_inserter(merged));
+      up[parent].swap(merged);
+    }
+    std::vector<int>().swap(up[i]);
+  }
+  for (int k = 0; k < (int)ncam; ++k) col(ncam - 1 - k);
+  return flops;
+}
+
 HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum) {
   api_check(p != nullptr, ARSLAM_E_INVALID_ARG, "null problem");
   api_check(p->n_cap >= 0 && p->n_tag >= 0 && p->n_obs >= 0, ARSLAM_E_INVALID_ARG, "negative sizes");
@@ -466,7 +512,7 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   std::vector<char> tfree(nt, 0);
   for (int t = 0; t < nt; ++t) tfree[t] = h.slot_free[3 + 6L * nc + 6L * t];
   std::vector<std::vector<int>> adj(nt);
-  if (ordering != 0 && nt > 1) {
+  if (nt > 1) {   // (also for the natural order: the scalar flop count reads it)
     if (adj_max) {   // co-visibility is global over ranks
       api_check(nt <= 16384, ARSLAM_E_UNSUPPORTED, "multi-GPU reduced ordering limited to 16384 tags");
       std::vector<uint8_t> bm((size_t)nt * nt, 0);
@@ -529,6 +575,7 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
     row += 3;
   }
   L.nR = row;
+  L.scalar_flops = scalar_cholesky_flops(adj, L.tag_row, L.cam_row >= 0);
   if (L.nR == 0) return L;
   L.N = round_up(L.nR + 1, kTileRows);
   const int T = L.T = (int)(L.N / kTileRows);

@@ -77,7 +77,15 @@ struct ReducedLayout {
   std::vector<uint8_t> pattern;     // [T*T] lower tile pattern of the assembled system
   int n_parts = 0;                  // ordering parts (ND: leaves + separators)
   long pad_rows = 0;                // alignment padding rows among the tag rows
+  double scalar_flops = 0.0;        // flops of the scalar Cholesky of the real rows in this order
 };
+
+// Flops of the scalar (row-level) Cholesky of the reduced system in the row
+// order tag_row gives, padding excluded: sum over columns of c (c + 1) + c + 1
+// with c the column's below-diagonal count from the symbolic factorization of
+// the tag co-visibility graph (6x6 dense blocks) plus the dense camera border.
+double scalar_cholesky_flops(const std::vector<std::vector<int>> &adj, const std::vector<int> &tag_row,
+                             bool camera);
 
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
                              const ReduceMaxU8 &pattern_max);

@@ -186,6 +186,7 @@ struct arslam_lm {
   arslam::LaunchTiming upd_timing;
   std::vector<hipEvent_t> upd_events;
   double dom_ms = 0.0, dom_flops = 0.0;
+  double scalar_flops = 0.0;   // scalar Cholesky flops of the reduced system's real rows (ReducedLayout)
   long dom_launches = 0;
 
   void timing_begin() {
@@ -341,6 +342,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   const std::vector<double> &corners = h.corners;
   const std::vector<unsigned char> &obs_active = h.obs_active;
   const int cam_row = L.cam_row;
+  scalar_flops = L.scalar_flops;
   nR = L.nR;
   has_f = nR > 0;
   if (has_f) {
@@ -793,6 +795,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->n_levels = plan.nlev;
   s->n_update_tiles = plan.total_upd_tiles;
   s->factor_update_flops = plan.total_upd_flops;
+  s->factor_scalar_flops = scalar_flops;
 }
 
 // ===========================================================================

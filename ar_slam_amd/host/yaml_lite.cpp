@@ -127,9 +127,12 @@ struct Parser {
   }
 
   Node value_of(const std::string &rest, int indent, int lineno) {
-    const std::string r = trim(rest);
+    std::string r = trim(rest);
     if (!r.empty()) {
       if (r.front() == '[') {
+        // a flow sequence may continue on more-indented lines (yaml-cpp and
+        // PyYAML both wrap long ones): join them until the bracket closes
+        while (r.back() != ']' && pos < lines.size() && lines[pos].indent > indent) r += " " + lines[pos++].text;
         if (r.back() != ']') fail("unterminated flow sequence");
         return flow_seq(r, lineno);
       }

@@ -113,7 +113,7 @@ class Summary(C.Structure):
                 ("t_dominant_ms", C.c_double), ("dominant_flops", C.c_double),
                 ("n_dominant_launches", C.c_long),
                 ("n_factor_tiles", C.c_long), ("n_levels", C.c_int), ("n_update_tiles", C.c_long),
-                ("factor_update_flops", C.c_double),
+                ("factor_update_flops", C.c_double), ("factor_scalar_flops", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 
     def to_dict(self):
@@ -430,7 +430,8 @@ class PlanInfo(C.Structure):
                 ("tiles_per_side", C.c_int), ("n_parts", C.c_int), ("camera_row", C.c_int),
                 ("n_levels", C.c_int), ("n_assembled_tiles", C.c_long), ("n_factor_tiles", C.c_long),
                 ("n_update_tiles", C.c_long), ("n_update_items", C.c_long), ("n_split_targets", C.c_long),
-                ("update_flops", C.c_double), ("n_dag_tasks", C.c_long), ("dag_valid", C.c_int)]
+                ("update_flops", C.c_double), ("n_dag_tasks", C.c_long), ("dag_valid", C.c_int),
+                ("factor_flops", C.c_double), ("scalar_flops", C.c_double)]
 
 
 def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, cap_const=None,

@@ -43,7 +43,16 @@ CONFIGS = {
     "medium": (200, 10, 8, 13),
     "cfg2": (1000, 20, 15, 1),
     "cfg3": (10000, 50, 40, 2),
+    # parity graph with SURVEY.md §8d's full rotation ranges: camera roll and
+    # tag yaw ~ U(-pi, pi), so angle-axis vectors reach |w| ~ pi
+    "wide": (300, 12, 10, 15),
+    # BASELINE.json configs[0]: the demo's 3 images of 6 tags (resources/images
+    # img1-3, demo_launch.py:39-110), replicated synthetically at 1020x768 --
+    # detection needs OpenCV's ArUco dictionaries, absent from the image
+    "cfg1": (3, 3, 2, 16),
 }
+FULL_ROTATION = {"wide"}
+TAGS_PER_CAPTURE = {"cfg1": 4}
 
 
 @dataclasses.dataclass
@@ -149,16 +158,17 @@ def _rot_axis(axis, ang):
     return rodrigues(axis * ang[:, None])
 
 
-def _sample_cameras(rng, n, x_lo, x_hi, y_lo, y_hi, max_tilt):
+def _sample_cameras(rng, n, x_lo, x_hi, y_lo, y_hi, max_tilt, roll_range=0.5 * np.pi):
     """World->camera rotations and centres of captures looking at the tag plane.
 
     World z points from the cameras towards the tag plane (z = 0), so an
-    untilted camera has R = Rz(roll); roll and tag yaw stay within +-90 deg so
-    no pose sits near the angle-axis singularity at |w| = pi.
+    untilted camera has R = Rz(roll).  cfg2/cfg3 keep roll and tag yaw within
+    +-90 deg (no pose near the angle-axis singularity at |w| = pi);
+    roll_range = pi is SURVEY.md §8d's U(-pi, pi) (the "wide" parity graph).
     """
     pos = np.stack([rng.uniform(x_lo, x_hi, n), rng.uniform(y_lo, y_hi, n),
                     -rng.uniform(0.6, 1.2, n)], 1)
-    roll = rng.uniform(-0.5 * np.pi, 0.5 * np.pi, n)
+    roll = rng.uniform(-roll_range, roll_range, n)
     tilt = rng.uniform(0.0, max_tilt, n)
     tilt_dir = rng.uniform(-np.pi, np.pi, n)
     R_roll = _rot_axis(np.tile([0, 0, 1.0], (n, 1)), roll)
@@ -187,7 +197,7 @@ def _visible_nearest(R_cw, pos, corners_w, centres, cand, k):
 
 def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
                init_trans_sigma=0.02, init_rot_sigma=0.02, f_init=1.1 * F_TRUE,
-               max_tilt=np.deg2rad(20.0), name=""):
+               max_tilt=np.deg2rad(20.0), name="", full_rotation=False):
     """Generate a connected capture/tag graph with exactly ``k`` tags per capture."""
     rng = np.random.Generator(np.random.PCG64(seed))
     n_tag = grid_x * grid_y
@@ -198,7 +208,8 @@ def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
     # tags face the cameras: in the reference's marker frame (x right, y down,
     # z away from the viewer; ar_slam_util.hpp:340-345 and calcInitValues
     # :52-95) the tag z axis points away from the cameras, i.e. along world +z
-    tag_true[:, 5] = rng.uniform(-0.5 * np.pi, 0.5 * np.pi, n_tag)
+    rot_range = np.pi if full_rotation else 0.5 * np.pi
+    tag_true[:, 5] = rng.uniform(-rot_range, rot_range, n_tag)
     camera_true = np.array([F_TRUE, 0.0, 0.0])
 
     # tag corner world points (Nt,4,3)
@@ -216,7 +227,7 @@ def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
     n_cand = min(n_tag, 128)
     while filled < n_captures:
         m = max(64, min(4096, (n_captures - filled) * 2))
-        R_cw, pos = _sample_cameras(rng, m, x_lo, x_hi, y_lo, y_hi, max_tilt)
+        R_cw, pos = _sample_cameras(rng, m, x_lo, x_hi, y_lo, y_hi, max_tilt, rot_range)
         # 3-D distance order == XY distance order (all tags at z = 0), so the
         # k nearest visible tags lie among the n_cand XY-nearest whenever at
         # least k of those are visible; otherwise fall back to every tag.
@@ -340,6 +351,10 @@ def make_localize_batch(map_name="cfg3", n_query=4096, seed=3, k=8, noise_px=0.5
 
 def config_graph(name, **kw):
     n, gx, gy, seed = CONFIGS[name]
+    if name in FULL_ROTATION:
+        kw.setdefault("full_rotation", True)
+    if name in TAGS_PER_CAPTURE:
+        kw.setdefault("k", TAGS_PER_CAPTURE[name])
     return make_graph(n, gx, gy, seed, name=name, **kw)
 
 

@@ -105,6 +105,31 @@ def control_trace(name, threads=8):
         json.dump(out, f, indent=1)
 
 
+def map_yaml(g, uid=lambda c: f"cap_{c}", tag_id=lambda t: f"aruco_4X4_50_{t}", focal=3000.0):
+    """A synthetic graph as a map file in the reference's layout (saveYaml ar_slam_util.cpp:387-465,
+    SURVEY.md Appendix C): blocks in capture order, captures and arucos at zero pose (as detected,
+    never solved: loadYaml leaves them uninitialized, :304-368), camera at the reference's default
+    focal (CameraParams, ar_slam_util.hpp:68-72) and the demo's 1020x768 image."""
+    blocks, arucos = [], {}
+    for b in range(g.n_obs):
+        t = int(g.obs_tag[b])
+        arucos.setdefault(tag_id(t), {"pose": [0.0] * 6})
+        blocks.append({"capture": uid(int(g.obs_cap[b])), "aruco": tag_id(t),
+                       "aruco_rect": [float(v) for v in g.corners[b]]})
+    captures = {uid(c): {"inv_pose": [0.0] * 6, "img_fn": f"img{c + 1}.jpg"} for c in range(g.n_cap)}
+    return {"blocks": blocks, "captures": captures, "arucos": arucos,
+            "camera": {"params": [focal, 0.0, 0.0], "width": synth.IMG_W, "height": synth.IMG_H}}
+
+
+def cfg1_fixture():
+    """cfg1 (BASELINE.json configs[0]): the demo's 3 captures / 6 tags as a detections map."""
+    import yaml
+    g = synth.config_graph("cfg1")
+    with open(os.path.join(HERE, "cfg1_map.yaml"), "w") as f:
+        f.write("# cfg1 replica: 3 captures / 6 tags, 1020x768, seed 16 (tests/golden/make_golden.py)\n")
+        yaml.safe_dump(map_yaml(g), f, sort_keys=False, default_flow_style=None)
+
+
 def lm_trace(name, threads=8):
     g = synth.config_graph(name)
     cam, cap, tag, s = O.solve_graph(g, num_threads=threads)
@@ -147,6 +172,10 @@ if __name__ == "__main__":
         control_trace(n)
         print("wrote control", n)
     names = [n for n in names if n != "control" and not n.startswith("ctl_")]
+    if "cfg1" in names:
+        cfg1_fixture()
+        print("wrote cfg1 map")
+        names = [n for n in names if n != "cfg1"]
     if "loc" in names:
         localize_golden()
         print("wrote loc")

@@ -90,8 +90,9 @@ def _compare_solves(g, ours, ref, n_cost_iters=5):
     assert np.abs(A - tag_r[used, :3]).max() < 1e-6
 
 
-@pytest.mark.parametrize("name", ["tiny", "small", "medium", "cfg2"])
+@pytest.mark.parametrize("name", ["tiny", "small", "medium", "cfg2", "wide"])
 def test_lm_solve_matches_oracle(lm, oracle, name):
+    """(wide: camera roll and tag yaw ~ U(-pi, pi), SURVEY.md §8d -- angle-axis up to |w| ~ pi)"""
     g = synth.config_graph(name)
     ref = oracle.solve_graph(g)
     ours = lm.solve_graph(g)

@@ -101,7 +101,7 @@ def test_golden_jacobian_table(oracle):
         np.testing.assert_array_equal(J, kat["J"][i])
 
 
-@pytest.mark.parametrize("name", ["tiny", "small", "medium"])
+@pytest.mark.parametrize("name", ["tiny", "small", "medium", "wide"])
 def test_golden_lm_traces(oracle, name):
     with open(os.path.join(GOLDEN, f"lm_{name}.json")) as f:
         gold = json.load(f)

@@ -92,6 +92,23 @@ def test_yaml_matches_pyyaml(L, tmp_path):
     np.testing.assert_array_equal(t.capture(c0)[1], [0.5, -1.0, 2.0, 0.1, 0.2, 0.3])
 
 
+def test_yaml_wrapped_flow_sequences_and_cfg1_fixture(L):
+    """Long flow sequences wrapped over several lines (PyYAML's default flow style, as
+    yaml-cpp reads them) load exactly; the committed cfg1 detections map loads as written."""
+    import os
+    yaml = pytest.importorskip("yaml")
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg1_map.yaml")
+    d = yaml.safe_load(open(path))
+    assert "\n    " in open(path).read()          # the fixture does wrap its rects
+    t = L.SlamSolver()
+    t.load_yaml(path)
+    assert (t.num_captures, t.num_arucos, t.num_blocks) == (3, 6, len(d["blocks"]))
+    for b in range(t.num_blocks):
+        np.testing.assert_array_equal(t.block(b)[2], d["blocks"][b]["aruco_rect"])
+    params, size = t.camera()
+    assert list(params) == d["camera"]["params"] and size == (1020, 768)
+
+
 def test_yaml_errors(L):
     t = L.SlamSolver()
     with pytest.raises(L.LMError):   # aruco_rect with 7 values (:353-355)
