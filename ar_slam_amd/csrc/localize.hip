@@ -29,7 +29,7 @@ namespace {
 constexpr int kMaxChunks = ARSLAM_LOC_MAX_OBS * 8 / 64;
 
 struct LocParams {
-  int nq;
+  int nq, nt;
   const double *cam;           // [3]
   const double *tag;           // [nt*6]
   const unsigned char *tim;    // [nt] or null
@@ -39,6 +39,7 @@ struct LocParams {
   const double *pose_in;       // [nq*6]
   double *pose_out;            // [nq*6]
   arslam_localize_result *res; // [nq]
+  const double *aw;            // [nt*4][4] world points of the (constant) tags' corners
   int init_from_map, max_k;
   int max_iters, max_invalid, jacobi;
   double ftol, gtol, ptol, r0, rmax, rmin, min_rel, dmin, dmax;
@@ -122,6 +123,68 @@ __device__ void init_capture_pose(const double *corners, const double *camera, c
   inv[2] -= ar_pose[2];
 }
 
+// ---- the constant map: tag corners in the world frame ----
+// localizeOne holds every tag and the camera constant (ar_slam_util.cpp:965,
+// 972), so the first half of projectCorner, a = R(w_t) c_i + t_t (:144-148),
+// is the same for every query and iteration: computed once per batch solve.
+__global__ void k_tag_corners(int nt, const double *__restrict__ tag, double *__restrict__ aw) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;   // 4 t + corner
+  if (e >= 4 * nt) return;
+  const double *tg = tag + 6L * (e >> 2);
+  const AngleAxis at = aa_prepare(tg + 3);
+  const double cpt[3] = {0.5 * kArucoSize * corner_dx(e & 3), 0.5 * kArucoSize * corner_dy(e & 3), 0.0};
+  double a[3];
+  aa_rotate(at, cpt, a);
+  aw[4L * e] = a[0] + tg[0];
+  aw[4L * e + 1] = a[1] + tg[1];
+  aw[4L * e + 2] = a[2] + tg[2];
+  aw[4L * e + 3] = 0.0;
+}
+
+// The capture's rotation, its matrix and right Jacobian: the same for every
+// row of the query, computed once per evaluation (not per row).
+struct CapFrame {
+  AngleAxis ac;
+  double M[9], Jr[9];
+};
+
+__device__ __forceinline__ void cap_frame(const double *x, CapFrame &F, bool jac) {
+  F.ac = aa_prepare(x + 3);
+  if (!jac) return;
+  aa_matrix(F.ac, F.M);
+  if (F.ac.big) aa_right_jacobian(F.ac, F.Jr);
+}
+
+// Residual row of a corner whose world point is aw: b = aw + t_c, p = R(w_c) b
+// (:152-155), r = f p_xy / p_z - obs (:157-162, :198-211); with J6 != null
+// also its 6 capture-block Jacobian entries [t_c, w_c].
+__device__ __forceinline__ double loc_row(const CapFrame &F, const double *x, const double *aw, double f,
+                                          int comp, double obs, double *J6) {
+  double b[3] = {aw[0] + x[0], aw[1] + x[1], aw[2] + x[2]}, p[3];
+  aa_rotate(F.ac, b, p);
+  const double r = f * ((comp == 0 ? p[0] : p[1]) / p[2]) - obs;
+  if (J6) {
+    const double xx = p[0] / p[2], yy = p[1] / p[2], fz = f / p[2];
+    const double P[3] = {comp == 0 ? fz : 0.0, comp == 0 ? 0.0 : fz, comp == 0 ? -fz * xx : -fz * yy};
+    double PM[3], v[3];
+    vecmat3(P, F.M, PM);
+    J6[0] = PM[0]; J6[1] = PM[1]; J6[2] = PM[2];
+    if (F.ac.big) {   // d/dw_c = -((P Mc) x b) Jr_c
+      double o[3];
+      cross3(PM, b, v);
+      vecmat3(v, F.Jr, o);
+      J6[3] = -o[0]; J6[4] = -o[1]; J6[5] = -o[2];
+    } else {          // small branch: -(P x b)
+      cross3(P, b, v);
+      J6[3] = -v[0]; J6[4] = -v[1]; J6[5] = -v[2];
+    }
+  }
+  return r;
+}
+
+// packed upper index of the diagonal entry (j, j) of the 6x6 normal matrix
+#define HD(j) ((j) * 6 - ((j) * ((j) - 1)) / 2)
+
 // ---- one query per wavefront ----
 template <int NCH>
 struct Rows {
@@ -132,82 +195,86 @@ struct Rows {
 // Residuals and capture-block Jacobian rows at x; wave-reduced cost, J'r,
 // column norms and the 21 upper entries of J'J.  Returns false if a residual
 // is not finite (uniform).
-template <int NCH>
+template <int NCH, int LPQ>
 __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const double *x, int lane,
-                                  Rows<NCH> &rows, double &cost, double g[6], double cn[6], double H[21]) {
+                                  Rows<NCH> &rows, double &cost, double g[6], double H[21],
+                                  const AngleAxis *ac_pre = nullptr) {
   double c = 0.0, gl[6] = {0, 0, 0, 0, 0, 0}, hl[21];
 #pragma unroll
   for (int e = 0; e < 21; ++e) hl[e] = 0.0;
   bool bad = false;
+  CapFrame F;
+  if (ac_pre) {   // the accepted candidate's rotation, from its cost evaluation
+    F.ac = *ac_pre;
+    aa_matrix(F.ac, F.M);
+    if (F.ac.big) aa_right_jacobian(F.ac, F.Jr);
+  } else {
+    cap_frame(x, F, true);
+  }
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
-    const int R = lane + 64 * ch;
+    const int R = lane + LPQ * ch;
     rows.r[ch] = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) rows.J[ch][j] = 0.0;
     if (R < nrow) {
       const int o = o0 + (R >> 3), row = R & 7;
-      const double *tg = p.tag + 6L * p.ot[o];
-      double j13[13];
-      const double r = residual_jacobian_row(p.cam, x, tg, row >> 1, row & 1, p.corners[8L * o + row], j13);
+      double j6[6];
+      const double r = loc_row(F, x, p.aw + 4L * (4 * p.ot[o] + (row >> 1)), p.cam[0], row & 1,
+                               p.corners[8L * o + row], j6);
       bad = bad || !isfinite(r);
       rows.r[ch] = r;
       c += r * r;
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
-        rows.J[ch][j] = j13[1 + j];
-        gl[j] += j13[1 + j] * r;
+        rows.J[ch][j] = j6[j];
+        gl[j] += j6[j] * r;
       }
       int e = 0;
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
-        for (int b = a; b < 6; ++b) hl[e++] += j13[1 + a] * j13[1 + b];
+        for (int b = a; b < 6; ++b) hl[e++] += j6[a] * j6[b];
     }
   }
-  cost = 0.5 * wave_sum(c);
+  cost = 0.5 * wave_sum<LPQ>(c);
 #pragma unroll
-  for (int j = 0; j < 6; ++j) g[j] = wave_sum(gl[j]);
+  for (int j = 0; j < 6; ++j) g[j] = wave_sum<LPQ>(gl[j]);
 #pragma unroll
-  for (int e = 0; e < 21; ++e) H[e] = wave_sum(hl[e]);
-  int e = 0;
-#pragma unroll
-  for (int a = 0; a < 6; ++a)
-#pragma unroll
-    for (int b = a; b < 6; ++b) {
-      if (a == b) cn[a] = H[e];
-      ++e;
-    }
-  return wave_max(bad ? 1.0 : 0.0) == 0.0;
+  for (int e = 0; e < 21; ++e) H[e] = wave_sum<LPQ>(hl[e]);
+  return wave_max<LPQ>(bad ? 1.0 : 0.0) == 0.0;
 }
 
-template <int NCH>
-__device__ double evaluate_cost(const LocParams &p, int o0, int nrow, const double *x, int lane, bool &finite) {
-  const AngleAxis ac = aa_prepare(x + 3);
+template <int NCH, int LPQ>
+__device__ double evaluate_cost(const LocParams &p, int o0, int nrow, const double *x, int lane, bool &finite,
+                              CapFrame &F) {
+  cap_frame(x, F, false);
   double c = 0.0;
   bool bad = false;
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
-    const int R = lane + 64 * ch;
+    const int R = lane + LPQ * ch;
     if (R < nrow) {
       const int o = o0 + (R >> 3), row = R & 7;
-      const double *tg = p.tag + 6L * p.ot[o];
-      const AngleAxis at = aa_prepare(tg + 3);
-      const double r = residual_row(ac, x, at, tg, p.cam[0], row >> 1, row & 1, p.corners[8L * o + row],
-                                    nullptr, nullptr);
+      const double r = loc_row(F, x, p.aw + 4L * (4 * p.ot[o] + (row >> 1)), p.cam[0], row & 1,
+                               p.corners[8L * o + row], nullptr);
       bad = bad || !isfinite(r);
       c += r * r;
     }
   }
-  finite = wave_max(bad ? 1.0 : 0.0) == 0.0;
-  return 0.5 * wave_sum(c);
+  finite = wave_max<LPQ>(bad ? 1.0 : 0.0) == 0.0;
+  return 0.5 * wave_sum<LPQ>(c);
 }
 
-// NCH = 64-row chunks per query (k <= 8 NCH observations)
-template <int NCH>
-__global__ __launch_bounds__(256) void k_localize(LocParams p) {
-  const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+// LPQ lanes per query (64: one query per wave; 32: two queries per wave, each
+// half-wave its own LM -- the 6x6 solves, the LM bookkeeping and the
+// capture's rotation then cost half the instructions per query), NCH =
+// LPQ-row chunks per query (k <= NCH LPQ / 8 observations).  One wavefront
+// per workgroup, so a finished wave's slot is reused at once.
+template <int NCH, int LPQ>
+__global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
+  const int lane = threadIdx.x & (LPQ - 1);
+  const int q = blockIdx.x * (64 / LPQ) + threadIdx.x / LPQ;
   if (q >= p.nq) return;
   const int o0 = p.qs[q], k = p.qs[q + 1] - o0;
   arslam_localize_result res;
@@ -237,9 +304,9 @@ __global__ __launch_bounds__(256) void k_localize(LocParams p) {
 
   // ---- iteration 0 ----
   Rows<NCH> rows;
-  double cost, g[6], cn[6], H[21];
+  double cost, g[6], H[21];   // (column norms squared = diag(H): HD(j))
   double x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-  bool finite = evaluate_jacobian<NCH>(p, o0, nrow, x, lane, rows, cost, g, cn, H);
+  bool finite = evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H);
   res.initial_cost = cost;
   if (!finite) {
     res.status = ARSLAM_FAILURE;
@@ -248,7 +315,7 @@ __global__ __launch_bounds__(256) void k_localize(LocParams p) {
   } else {
     double scale[6], diag[6];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) scale[j] = p.jacobi ? 1.0 / (1.0 + sqrt(cn[j])) : 1.0;
+    for (int j = 0; j < 6; ++j) scale[j] = p.jacobi ? 1.0 / (1.0 + sqrt(H[HD(j)])) : 1.0;
     double radius = p.r0, decrease = 2.0;
     bool reuse_diag = false, succ = true;
     int n_invalid = 0, iteration = 0;
@@ -267,7 +334,7 @@ __global__ __launch_bounds__(256) void k_localize(LocParams p) {
       // LevenbergMarquardtStrategy: D^2 = clamp(diag(J~'J~)) / radius
       if (!reuse_diag)
 #pragma unroll
-        for (int j = 0; j < 6; ++j) diag[j] = fmin(fmax(scale[j] * scale[j] * cn[j], p.dmin), p.dmax);
+        for (int j = 0; j < 6; ++j) diag[j] = fmin(fmax(scale[j] * scale[j] * H[HD(j)], p.dmin), p.dmax);
       reuse_diag = true;
       // (J~'J~ + D^2) y = J~'r, 6x6 Cholesky in every lane
       double A[21], y[6];
@@ -287,46 +354,50 @@ __global__ __launch_bounds__(256) void k_localize(LocParams p) {
       }
       // packed upper index of (a,b), a <= b
 #define UP(a, b) ((a) * 6 - ((a) * ((a) - 1)) / 2 + ((b) - (a)))
+      // in place: L[i][j] (i >= j) overwrites A[UP(j, i)]
       bool lin_ok = true;
-      double L[6][6];
+      double il[6];
+#define L_(i, j) A[UP(j, i)]
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
-        double s = A[UP(j, j)];
+        double s = L_(j, j);
 #pragma unroll
-        for (int m = 0; m < j; ++m) s -= L[j][m] * L[j][m];
+        for (int m = 0; m < j; ++m) s -= L_(j, m) * L_(j, m);
         lin_ok = lin_ok && s > 0.0;
         const double ljj = sqrt(s);
-        L[j][j] = ljj;
+        L_(j, j) = ljj;
+        il[j] = 1.0 / ljj;   // one division per pivot; the column and both substitutions multiply
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
-          double t = A[UP(j, i)];
+          double t = L_(i, j);
 #pragma unroll
-          for (int m = 0; m < j; ++m) t -= L[i][m] * L[j][m];
-          L[i][j] = t / ljj;
+          for (int m = 0; m < j; ++m) t -= L_(i, m) * L_(j, m);
+          L_(i, j) = t * il[j];
         }
       }
-#undef UP
       if (lin_ok) {
         double z[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
           double t = scale[i] * g[i];
 #pragma unroll
-          for (int m = 0; m < i; ++m) t -= L[i][m] * z[m];
-          z[i] = t / L[i][i];
+          for (int m = 0; m < i; ++m) t -= L_(i, m) * z[m];
+          z[i] = t * il[i];
         }
 #pragma unroll
         for (int i = 5; i >= 0; --i) {
           double t = z[i];
 #pragma unroll
-          for (int m = i + 1; m < 6; ++m) t -= L[m][i] * y[m];
-          y[i] = t / L[i][i];
+          for (int m = i + 1; m < 6; ++m) t -= L_(m, i) * y[m];
+          y[i] = t * il[i];
         }
         bool yfin = true;
 #pragma unroll
         for (int i = 0; i < 6; ++i) yfin = yfin && isfinite(y[i]);
         lin_ok = yfin;
       }
+#undef L_
+#undef UP
       // step = -y; model cost change m = -sum mr (r + mr/2), mr = J~ step
       double model = 0.0;
       bool valid = false;
@@ -339,7 +410,7 @@ __global__ __launch_bounds__(256) void k_localize(LocParams p) {
           for (int j = 0; j < 6; ++j) mr += rows.J[ch][j] * scale[j] * (-y[j]);
           mcc += mr * (rows.r[ch] + mr / 2.0);   // padding rows contribute 0
         }
-        model = -wave_sum(mcc);
+        model = -wave_sum<LPQ>(mcc);
         valid = model > 0.0;
       }
       if (!valid) {
@@ -358,7 +429,8 @@ __global__ __launch_bounds__(256) void k_localize(LocParams p) {
         sq += d * d;
       }
       bool cfin = true;
-      double cand = evaluate_cost<NCH>(p, o0, nrow, xc, lane, cfin);
+      CapFrame Fc;
+      double cand = evaluate_cost<NCH, LPQ>(p, o0, nrow, xc, lane, cfin, Fc);
       if (!cfin) cand = DBL_MAX;
       // ParameterToleranceReached / FunctionToleranceReached
       if (sqrt(sq) <= p.ptol * (x_norm + p.ptol)) { res.status = ARSLAM_CONVERGENCE; res.rule = ARSLAM_RULE_PARAMETER; break; }
@@ -369,7 +441,7 @@ __global__ __launch_bounds__(256) void k_localize(LocParams p) {
 #pragma unroll
         for (int j = 0; j < 6; ++j) x[j] = xc[j];
         x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-        (void)evaluate_jacobian<NCH>(p, o0, nrow, x, lane, rows, cost, g, cn, H);
+        (void)evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H, &Fc.ac);
         gmax = 0.0;
 #pragma unroll
         for (int j = 0; j < 6; ++j) gmax = fmax(gmax, fabs(g[j]));
@@ -440,7 +512,7 @@ struct arslam_localizer {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int nq = 0, nt = 0, nb = 0, init_from_map = 0, max_k = 0;
   bool has_tim = false, loaded = false;
-  DBuf<double> cam, tag, corners, pose_in, pose_out;
+  DBuf<double> cam, tag, corners, pose_in, pose_out, aw;
   DBuf<int> qs, ot;
   DBuf<unsigned char> tim;
   DBuf<arslam_localize_result> res;
@@ -498,6 +570,7 @@ struct arslam_localizer {
     has_tim = b->tag_in_map != nullptr;
     if (has_tim) up(tim, b->tag_in_map, nt);
     pose_out.alloc(std::max(6L * nq, 1L));
+    aw.alloc(std::max(16L * nt, 1L));
     res.alloc(std::max(nq, 1));
     hip_check(hipStreamSynchronize(stream), "load sync");
     loaded = true;
@@ -509,6 +582,7 @@ struct arslam_localizer {
     p.nq = nq; p.cam = cam.p; p.tag = tag.p; p.tim = has_tim ? tim.p : nullptr;
     p.qs = qs.p; p.ot = ot.p; p.corners = corners.p; p.pose_in = pose_in.p; p.pose_out = pose_out.p;
     p.res = res.p; p.init_from_map = init_from_map; p.max_k = max_k;
+    p.aw = aw.p; p.nt = nt;
     p.max_iters = opt.max_num_iterations; p.max_invalid = opt.max_num_consecutive_invalid_steps;
     p.jacobi = opt.jacobi_scaling;
     p.ftol = opt.function_tolerance; p.gtol = opt.gradient_tolerance; p.ptol = opt.parameter_tolerance;
@@ -537,10 +611,14 @@ struct arslam_localizer {
 namespace arslam {
 void launch_localize(const LocParams &p, hipStream_t s) {
   if (p.nq == 0) return;
-  const dim3 grid((unsigned)((p.nq + 3) / 4)), block(256);
-  if (p.max_k <= 8) hipLaunchKernelGGL(k_localize<1>, grid, block, 0, s, p);
-  else if (p.max_k <= 16) hipLaunchKernelGGL(k_localize<2>, grid, block, 0, s, p);
-  else hipLaunchKernelGGL(k_localize<kMaxChunks>, grid, block, 0, s, p);
+  if (p.nt > 0)   // the map's corner points (inside the timed region: one launch per batch solve)
+    hipLaunchKernelGGL(k_tag_corners, dim3((unsigned)((4 * p.nt + 255) / 256)), dim3(256), 0, s, p.nt, p.tag,
+                       const_cast<double *>(p.aw));
+  const dim3 block(64);
+  if (p.max_k <= 8)   // (cfg5: k = 8) two queries per wave
+    hipLaunchKernelGGL((k_localize<2, 32>), dim3((unsigned)((p.nq + 1) / 2)), block, 0, s, p);
+  else if (p.max_k <= 16) hipLaunchKernelGGL((k_localize<2, 64>), dim3((unsigned)p.nq), block, 0, s, p);
+  else hipLaunchKernelGGL((k_localize<kMaxChunks, 64>), dim3((unsigned)p.nq), block, 0, s, p);
 }
 }  // namespace arslam
 

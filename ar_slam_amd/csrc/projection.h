@@ -85,15 +85,21 @@ __device__ __forceinline__ void aa_matrix(const AngleAxis &a, double M[9]) {
 __device__ __forceinline__ void aa_right_jacobian(const AngleAxis &a, double Jr[9]) {
   double A, B;
   if (a.th < 0.5) {
-    double t = 1.0, fa = 2.0, fb = 6.0;
-    A = 0.0; B = 0.0;
+    // A = sum_k (-th2)^k / (2k+2)!, B = sum_k (-th2)^k / (2k+3)!, k < 7 (truncation
+    // < 1e-16 relative), by Horner on correctly rounded reciprocal factorials
+    // (no double divisions on the device; the oracle sums t / k! directly, the
+    // two agree to a few ulps of the Jacobian entries)
+    constexpr double ca[7] = {1.0 / 2.0, 1.0 / 24.0, 1.0 / 720.0, 1.0 / 40320.0, 1.0 / 3628800.0,
+                              1.0 / 479001600.0, 1.0 / 87178291200.0};
+    constexpr double cb[7] = {1.0 / 6.0, 1.0 / 120.0, 1.0 / 5040.0, 1.0 / 362880.0, 1.0 / 39916800.0,
+                              1.0 / 6227020800.0, 1.0 / 1307674368000.0};
+    const double x = -a.th2;
+    A = ca[6];
+    B = cb[6];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      A += t / fa;
-      B += t / fb;
-      t *= -a.th2;
-      fa *= (double)(2 * k + 3) * (2 * k + 4);
-      fb *= (double)(2 * k + 4) * (2 * k + 5);
+    for (int k = 5; k >= 0; --k) {
+      A = A * x + ca[k];
+      B = B * x + cb[k];
     }
   } else {
     const double sh = sin(0.5 * a.th);
@@ -191,15 +197,48 @@ __device__ __forceinline__ double residual_jacobian_row(const double *cam, const
   return r;
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+// Wave-wide reductions without the LDS crossbar (a __shfl_xor is a
+// ds_bpermute round trip per 32-bit half and step): DPP inside each 16-lane
+// row (xor 1, xor 2, half-row mirror, row mirror), then v_permlane16_swap
+// between the rows of a pair and v_permlane32_swap between the halves.
+// Every step combines a lane with its partner symmetrically, so all 64
+// lanes end with bit-identical results (the LM decisions stay wave-uniform).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+
+// W = 64: the whole wave; W = 32: each half-wave separately (two queries per
+// wave in k_localize).
+template <int W = 64, class Op>
+__device__ __forceinline__ double wave_reduce(double v, Op op) {
+  v = op(v, dpp_f64<0xB1>(v));    // quad_perm [1,0,3,2]: lane ^ 1
+  v = op(v, dpp_f64<0x4E>(v));    // quad_perm [2,3,0,1]: lane ^ 2
+  v = op(v, dpp_f64<0x141>(v));   // row_half_mirror: the other quad of each 8
+  v = op(v, dpp_f64<0x140>(v));   // row_mirror: the other 8 of each 16
+  unsigned long long u = __double_as_longlong(v);
+  const auto a = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+  v = op(__longlong_as_double((long long)(((unsigned long long)b[0] << 32) | a[0])),
+         __longlong_as_double((long long)(((unsigned long long)b[1] << 32) | a[1])));   // rows 2g, 2g+1
+  if (W == 32) return v;
+  u = __double_as_longlong(v);
+  const auto c = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
+  const auto d = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+  return op(__longlong_as_double((long long)(((unsigned long long)d[0] << 32) | c[0])),
+            __longlong_as_double((long long)(((unsigned long long)d[1] << 32) | c[1])));   // halves
+}
+
+template <int W = 64>
+__device__ __forceinline__ double wave_sum(double v) {
+  return wave_reduce<W>(v, [](double x, double y) { return x + y; });
+}
+template <int W = 64>
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
+  return wave_reduce<W>(v, [](double x, double y) { return fmax(x, y); });
 }
 
 

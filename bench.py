@@ -101,6 +101,14 @@ def bench_localize(args, world, rank):
     k_obs = b.n_obs / b.n_query
     bytes_per_qi = 2 * k_obs * (72 + 48) + 48
     avg_kernel_s = kms / args.steps * 1e-3
+    # The kernel is bound by fp64 VALU issue (trig, divisions, DPP reductions),
+    # not HBM: its roofline is VALU wave-instructions per second against one
+    # instruction per 4 cycles per SIMD (a wave64 fp64 FMA; MI355X: 256 CUs x 4
+    # SIMDs x 2.4 GHz), with the instruction count per launch from the
+    # committed PMC pass (profiles/pmc_localize.json, SQ_INSTS_VALU).
+    valu = load_pmc_localize()
+    valu_peak = 256 * 4 * 2.4e9 / 4 / 1e9   # G wave-instructions/s
+    achieved_valu = valu / avg_kernel_s / 1e9 if valu else None
     achieved = bytes_per_qi * q_iters / avg_kernel_s / 1e9
     out = {"metric": "localize queries/s, 4096-query batch against the 2k-tag cfg3 map",
            "value": world * b.n_query * args.steps / elapsed, "unit": "queries/s", "n_gpus": world,
@@ -108,13 +116,16 @@ def bench_localize(args, world, rank):
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
            "data": "synthetic (seeded generator, SURVEY.md §8d cfg5)",
            "config": {"workload": f"cfg5: {b.n_query} queries x {int(k_obs)} tags, map = cfg3 tags",
-                      "parallelism": "one wavefront per query"},
+                      "parallelism": "two queries per wavefront (32 lanes each)"},
            "query_iterations_per_s": world * q_iters * args.steps / elapsed,
            "mean_iterations_per_query": q_iters / b.n_query,
-           "roofline": {"bound": "hbm", "kernel": "k_localize", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                        "avg_launch_us": avg_kernel_s * 1e6,
-                        "bytes_per_query_iteration": bytes_per_qi},
+           "roofline": {"bound": "valu", "kernel": "k_localize (two queries per wave)",
+                        "achieved": achieved_valu, "peak": valu_peak, "unit": "G VALU-instructions/s",
+                        "frac": achieved_valu / valu_peak if achieved_valu else None, "traffic": None,
+                        "avg_launch_us": avg_kernel_s * 1e6, "valu_instructions_per_launch": valu,
+                        "hbm_view": {"achieved_GBps": achieved, "peak_GBps": HBM_PEAK_GBS,
+                                     "frac": achieved / HBM_PEAK_GBS,
+                                     "bytes_per_query_iteration": bytes_per_qi}},
            "cpu_baseline": None}
     if not args.no_cpu_baseline and world == 1:
         from oracle import oracle as O
@@ -131,6 +142,15 @@ def bench_localize(args, world, rank):
                                          f"localizeMany, single thread, {dt:.1f} s"}
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def load_pmc_localize():
+    """SQ_INSTS_VALU per k_localize launch from the committed PMC pass, if any."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_localize.json")) as f:
+            return json.load(f).get("valu_instructions_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def load_pmc_traffic():
