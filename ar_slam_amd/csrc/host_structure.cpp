@@ -501,7 +501,8 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
 }
 
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
-                             const ReduceMaxU8 &pattern_max) {
+                             const ReduceMaxU8 &pattern_max,
+                             const std::vector<int> *reuse_tag_row, long reuse_edges) {
   // Rows exist only for free tags and a free camera (constant / unused blocks
   // are not parameters).  Tags are ordered natural, RCM or by nested
   // dissection; with ND every part starts on a tile boundary so the tile
@@ -535,8 +536,14 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
       }
     }
   }
+  for (auto &v : adj) L.n_edges += (long)v.size();
+  bool reuse = reuse_tag_row && (int)reuse_tag_row->size() == std::max(nt, 1) && 10 * L.n_edges <= 11 * reuse_edges;
+  L.order_edges = reuse ? reuse_edges : L.n_edges;
+  for (int t = 0; reuse && t < nt; ++t) reuse = ((*reuse_tag_row)[t] >= 0) == (tfree[t] != 0);
   std::vector<std::vector<int>> parts;
-  if (ordering == 2 && nt > 1) {
+  if (reuse) {
+    // (the earlier order; rows below)
+  } else if (ordering == 2 && nt > 1) {
     // tag positions (initial values) embed the co-visibility graph for geometric separators
     std::vector<double> xyz(3L * nt);
     for (int t = 0; t < nt; ++t)
@@ -551,6 +558,14 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
     parts.push_back(order);
   }
   long row = 0, real = 0;
+  if (reuse) {
+    L.tag_row = *reuse_tag_row;
+    for (int t = 0; t < nt; ++t)
+      if (L.tag_row[t] >= 0) {
+        row = std::max(row, (long)L.tag_row[t] + 6);
+        real += 6;
+      }
+  }
   for (auto &part : parts) {
     bool any = false;
     for (int t : part) any = any || tfree[t];

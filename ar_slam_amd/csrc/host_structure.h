@@ -78,6 +78,8 @@ struct ReducedLayout {
   int n_parts = 0;                  // ordering parts (ND: leaves + separators)
   long pad_rows = 0;                // alignment padding rows among the tag rows
   double scalar_flops = 0.0;        // flops of the scalar Cholesky of the real rows in this order
+  long n_edges = 0;                 // co-visibility edges (directed) among the free tags
+  long order_edges = 0;             // edges when the tag order was computed (n_edges unless reused)
 };
 
 // Flops of the scalar (row-level) Cholesky of the reduced system in the row
@@ -87,8 +89,14 @@ struct ReducedLayout {
 double scalar_cholesky_flops(const std::vector<std::vector<int>> &adj, const std::vector<int> &tag_row,
                              bool camera);
 
+// reuse_tag_row: the tag rows of an earlier layout of the same problem family,
+// made when the co-visibility graph had reuse_edges edges; used as is (no new
+// ordering) when the set of free tags is unchanged and the graph has grown by
+// at most a tenth since -- an incremental solve that only added captures
+// keeps its elimination order until the fill it was made for is outdated.
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
-                             const ReduceMaxU8 &pattern_max);
+                             const ReduceMaxU8 &pattern_max,
+                             const std::vector<int> *reuse_tag_row = nullptr, long reuse_edges = 0);
 
 // Deterministic Schur assembly.  k_schur stores capture c's local reduced
 // system at slab + cap_off[c] block-packed: local blocks U = 0 (f, 1 row),

@@ -68,14 +68,20 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Device buffer; grow-only, so reloading a problem of the same or a smaller
+// size (every optimize() of an incremental solve) does no hipMalloc/hipFree.
 template <class T>
 struct DevBuf {
   T *p = nullptr;
-  size_t n = 0;
+  size_t n = 0, cap = 0;
   void alloc(size_t count) {
-    release();
     n = count;
-    if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+    if (count <= cap) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+    cap = count;
   }
   void upload(const T *h, size_t count, hipStream_t s) {
     if (count) HIP_CHECK(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
@@ -83,7 +89,7 @@ struct DevBuf {
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
-    n = 0;
+    n = cap = 0;
   }
   ~DevBuf() { release(); }
 };
@@ -150,6 +156,10 @@ struct arslam_lm {
   std::vector<int> pk_obs_cap, pk_obs_tag;
   std::vector<double> pk_corners;
   std::unordered_set<double *> constant;
+  // The pointer-keyed structure (blocks, residuals, constants) changed since
+  // the last load: arslam_lm_solve reloads; otherwise it reuses the resident
+  // problem, plan and buffers and uploads only the parameter values.
+  bool pk_dirty = true;
 
   // ---- loaded problem ----
   bool loaded = false;
@@ -160,6 +170,7 @@ struct arslam_lm {
   std::vector<unsigned char> slot_free;
   std::vector<double> x0;   // initial slots
   long nb_global = 0;       // observations over all ranks
+  double setup_s = 0.0;     // host structure + ordering + plan + upload of the last load (or value reload)
   arslam::DevProblem P{};
   hipStream_t stream = nullptr;
   int device = 0;
@@ -270,6 +281,12 @@ struct arslam_lm {
   }
 
   void load(const arslam_soa_problem *p);
+  void reload_values(const arslam_soa_problem *p);
+  bool pk_loaded = false;   // the resident problem came from the pointer-keyed API
+  bool reuse_order = false;  // load(): keep the previous tag order when the free tags are unchanged
+  std::vector<int> prev_tag_row;
+  int prev_ordering = -1, prev_skip = -1;
+  long prev_order_edges = 0;
   void linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
   // linearize split at the host read: enqueue (results copied to h_lin), collect after a sync
   void linearize_launch();
@@ -299,6 +316,7 @@ long round_up(long v, long m) { return (v + m - 1) / m * m; }
 }  // namespace
 
 void arslam_lm::load(const arslam_soa_problem *p) {
+  const double t_load = now_s();
   loaded = false;
   if (nranks > 1) ensure_stream();   // the structure exchange below runs on the device
   // host structure; with several ranks the tag use, the co-visibility and the
@@ -323,7 +341,10 @@ void arslam_lm::load(const arslam_soa_problem *p) {
       HIP_CHECK(hipStreamSynchronize(stream));
     };
   }
+  static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
+  double tp[6] = {now_s(), 0, 0, 0, 0, 0};
   arslam::HostProblem h = arslam::host_problem(p, deg_sum);   // validates p
+  tp[1] = now_s();
   ensure_stream();
   soa = *p;
   nc = h.nc;
@@ -334,14 +355,25 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   slot_free = h.slot_free;
   x0 = h.x0;
   const int maxk = h.maxk;
+  // an incremental re-load (pointer-keyed path, same options) whose free tags
+  // are unchanged keeps the previous elimination order: the ordering (nested
+  // dissection) is the largest part of the host setup
+  const bool can_reuse = reuse_order && !prev_tag_row.empty() && prev_ordering == opt.reduced_ordering &&
+                         prev_skip == opt.cholesky_skip_zero_tiles;
   arslam::ReducedLayout L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0,
-                                                   u8_max, u8_max);
+                                                   u8_max, u8_max, can_reuse ? &prev_tag_row : nullptr,
+                                                   prev_order_edges);
+  prev_tag_row = L.tag_row;
+  prev_order_edges = L.order_edges;
+  prev_ordering = opt.reduced_ordering;
+  prev_skip = opt.cholesky_skip_zero_tiles;
   const std::vector<int> &cap_start = h.cap_start, &obs_tag = h.obs_tag, &obs_lblk = h.obs_lblk,
                          &cap_blk_start = h.cap_blk_start, &blk_tag = h.blk_tag, &tag_start = h.tag_start,
                          &tag_obs = h.tag_obs, &tag_row = L.tag_row, &row_slot = L.row_slot;
   const std::vector<double> &corners = h.corners;
   const std::vector<unsigned char> &obs_active = h.obs_active;
   const int cam_row = L.cam_row;
+  tp[2] = now_s();
   scalar_flops = L.scalar_flops;
   nR = L.nR;
   has_f = nR > 0;
@@ -352,6 +384,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
     N = 0;
     arslam::llt_plan_free(plan);
   }
+  tp[3] = now_s();
 
   // ---- device upload ----
   d_cap_start.alloc(nc + 1); d_cap_start.upload(cap_start.data(), nc + 1, stream);
@@ -382,7 +415,9 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
   int n_dest = 0, n_items = 0, n_splits = 0;
   if (has_f) {
+    tp[4] = now_s();
     const arslam::SchurGather sg = arslam::schur_gather_plan(h, L);
+    tp[5] = now_s();
     n_dest = (int)sg.dest_start.size() - 1;
     d_cap_off.alloc(nc + 1); d_cap_off.upload(sg.cap_off.data(), nc + 1, stream);
     d_slab.alloc(std::max(sg.cap_off[nc], 1L));
@@ -422,7 +457,28 @@ void arslam_lm::load(const arslam_soa_problem *p) {
   P.gather_items = d_gather_items.p; P.gather_splits = d_gather_splits.p; P.gather_part = d_gather_part.p;
   P.n_items = n_items; P.n_splits = n_splits;
   HIP_CHECK(hipStreamSynchronize(stream));
+  soa = *p;
   loaded = true;
+  setup_s = now_s() - t_load;
+  if (prof)
+    std::fprintf(stderr, "arslam setup: nc %d nt %d host %.3f layout %.3f plan %.3f upload %.3f gather %.3f rest %.3f ms\n",
+                 nc, nt, 1e3 * (tp[1] - tp[0]), 1e3 * (tp[2] - tp[1]), 1e3 * (tp[3] - tp[2]),
+                 1e3 * (tp[4] - tp[3]), 1e3 * (tp[5] - tp[4]), 1e3 * (now_s() - tp[5]));
+}
+
+// Same structure as the loaded problem, new parameter values (the pointer-keyed
+// path when no block, residual or constant changed since the last load).
+void arslam_lm::reload_values(const arslam_soa_problem *p) {
+  const double t0 = now_s();
+  fail_if(!loaded || p->n_cap != nc || p->n_tag != nt || p->n_obs != nb, ARSLAM_E_STATE,
+          "reload_values: structure differs from the loaded problem");
+  std::memcpy(x0.data(), p->camera, 3 * sizeof(double));
+  if (nc) std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
+  if (nt) std::memcpy(x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
+  d_x0.upload(x0.data(), n, stream);
+  HIP_CHECK(hipStreamSynchronize(stream));
+  soa = *p;
+  setup_s = now_s() - t0;
 }
 
 // Evaluate residuals/Jacobian at x: cost, gradient (unscaled), column norms
@@ -510,6 +566,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   dom_launches = 0;
   s->n_obs = nb;
   s->n_reduced = has_f ? (int)nR : 0;
+  s->setup_time_s = setup_s;
   x = d_xa.p;
   xc = d_xb.p;
   HIP_CHECK(hipMemcpyAsync(x, d_x0.p, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
@@ -889,7 +946,7 @@ int arslam_lm_set_options(arslam_lm *h, const arslam_lm_options *opt) {
             ARSLAM_E_INVALID_ARG, "max_num_iterations out of range");
     if (opt->device != h->opt.device || opt->reduced_ordering != h->opt.reduced_ordering ||
         opt->cholesky_skip_zero_tiles != h->opt.cholesky_skip_zero_tiles)
-      h->loaded = false;
+      h->loaded = false, h->pk_dirty = true;
     h->opt = *opt;
   });
 }
@@ -929,6 +986,7 @@ int arslam_lm_add_residual_block(arslam_lm *h, const double corners[8], double *
     } else {
       t = ti->second;
     }
+    h->pk_dirty = true;
     h->pk_obs_cap.push_back(c);
     h->pk_obs_tag.push_back(t);
     h->pk_corners.insert(h->pk_corners.end(), corners, corners + 8);
@@ -940,13 +998,15 @@ int arslam_lm_set_parameter_block_constant(arslam_lm *h, double *block) {
   return guarded([&] {
     fail_if(block != h->camera_ptr && !h->cap_of.count(block) && !h->tag_of.count(block),
             ARSLAM_E_INVALID_ARG, "parameter block is not part of the problem");
-    h->constant.insert(block);
+    if (h->constant.insert(block).second) h->pk_dirty = true;
   });
 }
 
 int arslam_lm_set_parameter_block_variable(arslam_lm *h, double *block) {
   if (!h || !block) return ARSLAM_E_INVALID_ARG;
-  return guarded([&] { h->constant.erase(block); });
+  return guarded([&] {
+    if (h->constant.erase(block)) h->pk_dirty = true;
+  });
 }
 
 int arslam_lm_num_residual_blocks(const arslam_lm *h) {
@@ -979,13 +1039,21 @@ int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
     p.corners = h->pk_corners.data();
     p.camera_const = h->constant.count(h->camera_ptr) ? 1 : 0;
     p.cap_const = cc.data(); p.tag_const = tc.data();
-    h->load(&p);
+    if (h->loaded && h->pk_loaded && !h->pk_dirty) {
+      h->reload_values(&p);   // same problem, new values: no host rebuild, no re-upload of observations
+    } else {
+      h->reuse_order = h->pk_loaded;   // a grown pointer-keyed problem (not the first load)
+      h->load(&p);
+      h->reuse_order = false;
+      h->pk_loaded = true;
+      h->pk_dirty = false;
+    }
     h->solve(summary);
     // write the final state into the caller's blocks (Ceres writes parameters back)
     std::memcpy(h->camera_ptr, cam.data(), 3 * sizeof(double));
     for (int c = 0; c < nc; ++c) std::memcpy(h->cap_ptrs[c], &cap[6L * c], 6 * sizeof(double));
     for (int t = 0; t < nt; ++t) std::memcpy(h->tag_ptrs[t], &tag[6L * t], 6 * sizeof(double));
-    h->loaded = false;   // the SoA buffers above go out of scope
+    h->soa = arslam_soa_problem{};   // (the arrays above go out of scope; the device problem stays)
   });
 }
 
@@ -998,17 +1066,27 @@ int arslam_lm_reset(arslam_lm *h) {
     h->pk_obs_cap.clear(); h->pk_obs_tag.clear(); h->pk_corners.clear();
     h->constant.clear();
     h->loaded = false;
+    h->pk_dirty = true;
+    h->pk_loaded = false;
+    h->prev_tag_row.clear();
   });
 }
 
 int arslam_lm_load_soa(arslam_lm *h, const arslam_soa_problem *p) {
   if (!h || !p) return ARSLAM_E_INVALID_ARG;
-  return guarded([&] { h->load(p); });
+  return guarded([&] {
+    h->pk_loaded = false;
+    h->pk_dirty = true;
+    h->load(p);
+  });
 }
 
 int arslam_lm_solve_loaded(arslam_lm *h, arslam_lm_summary *summary) {
   if (!h || !summary) return ARSLAM_E_INVALID_ARG;
-  return guarded([&] { h->solve(summary); });
+  return guarded([&] {
+    fail_if(h->pk_loaded, ARSLAM_E_STATE, "no problem loaded by arslam_lm_load_soa");
+    h->solve(summary);
+  });
 }
 
 int arslam_lm_solve_soa(arslam_soa_problem *p, const arslam_lm_options *opt,
@@ -1045,6 +1123,7 @@ int arslam_lm_set_comm_callback(arslam_lm *h, int rank, int nranks, arslam_allre
     h->comm_cb = nranks > 1 ? fn : nullptr;
     h->comm_cb_ctx = ctx;
     h->loaded = false;
+    h->pk_dirty = true;
   });
 }
 
@@ -1057,6 +1136,7 @@ int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks, const unsigned char i
     h->rank = rank;
     h->nranks = nranks;
     h->loaded = false;
+    h->pk_dirty = true;
     if (nranks > 1) {
       ncclUniqueId u;
       std::memcpy(&u, id, sizeof(u));

@@ -130,6 +130,12 @@ int arslam_slam_last_summary(const arslam_slam *h, arslam_lm_summary *s) {
   return ARSLAM_OK;
 }
 
+int arslam_slam_solve_summary(const arslam_slam *h, int i, arslam_lm_summary *s) {
+  if (!h || !s || i < 0 || i >= (int)h->s.solveLog().size()) return ARSLAM_E_INVALID_ARG;
+  *s = h->s.solveLog()[i].summary;
+  return ARSLAM_OK;
+}
+
 int arslam_slam_capture(const arslam_slam *h, int c, char *uid, int cap, double inv_pose[6]) {
   if (!h || c < 0 || c >= (int)h->s.numCaptures()) return ARSLAM_E_INVALID_ARG;
   const arslam::Capture &cp = h->s.at(arslam::CaptureHandle{(unsigned)c});

@@ -53,8 +53,8 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_slam_load_yaml_string", "arslam_slam_save_yaml", "arslam_slam_add_detections",
            "arslam_slam_solve", "arslam_slam_solve_incremental", "arslam_slam_localize_many",
            "arslam_slam_num_captures", "arslam_slam_num_arucos", "arslam_slam_num_blocks",
-           "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_capture",
-           "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
+           "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_solve_summary",
+           "arslam_slam_capture", "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
            "arslam_slam_block", "arslam_slam_camera", "arslam_slam_set_camera",
            "arslam_slam_get_transforms", "arslam_slam_camera_info"]
 
@@ -157,7 +157,8 @@ def lib():
                "arslam_slam_load_yaml_string", "arslam_slam_save_yaml", "arslam_slam_add_detections",
                "arslam_slam_solve", "arslam_slam_solve_incremental", "arslam_slam_localize_many",
                "arslam_slam_num_captures", "arslam_slam_num_arucos", "arslam_slam_num_blocks",
-               "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_capture",
+               "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_solve_summary",
+               "arslam_slam_capture",
                "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
                "arslam_slam_block", "arslam_slam_camera", "arslam_slam_set_camera",
                "arslam_slam_get_transforms", "arslam_slam_camera_info"):
@@ -603,6 +604,12 @@ class SlamSolver:
     def last_summary(self):
         s = Summary()
         _check(lib().arslam_slam_last_summary(self._h, C.byref(s)))
+        return s.to_dict()
+
+    def solve_summary(self, i):
+        """Summary of optimize() call i."""
+        s = Summary()
+        _check(lib().arslam_slam_solve_summary(self._h, C.c_int(i), C.byref(s)))
         return s.to_dict()
 
     def capture(self, c):

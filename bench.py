@@ -68,6 +68,31 @@ def cpu_baseline(g, threads, name):
                       f"{dt:.1f} s"}
 
 
+def bench_incremental(name="cfg2"):
+    """The reference's real flow (ArSlamSolver::solveIncremental, ar_slam_util.cpp:629-742): one
+    Detections message per capture, each followed by a full Solve of the problem so far (:736),
+    through the C++ host mirror and the pointer-keyed C-ABI (the drop-in path, host buffers, setup
+    included).  Reported beside the headline line, never as `value`."""
+    from ar_slam_amd import lm, synth
+    g = synth.config_graph(name)
+    s = lm.SlamSolver()
+    s.set_camera(g.camera)
+    t0 = time.perf_counter()
+    for c in range(g.n_cap):
+        sel = g.obs_cap == c
+        s.add_detections(f"cap{c}", [f"tag_{t}" for t in g.obs_tag[sel]], g.corners[sel])
+        s.solve_incremental()
+    wall = time.perf_counter() - t0
+    n = s.num_solves
+    sums = [s.solve_summary(i) for i in range(n)]
+    setup = sum(d["setup_time_s"] for d in sums)
+    mini = sum(d["minimizer_time_s"] for d in sums)
+    return {"flow": f"solveIncremental on {name} ({g.n_cap} captures / {g.n_tag} tags), one message per capture",
+            "wall_s": wall, "solves": n, "lm_iterations": sum(d["num_linear_solves"] for d in sums),
+            "setup_ms_per_solve": 1e3 * setup / n, "minimizer_ms_per_solve": 1e3 * mini / n,
+            "final_rms_px": sums[-1]["final_rms_px"]}
+
+
 def bench_localize(args, world, rank):
     """cfg5: batched localizeMany of 4096 queries against cfg3's map (BASELINE.json configs[4]).
 
@@ -171,6 +196,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-incremental", action="store_true", help="skip the solveIncremental (cfg2) side line")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--skip-zero-tiles", type=int, default=1)
@@ -295,6 +321,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_incremental and args.config == "cfg3":
+            out["incremental_cfg2"] = bench_incremental("cfg2")
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(g, threads, args.config)

@@ -126,6 +126,8 @@ typedef struct {
   int n_levels;                 /* levels of the tile elimination tree (launch pairs) */
   long n_update_tiles;          /* tile updates (MFMA work items) */
   double factor_update_flops;   /* useful flops of the trailing updates */
+  double factor_scalar_flops;   /* flops of the scalar Cholesky of the real rows (the algorithmic count:
+                                   no padding rows, no zeros inside fill tiles) per factorization */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
 } arslam_lm_summary;

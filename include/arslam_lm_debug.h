@@ -54,6 +54,9 @@ typedef struct {
   double update_flops;     /* algorithmic flops of the trailing updates per factorization */
   long n_dag_tasks;        /* tasks of the persistent executor's graph */
   int dag_valid;           /* 1: run one at a time in ticket order, every wait is already met */
+  double factor_flops;     /* flops of the tile plan per factorization (POTRF, TRSM, updates, inverses) */
+  double scalar_flops;     /* flops of the scalar Cholesky of the real rows in this order (no padding,
+                              no structurally zero entries inside tiles) */
 } arslam_plan_info;
 
 /* diagnostic builds only (-DARSLAM_SCHUR_STAMPS): per-phase cycles of the

@@ -55,6 +55,8 @@ int arslam_slam_num_arucos(const arslam_slam *h);
 int arslam_slam_num_blocks(const arslam_slam *h);
 int arslam_slam_num_solves(const arslam_slam *h);   /* optimize() calls so far */
 int arslam_slam_last_summary(const arslam_slam *h, arslam_lm_summary *s);
+/* the summary of optimize() call i (0 <= i < arslam_slam_num_solves) */
+int arslam_slam_solve_summary(const arslam_slam *h, int i, arslam_lm_summary *s);
 
 /* capture c: uid (copied, NUL-terminated, truncated to cap), inv_pose[6] */
 int arslam_slam_capture(const arslam_slam *h, int c, char *uid, int cap, double inv_pose[6]);

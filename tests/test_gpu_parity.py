@@ -118,6 +118,40 @@ def test_pointer_api_matches_soa(lm):
     np.testing.assert_allclose(np.stack(caps), cap2, rtol=1e-8, atol=1e-9)
 
 
+def test_pointer_api_resolve_reuses_the_resident_problem(lm):
+    """Solving an unchanged pointer-keyed problem again reloads only the parameter values (no
+    host rebuild, no plan, no observation upload: setup_time_s drops), from the caller's current
+    block values, and gives exactly what a fresh problem gives from those values."""
+    g = synth.config_graph("small")
+    camera = g.camera.copy()
+    caps = [g.cap[c].copy() for c in range(g.n_cap)]
+    tags = [g.tag[t].copy() for t in range(g.n_tag)]
+    prob = lm.Problem()
+    for b in range(g.n_obs):
+        prob.add_residual_block(g.corners[b], camera, caps[g.obs_cap[b]], tags[g.obs_tag[b]])
+    s1 = prob.solve()
+    # perturb the solved state in the caller's blocks, solve again (same structure)
+    camera[0] *= 1.02
+    for c in caps:
+        c[:3] += 0.01
+    start = (camera.copy(), np.stack(caps).copy(), np.stack(tags).copy())
+    s2 = prob.solve()
+    assert s2["setup_time_s"] < 0.5 * s1["setup_time_s"]
+    fresh = lm.Problem()
+    cam_f = start[0].copy()
+    caps_f = [c.copy() for c in start[1]]
+    tags_f = [t.copy() for t in start[2]]
+    for b in range(g.n_obs):
+        fresh.add_residual_block(g.corners[b], cam_f, caps_f[g.obs_cap[b]], tags_f[g.obs_tag[b]])
+    s3 = fresh.solve()
+    assert [i["cost"] for i in s2["iterations"]] == [i["cost"] for i in s3["iterations"]]
+    np.testing.assert_array_equal(camera, cam_f)
+    # a structural change (a block held constant) rebuilds
+    prob.set_parameter_block_constant(tags[0])
+    s4 = prob.solve()
+    assert s4["setup_time_s"] > s2["setup_time_s"]
+
+
 def test_localize_constant_map(lm, oracle):
     """localizeOne: tags and camera constant (ar_slam_util.cpp:965,972), one free capture each."""
     g = synth.config_graph("medium")
