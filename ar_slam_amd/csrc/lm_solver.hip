@@ -171,6 +171,7 @@ struct arslam_lm {
   std::vector<double> x0;   // initial slots
   long nb_global = 0;       // observations over all ranks
   double setup_s = 0.0;     // host structure + ordering + plan + upload of the last load (or value reload)
+  double comm_bytes = 0.0;  // bytes this rank all-reduced (RCCL or the host callback) since the count was reset
   arslam::DevProblem P{};
   hipStream_t stream = nullptr;
   int device = 0;
@@ -249,6 +250,7 @@ struct arslam_lm {
   void allreduce_any(void *buf, size_t count, int dtype, int op) {
     if (nranks <= 1 || count == 0) return;
     const size_t bytes = count * (dtype == ARSLAM_DT_F64 ? sizeof(double) : 1);
+    comm_bytes += (double)bytes;
     if (comm_cb) {
       comm_stage.resize(bytes);
       HIP_CHECK(hipMemcpyAsync(comm_stage.data(), buf, bytes, hipMemcpyDeviceToHost, stream));
@@ -564,6 +566,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   }
   dom_ms = dom_flops = 0.0;
   dom_launches = 0;
+  comm_bytes = 0.0;
   s->n_obs = nb;
   s->n_reduced = has_f ? (int)nR : 0;
   s->setup_time_s = setup_s;
@@ -853,6 +856,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->n_update_tiles = plan.total_upd_tiles;
   s->factor_update_flops = plan.total_upd_flops;
   s->factor_scalar_flops = scalar_flops;
+  s->comm_bytes = comm_bytes;
 }
 
 // ===========================================================================

@@ -114,6 +114,7 @@ class Summary(C.Structure):
                 ("n_dominant_launches", C.c_long),
                 ("n_factor_tiles", C.c_long), ("n_levels", C.c_int), ("n_update_tiles", C.c_long),
                 ("factor_update_flops", C.c_double), ("factor_scalar_flops", C.c_double),
+                ("comm_bytes", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 
     def to_dict(self):

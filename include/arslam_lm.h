@@ -128,6 +128,7 @@ typedef struct {
   double factor_update_flops;   /* useful flops of the trailing updates */
   double factor_scalar_flops;   /* flops of the scalar Cholesky of the real rows (the algorithmic count:
                                    no padding rows, no zeros inside fill tiles) per factorization */
+  double comm_bytes;            /* multi-rank: bytes this rank all-reduced during the solve */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
 } arslam_lm_summary;
