@@ -192,6 +192,8 @@ struct arslam_lm {
   arslam::LltPlan plan;
   double *x = nullptr, *xc = nullptr;
   unsigned long long dbg_indefinite_mask = 0;   // arslam_lm_debug_force_indefinite
+  arslam_iteration_callback iter_cb = nullptr;  // arslam_lm_set_iteration_callback
+  void *iter_cb_ctx = nullptr;
   int n_fparts = 0;
 
   Timer timers[PH_N];
@@ -637,6 +639,15 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     t_iter = tn;
     if (s->n_iters <= ARSLAM_LM_MAX_ITERS) s->iters[s->n_iters++] = it;
     if (o.minimizer_progress_to_stdout && root) print_row(it);
+    if (iter_cb) {   // Ceres RunCallbacks: after the record, before the stop rules
+      const int r = iter_cb(iter_cb_ctx, &it);
+      if (r == ARSLAM_SOLVER_ABORT) {
+        s->termination = ARSLAM_USER_FAILURE; s->rule = ARSLAM_RULE_USER_CALLBACK; return true;
+      }
+      if (r == ARSLAM_SOLVER_TERMINATE_SUCCESSFULLY) {
+        s->termination = ARSLAM_USER_SUCCESS; s->rule = ARSLAM_RULE_USER_CALLBACK; return true;
+      }
+    }
     if (it.iteration >= o.max_num_iterations) {
       s->termination = ARSLAM_NO_CONVERGENCE; s->rule = ARSLAM_RULE_MAX_ITERS; return true;
     }
@@ -1153,6 +1164,13 @@ int arslam_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int arslam_lm_set_iteration_callback(arslam_lm *h, arslam_iteration_callback fn, void *ctx) {
+  if (!h) return ARSLAM_E_INVALID_ARG;
+  h->iter_cb = fn;
+  h->iter_cb_ctx = ctx;
+  return ARSLAM_OK;
 }
 
 int arslam_lm_debug_force_indefinite(arslam_lm *h, unsigned long long step_mask) {

@@ -28,10 +28,10 @@ LIB_PATH = os.environ.get("ARSLAM_LIB") or os.path.join(HERE, "libarslam_lm.so")
 MAX_ITERS = 1024
 COMM_ID_BYTES = 128
 
-TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE"}
+TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE", 3: "USER_SUCCESS", 4: "USER_FAILURE"}
 RULES = {0: "none", 1: "gradient_tolerance", 2: "parameter_tolerance", 3: "function_tolerance",
          4: "min_trust_region_radius", 5: "max_num_iterations", 6: "invalid_steps",
-         7: "evaluation_failed"}
+         7: "evaluation_failed", 8: "user_callback"}
 ERRORS = {-1: "INVALID_ARG", -2: "UNSUPPORTED", -3: "NO_DEVICE", -4: "HIP", -5: "OUT_OF_MEMORY",
           -6: "COMM", -7: "STATE", -8: "DEVICE"}
 
@@ -43,6 +43,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
            "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm", "arslam_lm_set_comm_callback",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
+           "arslam_lm_set_iteration_callback",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_break_dependency",
@@ -60,6 +61,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
 
 _dp = C.POINTER(C.c_double)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
+SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = 0, 1, 2
 _ip = C.POINTER(C.c_int)
 _up = C.POINTER(C.c_ubyte)
 
@@ -96,6 +98,9 @@ class Iteration(C.Structure):
                 ("trust_region_radius", C.c_double),
                 ("step_is_valid", C.c_int), ("step_is_successful", C.c_int),
                 ("iteration_time", C.c_double), ("cumulative_time", C.c_double)]
+
+
+ITER_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(Iteration))
 
 
 class Summary(C.Structure):
@@ -193,6 +198,7 @@ def lib():
     L.arslam_debug_dense_llt.argtypes = [C.c_long, _dp, _dp, _dp, C.POINTER(C.c_int)]
     L.arslam_debug_angle_axis_rotate.argtypes = [C.c_int, _dp, _dp, _dp, _ip]
     L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
+    L.arslam_lm_set_iteration_callback.argtypes = [C.c_void_p, ITER_CB, C.c_void_p]
     L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
     _lib = L
     return L
@@ -278,6 +284,24 @@ class _Handle:
         o = Options()
         _check(lib().arslam_lm_get_options(self._h, C.byref(o)))
         return o
+
+    def set_iteration_callback(self, fn):
+        """ceres::IterationCallback: fn(iteration dict) -> SOLVER_CONTINUE / SOLVER_ABORT /
+        SOLVER_TERMINATE_SUCCESSFULLY (None = continue); fn=None removes it."""
+        if fn is None:
+            self._iter_cb = None
+            _check(lib().arslam_lm_set_iteration_callback(self._h, C.cast(None, ITER_CB), None))
+            return
+
+        def tramp(ctx, it):
+            try:
+                d = {f: getattr(it.contents, f) for f, _ in Iteration._fields_}
+                r = fn(d)
+                return SOLVER_CONTINUE if r is None else int(r)
+            except Exception:   # noqa: BLE001 -- a raising callback aborts the solve
+                return SOLVER_ABORT
+        self._iter_cb = ITER_CB(tramp)
+        _check(lib().arslam_lm_set_iteration_callback(self._h, self._iter_cb, None))
 
     def debug_force_indefinite(self, step_mask):
         """Test hook: linear solves whose bit min(i,63) is set in step_mask see an indefinite

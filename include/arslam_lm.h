@@ -53,13 +53,14 @@ enum {
 enum { ARSLAM_ELIM_AUTO = 0, ARSLAM_ELIM_CAPTURES = 1 };
 
 /* Ceres termination types (ceres::TerminationType) */
-enum { ARSLAM_CONVERGENCE = 0, ARSLAM_NO_CONVERGENCE = 1, ARSLAM_FAILURE = 2 };
+enum { ARSLAM_CONVERGENCE = 0, ARSLAM_NO_CONVERGENCE = 1, ARSLAM_FAILURE = 2, ARSLAM_USER_SUCCESS = 3,
+       ARSLAM_USER_FAILURE = 4 };
 
 /* which termination test fired */
 enum {
   ARSLAM_RULE_NONE = 0, ARSLAM_RULE_GRADIENT = 1, ARSLAM_RULE_PARAMETER = 2,
   ARSLAM_RULE_FUNCTION = 3, ARSLAM_RULE_MIN_RADIUS = 4, ARSLAM_RULE_MAX_ITERS = 5,
-  ARSLAM_RULE_INVALID_STEPS = 6, ARSLAM_RULE_EVAL_FAILED = 7
+  ARSLAM_RULE_INVALID_STEPS = 6, ARSLAM_RULE_EVAL_FAILED = 7, ARSLAM_RULE_USER_CALLBACK = 8
 };
 
 /* ceres::Solver::Options subset used by ArSlamSolver::optimize
@@ -208,6 +209,18 @@ enum { ARSLAM_DT_F64 = 0, ARSLAM_DT_U8 = 1 };
 enum { ARSLAM_OP_SUM = 0, ARSLAM_OP_MAX = 1 };
 typedef int (*arslam_allreduce_fn)(void *ctx, void *buf, size_t count, int dtype, int op);
 int arslam_lm_set_comm_callback(arslam_lm *h, int rank, int nranks, arslam_allreduce_fn fn, void *ctx);
+
+/* ceres::IterationCallback (Solver::Options::callbacks; the reference installs
+ * one for its debug display, ar_slam_util.cpp:982-998, 1006-1009): called
+ * after every iteration is recorded (iteration 0 included), before the
+ * termination tests, with the parameter blocks already written back when
+ * update_state_every_iteration is set.  Return ARSLAM_SOLVER_CONTINUE,
+ * ARSLAM_SOLVER_ABORT (termination ARSLAM_USER_FAILURE) or
+ * ARSLAM_SOLVER_TERMINATE_SUCCESSFULLY (ARSLAM_USER_SUCCESS).  fn = NULL
+ * removes it.  Runs on the calling thread, inside arslam_lm_solve*. */
+enum { ARSLAM_SOLVER_CONTINUE = 0, ARSLAM_SOLVER_ABORT = 1, ARSLAM_SOLVER_TERMINATE_SUCCESSFULLY = 2 };
+typedef int (*arslam_iteration_callback)(void *ctx, const arslam_lm_iteration *it);
+int arslam_lm_set_iteration_callback(arslam_lm *h, arslam_iteration_callback fn, void *ctx);
 
 /* Diagnostics */
 int arslam_device_count(void);

@@ -85,6 +85,33 @@ def test_control_trace_matches_oracle(lm, name):
     assert abs(cam[0] - gold["final_focal"]) <= 1e-8 * gold["final_focal"]
 
 
+def test_iteration_callback(lm):
+    """ceres::IterationCallback semantics (the reference's debug display callback,
+    ar_slam_util.cpp:982-998): called once per recorded iteration from iteration 0, sees the
+    written-back state under update_state_every_iteration (:1006-1009), and can stop the solve
+    with USER_SUCCESS or USER_FAILURE."""
+    g = synth.config_graph("small")
+    seen = []
+    rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners,
+                            update_state_every_iteration=1)
+
+    def cb(it):
+        seen.append((it["iteration"], it["cost"], rp.camera[0]))
+    rp.set_iteration_callback(cb)
+    s = rp.solve()
+    assert [i for i, _, _ in seen] == [it["iteration"] for it in s["iterations"]]
+    assert [c for _, c, _ in seen] == [it["cost"] for it in s["iterations"]]
+    assert seen[0][2] == g.camera[0] and seen[-1][2] == rp.camera[0]   # state written back each time
+    rp.set_iteration_callback(lambda it: lm.SOLVER_TERMINATE_SUCCESSFULLY if it["iteration"] == 2 else None)
+    s = rp.solve()
+    assert (s["termination"], s["rule"], len(s["iterations"])) == ("USER_SUCCESS", "user_callback", 3)
+    rp.set_iteration_callback(lambda it: lm.SOLVER_ABORT)
+    s = rp.solve()
+    assert (s["termination"], len(s["iterations"])) == ("USER_FAILURE", 1)
+    rp.set_iteration_callback(None)
+    assert rp.solve()["termination"] == "CONVERGENCE"
+
+
 def test_broken_dependency_is_a_device_error(lm):
     """A task-graph wait that can never be met ends the solve with ARSLAM_E_DEVICE naming the
     ticket (it used to become an invalid LM step); a fresh load solves normally again."""
