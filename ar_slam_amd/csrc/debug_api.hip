@@ -228,6 +228,22 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
   }
 }
 
+extern "C" int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[4]) {
+  if (!p || !out) return ARSLAM_E_INVALID_ARG;
+  try {
+    const arslam::SchurSide cs = arslam::ceres_schur_side(p);
+    out[0] = cs.e_cap;
+    out[1] = cs.e_tag;
+    out[2] = cs.e_cam;
+    out[3] = cs.max_tag_obs;
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}
+
 // diagnostic build only (-DARSLAM_SCHUR_STAMPS): accumulated per-phase cycles of k_schur
 extern "C" int arslam_debug_schur_stamps(unsigned long long out[16]) {
   if (!out) return ARSLAM_E_INVALID_ARG;

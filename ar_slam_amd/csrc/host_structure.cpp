@@ -415,6 +415,113 @@ double scalar_cholesky_flops(const std::vector<std::vector<int>> &adj, const std
   return flops;
 }
 
+// Ceres 2.0 (reorder_program.cc ComputeStableSchurOrdering, graph_algorithms.h
+// StableIndependentSetOrdering): vertices are the
+// non-constant parameter blocks in program order -- the order in which
+// AddResidualBlock(cost, nullptr, camera, capture, tag) first saw them,
+// ar_slam_util.cpp:723-727 -- with an edge between every two non-constant
+// blocks of one residual.  The vertices are stable-sorted by ascending degree
+// and taken greedily: a vertex none of whose neighbours is taken joins the
+// independent set (the e-blocks).
+SchurSide ceres_schur_side(const arslam_soa_problem *p) {
+  SchurSide out;
+  api_check(p != nullptr, ARSLAM_E_INVALID_ARG, "null problem");
+  api_check(p->n_cap >= 0 && p->n_tag >= 0 && p->n_obs >= 0, ARSLAM_E_INVALID_ARG, "negative sizes");
+  api_check(!p->n_obs || (p->obs_cap && p->obs_tag), ARSLAM_E_INVALID_ARG, "null observation arrays");
+  const int nc = p->n_cap, nt = p->n_tag, nb = p->n_obs;
+  for (int b = 0; b < nb; ++b) {
+    api_check(p->obs_cap[b] >= 0 && p->obs_cap[b] < nc, ARSLAM_E_INVALID_ARG, "obs_cap out of range");
+    api_check(p->obs_tag[b] >= 0 && p->obs_tag[b] < nt, ARSLAM_E_INVALID_ARG, "obs_tag out of range");
+  }
+  if (nb == 0) return out;
+  auto cap_free = [&](int c) { return !(p->cap_const && p->cap_const[c]); };
+  auto tag_free = [&](int t) { return !(p->tag_const && p->tag_const[t]); };
+  const bool cam_free = !p->camera_const;
+  // distinct (capture, tag) pairs in both directions
+  std::vector<std::pair<int, int>> ct(nb);
+  for (int b = 0; b < nb; ++b) ct[b] = {p->obs_cap[b], p->obs_tag[b]};
+  std::vector<int> tag_nobs(nt, 0);
+  for (int b = 0; b < nb; ++b) out.max_tag_obs = std::max(out.max_tag_obs, ++tag_nobs[p->obs_tag[b]]);
+  std::sort(ct.begin(), ct.end());
+  ct.erase(std::unique(ct.begin(), ct.end()), ct.end());
+  std::vector<int> cap_adj_start(nc + 1, 0), tag_adj_start(nt + 1, 0);
+  for (auto &e : ct) {
+    if (!cap_free(e.first) || !tag_free(e.second)) continue;
+    cap_adj_start[e.first + 1]++;
+    tag_adj_start[e.second + 1]++;
+  }
+  for (int c = 0; c < nc; ++c) cap_adj_start[c + 1] += cap_adj_start[c];
+  for (int t = 0; t < nt; ++t) tag_adj_start[t + 1] += tag_adj_start[t];
+  std::vector<int> cap_adj(cap_adj_start[nc]), tag_adj(tag_adj_start[nt]);
+  {
+    std::vector<int> fc(cap_adj_start.begin(), cap_adj_start.end() - 1), ft(tag_adj_start.begin(), tag_adj_start.end() - 1);
+    for (auto &e : ct) {
+      if (!cap_free(e.first) || !tag_free(e.second)) continue;
+      cap_adj[fc[e.first]++] = e.second;
+      tag_adj[ft[e.second]++] = e.first;
+    }
+  }
+  // vertex ids: 0 camera, 1 + c capture, 1 + nc + t tag; program order
+  const int nv = 1 + nc + nt;
+  std::vector<int> order;
+  order.reserve(nv);
+  std::vector<char> seen(nv, 0);
+  auto visit = [&](int v, bool free_) {
+    if (free_ && !seen[v]) { seen[v] = 1; order.push_back(v); }
+  };
+  for (int b = 0; b < nb; ++b) {
+    visit(0, cam_free);
+    visit(1 + p->obs_cap[b], cap_free(p->obs_cap[b]));
+    visit(1 + nc + p->obs_tag[b], tag_free(p->obs_tag[b]));
+  }
+  const int cam_deg = (int)order.size() - (cam_free ? 1 : 0);
+  auto degree = [&](int v) {
+    if (v == 0) return cam_deg;
+    if (v <= nc) return cap_adj_start[v] - cap_adj_start[v - 1] + (cam_free ? 1 : 0);
+    const int t = v - 1 - nc;
+    return tag_adj_start[t + 1] - tag_adj_start[t] + (cam_free ? 1 : 0);
+  };
+  std::vector<int> deg(nv, 0);
+  for (int v : order) deg[v] = degree(v);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return deg[a] < deg[b]; });
+  enum : char { kWhite = 0, kGrey = 1, kBlack = 2 };
+  std::vector<char> color(nv, kWhite);
+  for (int v : order) {
+    if (color[v] != kWhite) continue;
+    color[v] = kBlack;
+    if (v == 0) {
+      ++out.e_cam;
+      for (int u : order) if (u != 0 && color[u] == kWhite) color[u] = kGrey;   // every block shares a residual with it
+      continue;
+    }
+    if (cam_free && color[0] == kWhite) color[0] = kGrey;
+    if (v <= nc) {
+      ++out.e_cap;
+      for (int q = cap_adj_start[v - 1]; q < cap_adj_start[v]; ++q) {
+        const int u = 1 + nc + cap_adj[q];
+        if (color[u] == kWhite) color[u] = kGrey;
+      }
+    } else {
+      ++out.e_tag;
+      const int t = v - 1 - nc;
+      for (int q = tag_adj_start[t]; q < tag_adj_start[t + 1]; ++q) {
+        const int u = 1 + tag_adj[q];
+        if (color[u] == kWhite) color[u] = kGrey;
+      }
+    }
+  }
+  return out;
+}
+
+arslam_soa_problem swap_roles(const arslam_soa_problem &p) {
+  arslam_soa_problem s = p;
+  s.n_cap = p.n_tag; s.n_tag = p.n_cap;
+  s.cap = p.tag; s.tag = p.cap;
+  s.obs_cap = p.obs_tag; s.obs_tag = p.obs_cap;
+  s.cap_const = p.tag_const; s.tag_const = p.cap_const;
+  return s;
+}
+
 HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum) {
   api_check(p != nullptr, ARSLAM_E_INVALID_ARG, "null problem");
   api_check(p->n_cap >= 0 && p->n_tag >= 0 && p->n_obs >= 0, ARSLAM_E_INVALID_ARG, "negative sizes");

@@ -65,6 +65,18 @@ std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>
 
 HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum);
 
+// Ceres 2.0's e-block set for DENSE_SCHUR with no user ordering
+// (ReorderProgramForSchurTypeLinearSolver -> ComputeStableSchurOrdering ->
+// StableIndependentSetOrdering), counted by kind; max_tag_obs = most
+// observations of one tag (the per-e-block limit if tags are eliminated).
+struct SchurSide {
+  int e_cap = 0, e_tag = 0, e_cam = 0;
+  int max_tag_obs = 0;
+};
+SchurSide ceres_schur_side(const arslam_soa_problem *p);
+// the same problem with the roles of captures and tags exchanged (pointers only)
+arslam_soa_problem swap_roles(const arslam_soa_problem &p);
+
 // Row layout of the reduced system and its tile pattern (before fill).
 //   ordering 0 natural, 1 reverse Cuthill-McKee, 2 nested dissection (parts
 //   aligned to 64-row tiles); the camera's 3 rows come last; the rhs is row nR.

@@ -43,6 +43,11 @@ struct DevProblem {
   long N;              // padded matrix size (multiple of kTile, > nR)
   long lda;            // leading dimension of S
   int max_obs_per_cap;
+  // 1: the e-blocks (the "capture" slots, CSR cap_start) are the problem's tags
+  // and the f-blocks (the "tag" slots) its captures -- ARSLAM_ELIM_TAGS: the
+  // residual is then evaluated with the two pose arguments exchanged and the
+  // two 6-column halves of its Jacobian row swapped back into e|f order
+  int swap_roles;
   int cam_row;               // first reduced row of the camera block, -1 if the camera is not free
   const int *cap_start;      // [nc+1]  CSR of observations by capture
   const int *obs_tag;        // [nb]

@@ -69,8 +69,19 @@ __device__ void fill_rows(const DevProblem &P, const double *x, const double *sc
     const int t = P.obs_tag[obs];
     const double *tag = x + slot_tag(P, t);
     double J[13];
-    const double r = residual_jacobian_row(cam, cap, tag, corner, comp,
+    // (tag elimination: the e-block is the problem's tag -- projectCorner
+    // still takes the capture first; the Jacobian halves come back as e|f)
+    const bool sw = P.swap_roles != 0;
+    const double r = residual_jacobian_row(cam, sw ? tag : cap, sw ? cap : tag, corner, comp,
                                            P.corners[8L * obs + 2 * corner + comp], J);
+    if (sw) {
+#pragma unroll
+      for (int j = 1; j < 7; ++j) {
+        const double v = J[j];
+        J[j] = J[j + 6];
+        J[j + 6] = v;
+      }
+    }
     double *dst = rows + (long)row * kRowStride;
     if (scale) {
       const double *sc = scale + slot_cap(P, c);
@@ -824,8 +835,10 @@ __global__ __launch_bounds__(kWave) void k_cost(DevProblem P, const double *__re
       const int obs = o0 + q;
       const double *tag = x + slot_tag(P, P.obs_tag[obs]);
       const AngleAxis at = aa_prepare(tag + 3);
-      const double r = residual_row(ac, cap, at, tag, cam[0], corner, comp,
-                                    P.corners[8L * obs + 2 * corner + comp], nullptr, nullptr);
+      const double obsv = P.corners[8L * obs + 2 * corner + comp];
+      const bool sw = P.swap_roles != 0;   // tag elimination: the capture is the f-block
+      const double r = residual_row(sw ? at : ac, sw ? tag : cap, sw ? ac : at, sw ? cap : tag, cam[0], corner,
+                                    comp, obsv, nullptr, nullptr);
       if (!isfinite(r)) bad = 1.0;
       r2 = r * r;
     }

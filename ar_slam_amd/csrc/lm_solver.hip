@@ -285,6 +285,8 @@ struct arslam_lm {
   }
 
   void load(const arslam_soa_problem *p);
+  int elim_used = ARSLAM_ELIM_CAPTURES;   // the side load() eliminates (the device problem is role-swapped for TAGS)
+  int ceres_e_cap = 0, ceres_e_tag = 0;   // Ceres 2.0's e-block set of the loaded problem, by kind
   void reload_values(const arslam_soa_problem *p);
   bool pk_loaded = false;   // the resident problem came from the pointer-keyed API
   bool reuse_order = false;  // load(): keep the previous tag order when the free tags are unchanged
@@ -319,9 +321,26 @@ long round_up(long v, long m) { return (v + m - 1) / m * m; }
 
 }  // namespace
 
-void arslam_lm::load(const arslam_soa_problem *p) {
+void arslam_lm::load(const arslam_soa_problem *p_in) {
   const double t_load = now_s();
   loaded = false;
+  // the e-block side (ARSLAM_ELIM_*): Ceres' own independent set decides AUTO;
+  // tag elimination runs the same kernels on the role-swapped problem
+  const arslam::SchurSide cs = arslam::ceres_schur_side(p_in);
+  ceres_e_cap = cs.e_cap;
+  ceres_e_tag = cs.e_tag;
+  int side = opt.elimination;
+  if (side == ARSLAM_ELIM_AUTO)
+    side = (nranks == 1 && cs.e_tag > cs.e_cap && cs.max_tag_obs <= arslam::kMaxObsPerCapture) ? ARSLAM_ELIM_TAGS
+                                                                                              : ARSLAM_ELIM_CAPTURES;
+  fail_if(side == ARSLAM_ELIM_TAGS && nranks > 1, ARSLAM_E_UNSUPPORTED,
+          "tag elimination is single-rank only (the shards are capture ranges)");
+  fail_if(side == ARSLAM_ELIM_TAGS && cs.max_tag_obs > arslam::kMaxObsPerCapture, ARSLAM_E_UNSUPPORTED,
+          "tag elimination: more than 64 observations of one tag");
+  if (side != elim_used) prev_tag_row.clear();   // the f-side changed: no order to reuse
+  elim_used = side;
+  const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
+  const arslam_soa_problem *p = side == ARSLAM_ELIM_TAGS ? &swapped : p_in;
   if (nranks > 1) ensure_stream();   // the structure exchange below runs on the device
   // host structure; with several ranks the tag use, the co-visibility and the
   // tile pattern are made global by max/sum all-reduces (same on every rank)
@@ -450,6 +469,7 @@ void arslam_lm::load(const arslam_soa_problem *p) {
 
   P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nR = nR; P.N = N; P.lda = N; P.cam_row = cam_row;
   P.max_obs_per_cap = std::max(maxk, 1);
+  P.swap_roles = elim_used == ARSLAM_ELIM_TAGS ? 1 : 0;
   P.cap_start = d_cap_start.p; P.obs_tag = d_obs_tag.p; P.obs_lblk = d_obs_lblk.p;
   P.cap_blk_start = d_cap_blk_start.p; P.blk_tag = d_blk_tag.p;
   P.obs_active = d_obs_active.p; P.slot_free = d_slot_free.p;
@@ -472,8 +492,10 @@ void arslam_lm::load(const arslam_soa_problem *p) {
 
 // Same structure as the loaded problem, new parameter values (the pointer-keyed
 // path when no block, residual or constant changed since the last load).
-void arslam_lm::reload_values(const arslam_soa_problem *p) {
+void arslam_lm::reload_values(const arslam_soa_problem *p_in) {
   const double t0 = now_s();
+  const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
+  const arslam_soa_problem *p = elim_used == ARSLAM_ELIM_TAGS ? &swapped : p_in;
   fail_if(!loaded || p->n_cap != nc || p->n_tag != nt || p->n_obs != nb, ARSLAM_E_STATE,
           "reload_values: structure differs from the loaded problem");
   std::memcpy(x0.data(), p->camera, 3 * sizeof(double));
@@ -868,6 +890,9 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->factor_update_flops = plan.total_upd_flops;
   s->factor_scalar_flops = scalar_flops;
   s->comm_bytes = comm_bytes;
+  s->elimination_used = elim_used;
+  s->ceres_e_captures = ceres_e_cap;
+  s->ceres_e_tags = ceres_e_tag;
 }
 
 // ===========================================================================
@@ -940,9 +965,9 @@ int arslam_lm_create(arslam_lm **out, const arslam_lm_options *opt) {
   return guarded([&] {
     auto *h = new arslam_lm();
     if (opt) h->opt = *opt; else arslam_lm_options_init(&h->opt);
-    if (h->opt.elimination != ARSLAM_ELIM_AUTO && h->opt.elimination != ARSLAM_ELIM_CAPTURES) {
+    if (h->opt.elimination < ARSLAM_ELIM_AUTO || h->opt.elimination > ARSLAM_ELIM_TAGS) {
       delete h;
-      throw Error(ARSLAM_E_UNSUPPORTED, "only capture elimination is implemented");
+      throw Error(ARSLAM_E_INVALID_ARG, "elimination must be ARSLAM_ELIM_AUTO, _CAPTURES or _TAGS");
     }
     *out = h;
   });
@@ -953,14 +978,14 @@ void arslam_lm_destroy(arslam_lm *h) { delete h; }
 int arslam_lm_set_options(arslam_lm *h, const arslam_lm_options *opt) {
   if (!h || !opt) return ARSLAM_E_INVALID_ARG;
   return guarded([&] {
-    fail_if(opt->elimination != ARSLAM_ELIM_AUTO && opt->elimination != ARSLAM_ELIM_CAPTURES,
-            ARSLAM_E_UNSUPPORTED, "only capture elimination is implemented");
+    fail_if(opt->elimination < ARSLAM_ELIM_AUTO || opt->elimination > ARSLAM_ELIM_TAGS, ARSLAM_E_INVALID_ARG,
+            "elimination must be ARSLAM_ELIM_AUTO, _CAPTURES or _TAGS");
     fail_if(opt->factor_executor != 0 && opt->factor_executor != 1, ARSLAM_E_INVALID_ARG,
             "factor_executor must be 0 or 1");
     fail_if(opt->max_num_iterations < 0 || opt->max_num_iterations > ARSLAM_LM_MAX_ITERS,
             ARSLAM_E_INVALID_ARG, "max_num_iterations out of range");
     if (opt->device != h->opt.device || opt->reduced_ordering != h->opt.reduced_ordering ||
-        opt->cholesky_skip_zero_tiles != h->opt.cholesky_skip_zero_tiles)
+        opt->cholesky_skip_zero_tiles != h->opt.cholesky_skip_zero_tiles || opt->elimination != h->opt.elimination)
       h->loaded = false, h->pk_dirty = true;
     h->opt = *opt;
   });

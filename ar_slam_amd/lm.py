@@ -47,7 +47,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_break_dependency",
-           "arslam_debug_reduced_plan", "arslam_debug_schur_stamps",
+           "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
            "arslam_slam_create", "arslam_slam_destroy", "arslam_slam_set_verbose", "arslam_slam_load_yaml",
@@ -62,6 +62,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
 _dp = C.POINTER(C.c_double)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
 SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = 0, 1, 2
+ELIM_AUTO, ELIM_CAPTURES, ELIM_TAGS = 0, 1, 2   # arslam_lm_options.elimination
 _ip = C.POINTER(C.c_int)
 _up = C.POINTER(C.c_ubyte)
 
@@ -120,6 +121,7 @@ class Summary(C.Structure):
                 ("n_factor_tiles", C.c_long), ("n_levels", C.c_int), ("n_update_tiles", C.c_long),
                 ("factor_update_flops", C.c_double), ("factor_scalar_flops", C.c_double),
                 ("comm_bytes", C.c_double),
+                ("elimination_used", C.c_int), ("ceres_e_captures", C.c_int), ("ceres_e_tags", C.c_int),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 
     def to_dict(self):
@@ -197,6 +199,7 @@ def lib():
     L.arslam_debug_residual_jacobian.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp, _dp]
     L.arslam_debug_dense_llt.argtypes = [C.c_long, _dp, _dp, _dp, C.POINTER(C.c_int)]
     L.arslam_debug_angle_axis_rotate.argtypes = [C.c_int, _dp, _dp, _dp, _ip]
+    L.arslam_debug_ceres_e_blocks.argtypes = [C.POINTER(SoaProblem), _ip]
     L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
     L.arslam_lm_set_iteration_callback.argtypes = [C.c_void_p, ITER_CB, C.c_void_p]
     L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
@@ -469,6 +472,18 @@ def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const
     _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
                                            tag_row.ctypes.data_as(_ip)))
     return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]
+
+
+def debug_ceres_e_blocks(camera, cap, tag, obs_cap, obs_tag, corners=None, camera_const=False, cap_const=None,
+                         tag_const=None):
+    """Host-only: Ceres 2.0's DENSE_SCHUR e-block set (the rule ELIM_AUTO follows), as
+    {captures, tags, camera, max_tag_obs}."""
+    if corners is None:
+        corners = np.zeros((len(obs_cap), 8))
+    A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const, cap_const, tag_const)
+    out = np.zeros(4, np.int32)
+    _check(lib().arslam_debug_ceres_e_blocks(C.byref(A.s), out.ctypes.data_as(_ip)))
+    return dict(captures=int(out[0]), tags=int(out[1]), camera=int(out[2]), max_tag_obs=int(out[3]))
 
 
 # ---- batched localize (include/arslam_localize.h) ----

@@ -49,8 +49,15 @@ enum {
   ARSLAM_E_DEVICE = -8          /* a device executor fault (a dependency wait that never completed) */
 };
 
-/* which side of the camera/tag graph the Schur complement eliminates */
-enum { ARSLAM_ELIM_AUTO = 0, ARSLAM_ELIM_CAPTURES = 1 };
+/* Which side of the capture/tag graph the Schur complement eliminates
+ * (DENSE_SCHUR's e-blocks, ar_slam_util.cpp:1011).  AUTO follows Ceres 2.0's
+ * own choice (ReorderProgramForSchurTypeLinearSolver -> ComputeStableSchurOrdering:
+ * the stable greedy independent set of the Hessian graph in ascending degree,
+ * blocks in program order): the side that holds the majority of that set is
+ * eliminated (Ceres may mix the two sides; the step is the same exact solve of
+ * the same system, only the rounding differs).  Multi-rank solves always
+ * eliminate captures (the shards are capture ranges). */
+enum { ARSLAM_ELIM_AUTO = 0, ARSLAM_ELIM_CAPTURES = 1, ARSLAM_ELIM_TAGS = 2 };
 
 /* Ceres termination types (ceres::TerminationType) */
 enum { ARSLAM_CONVERGENCE = 0, ARSLAM_NO_CONVERGENCE = 1, ARSLAM_FAILURE = 2, ARSLAM_USER_SUCCESS = 3,
@@ -130,6 +137,9 @@ typedef struct {
   double factor_scalar_flops;   /* flops of the scalar Cholesky of the real rows (the algorithmic count:
                                    no padding rows, no zeros inside fill tiles) per factorization */
   double comm_bytes;            /* multi-rank: bytes this rank all-reduced during the solve */
+  int elimination_used;         /* ARSLAM_ELIM_CAPTURES or ARSLAM_ELIM_TAGS */
+  int ceres_e_captures;         /* Ceres 2.0's e-block set for this problem (ComputeStableSchurOrdering): */
+  int ceres_e_tags;             /*   captures and tags in it (the camera joins it only in degenerate graphs) */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
 } arslam_lm_summary;

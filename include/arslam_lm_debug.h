@@ -77,6 +77,11 @@ int arslam_debug_schur_stamps(unsigned long long out[16]);
 int arslam_lm_debug_force_indefinite(arslam_lm *h, unsigned long long step_mask);
 int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken);
 
+/* Ceres 2.0's DENSE_SCHUR e-block set for problem p (ComputeStableSchurOrdering,
+ * the rule ARSLAM_ELIM_AUTO follows), host only: out = {captures, tags,
+ * camera (0/1) in the set, most observations of one tag}. */
+int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[4]);
+
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);
 
