@@ -652,7 +652,23 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
 //               target's earlier levels, so the summation order is fixed.
 // ---------------------------------------------------------------------------
 constexpr int kLtdSize = 4 * 16 * LI;   // 1152 doubles
-constexpr long kSpinCap = 1L << 16;   // ~0.1 s of polling: far beyond any legitimate wait
+constexpr long kSpinCap = 1L << 16;
+// s_sleep units (64 cycles) between two polls of a dependency counter.  Every
+// poll is a device-scope atomic performed at the memory side; with a few
+// hundred update tasks waiting at once, polling every 64 cycles slowed the
+// whole factorization (the chain's own loads and hand-offs queue behind the
+// polls): cfg3 k_factor_dag 796 -> 757 us with the update tasks polling
+// every 16 units, flat from 16 to 32, worse at 64 (tools/variant_bench.sh).
+// The chain tasks (POTRF, TRSM) and the backward solve keep polling fast.
+#ifndef ARSLAM_POLL_SLEEP
+#define ARSLAM_POLL_SLEEP 16   // update tasks
+#endif
+#ifndef ARSLAM_CHAIN_SLEEP
+#define ARSLAM_CHAIN_SLEEP 1   // POTRF / TRSM tasks
+#endif
+#ifndef ARSLAM_BSOLVE_SLEEP
+#define ARSLAM_BSOLVE_SLEEP 1  // k_bsolve_dag (its waits are all on the chain)
+#endif   // ~0.1 s of polling: far beyond any legitimate wait
 
 // Poll a dependency counter with an atomic read-modify-write (+0): counters
 // are advanced by device-scope atomic adds, and an RMW is performed where
@@ -757,17 +773,25 @@ __device__ __forceinline__ void store_tile_wt(double *__restrict__ g, const doub
 // broken graph drains in one spin cap instead of one per task.  Lane q polls
 // wait q (64 at a time), so a task's counters are read in one round trip, not
 // one after another.
-__device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag, int lane) {
+__device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag, int lane, bool chain) {
   for (int base = w0; base < w1; base += 64) {
     const int w = base + lane;
     const bool mine = w < w1;
     const int2 cv = mine ? waits[w] : make_int2(0, 0);
     long spins = 0;
+#ifdef ARSLAM_POLL_ONCE
+    bool open = mine;   // lanes whose counter has reached its value stop polling (counters only grow)
+    for (;;) {
+      if (open) open = ld_acquire_relaxed(counters + cv.x) < cv.y;
+      if (__builtin_amdgcn_ballot_w64(open) == 0) break;
+#else
     for (;;) {
       // (every lane re-polls each round: no loop-carried per-lane state)
       const int got = mine ? ld_acquire_relaxed(counters + cv.x) : 0;
       if (__builtin_amdgcn_ballot_w64(mine && got < cv.y) == 0) break;
-      __builtin_amdgcn_s_sleep(1);
+#endif
+      if (chain) __builtin_amdgcn_s_sleep(ARSLAM_CHAIN_SLEEP);
+      else __builtin_amdgcn_s_sleep(ARSLAM_POLL_SLEEP);
       if (++spins > kSpinCap) return false;
       if ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0) return false;
     }
@@ -884,7 +908,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     const int2 sub = a.sub[t];
     if (w == 0) {
       const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], sub.x >= 0 ? sub.y : a.wait_off[t + 1], a.flag,
-                               lane);
+                               lane, task.x != 2);
       if (lane == 0) {
         if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
         // a drawn continuation target: run it only if its predecessor did not claim it
@@ -991,7 +1015,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         const bool pref = sh[5] != 0;   // (written inside the POTRF, barriers since)
         if (!pref) {
           if (w == 0) {
-            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane);
+            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane, true);
             if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
           }
           __syncthreads();
@@ -1127,7 +1151,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           long spins = 0;
           bool ok = true;
           while (ld_acquire_relaxed(applied + task.w) < task.z) {
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(ARSLAM_POLL_SLEEP);
             if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(a.flag) < 0)) {
               ok = false;
               break;
@@ -1309,7 +1333,7 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
         if (lane == 0) {
           long spins = 0;
           while (ld_acquire_relaxed(done + i) < 1) {
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(ARSLAM_BSOLVE_SLEEP);
             if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(flag) != 0)) {
               atomicCAS(flag, 0, -(4000000 + b));
               ok = false;
