@@ -1393,25 +1393,34 @@ void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s) {
 namespace {
 // One launch zeroing the persistent executors' counters (and the step's
 // failure flag) instead of a fill launch per array.
-__global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c, long nc, int *d, long nd) {
+// (with ld.n > 0 also the step's LM diagonal: k_lm_diag's work, one launch less)
+__global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c, long nc, int *d, long nd,
+                             LmDiagArgs ld) {
   const long n = na + nb + nc + nd;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n + ld.n; e += (long)gridDim.x * blockDim.x) {
     if (e < na) a[e] = 0;
     else if (e < na + nb) b[e - na] = 0;
     else if (e < na + nb + nc) c[e - na - nb] = 0;
-    else d[e - na - nb - nc] = 0;
+    else if (e < n) d[e - na - nb - nc] = 0;
+    else {
+      const long i = e - n;
+      const double v = ld.scale[i] * ld.scale[i] * ld.colnorm[i];   // squared column norm of J diag(s)
+      ld.diag[i] = fmin(fmax(v, ld.dmin), ld.dmax);
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 0;
 }
 }  // namespace
 
-void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s) {
+void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagArgs *ld) {
   const long na = P.n_dag_tasks ? 2 * P.n_tiles + 2 : 0, nb = P.n_dag_tasks, nc = P.n_split,
              nd = P.h_bcols.empty() ? 0 : (long)P.T + 1;
-  const long n = na + nb + nc + nd;
+  LmDiagArgs l{};
+  if (ld) l = *ld;
+  const long n = na + nb + nc + nd + l.n;
   const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 1024));
   hipLaunchKernelGGL(k_exec_reset, dim3(grid), dim3(256), 0, s, flag, P.dag_counters, na, P.dag_claimed, nb,
-                     P.upd_cnt, nc, P.bs_counters, nd);
+                     P.upd_cnt, nc, P.bs_counters, nd, l);
 }
 
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s) {

@@ -48,6 +48,8 @@ struct DevProblem {
   // residual is then evaluated with the two pose arguments exchanged and the
   // two 6-column halves of its Jacobian row swapped back into e|f order
   int swap_roles;
+  int nf;                    // f-side parameter slots: camera 3 + 6 nt
+  const int *fslot_row;      // [nf]    reduced row of f-side slot j (camera j < 3, tag slot 3 + 6 t + a), -1 if none
   int cam_row;               // first reduced row of the camera block, -1 if the camera is not free
   const int *cap_start;      // [nc+1]  CSR of observations by capture
   const int *obs_tag;        // [nb]
@@ -171,13 +173,17 @@ void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double
                   hipStream_t s);
 void launch_lm_diag(const DevProblem &P, const double *scale, const double *colnorm, double dmin,
                     double dmax, double *diag, hipStream_t s);
+// (prep = true: k_prep_reduced's diagonal work is done by the gather itself --
+// single rank only, where the gathered S is final)
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                  double radius, double *S, hipStream_t s);
+                  double radius, double *S, hipStream_t s, bool prep = false);
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
                          hipStream_t s);
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
                     double radius, const double *yF, double *xc, double *parts, hipStream_t s,
                     bool reuse_ui = false);
+// candidate f-side slots: xc = x - s yF on reduced rows, xc = x elsewhere (every
+// f-side slot is written); fparts: 2 per 256 reduced rows
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,
                      double *xc, double *fparts, hipStream_t s);
 void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_t s);
@@ -214,8 +220,16 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
 // (reset = false: the counters were zeroed by launch_exec_reset)
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups,
                           int *progress = nullptr, unsigned long long *trace = nullptr, bool reset = true);
+// the LM diagonal clamp(s^2 colnorm, dmin, dmax) over n slots (k_lm_diag)
+struct LmDiagArgs {
+  long n;
+  const double *scale, *colnorm;
+  double dmin, dmax;
+  double *diag;
+};
 // *flag and every counter of the two persistent executors to zero, one launch
-void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s);
+// (with ld: the LM diagonal in the same launch)
+void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagArgs *ld = nullptr);
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s);
 // The same backward solve as one persistent launch (columns in root-first

@@ -576,10 +576,41 @@ __device__ __forceinline__ double gather_groups(double s, const GatherLane &g, d
 // G lane groups stride over them with 8 slab loads in flight per lane, and
 // the groups' partials are added in group order -- a fixed summation order,
 // no atomics.  Pieces store partial sums for k_schur_combine.
-__global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__restrict__ S) {
+// The D_f^2 of a reduced row's diagonal element (prep: the gather adds it when
+// it writes the element, k_prep_reduced's work), else 0.
+__device__ __forceinline__ double prep_d2(const DevProblem &P, const double *diag, double radius, long r,
+                                          long col) {
+  if (!diag || r != col || r >= P.nR) return 0.0;
+  const int slot = P.row_slot[r];
+  return slot >= 0 ? lm_d2(diag, slot, radius) : 0.0;
+}
+
+// k_prep_reduced's diagonal elements that no gather item writes: alignment
+// padding and the rows past the rhs become identity rows, the rhs row a pivot
+// large enough to stay positive (in prep mode the gather leaves the rhs-rhs
+// element to this), the camera's l1/l2 rows get their D_f^2
+__device__ __forceinline__ void prep_pad_row(const DevProblem &P, const double *diag, double radius, double *S,
+                                             long i) {
+  if (i >= P.N) return;
+  if (i < P.nR && P.row_slot[i] >= 0) {
+    // the camera's l1, l2 rows (zero Jacobian columns, no Schur block): D_f^2 only
+    if (P.cam_row >= 0 && i > P.cam_row && i <= P.cam_row + 2)
+      *reduced_elem(S, P, i, i) = lm_d2(diag, P.row_slot[i], radius);
+    return;
+  }
+  *reduced_elem(S, P, i, i) = i == P.nR ? 1e300 : 1.0;
+}
+
+__global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__restrict__ S,
+                                                      const double *__restrict__ diag, double radius) {
   __shared__ double part[4][kWave];
   __shared__ SchurContrib cts[4][kWave];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n_item_blocks = (P.n_items + 3) / 4;
+  if (diag && (int)blockIdx.x >= n_item_blocks) {   // (prep) the rows no item writes
+    prep_pad_row(P, diag, radius, S, (long)(blockIdx.x - n_item_blocks) * 256 + threadIdx.x);
+    return;
+  }
   const int it = blockIdx.x * 4 + w;
   if (it >= P.n_items) return;
   const int4 item = P.gather_items[it];
@@ -610,12 +641,13 @@ __global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__re
     P.gather_part[(long)item.w * 36 + lane] = s;
   } else {
     const long r = rr.x + g.i, col = rr.y + g.j;
-    if (r >= col) *reduced_elem(S, P, r, col) = s;
+    if (r >= col && !(diag && r == P.nR && col == P.nR)) *reduced_elem(S, P, r, col) = s + prep_d2(P, diag, radius, r, col);
   }
 }
 
 // Split destinations: the pieces' partial sums, in piece order.
-__global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__restrict__ S) {
+__global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__restrict__ S,
+                                                       const double *__restrict__ diag, double radius) {
   __shared__ double part[4][kWave];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int sp = blockIdx.x * 4 + w;
@@ -636,7 +668,8 @@ __global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__r
   }
   s = gather_groups(s, g, part[w], lane);
   const long r = rr.x + g.i, col = rr.y + g.j;
-  if (lane < g.E && r >= col) *reduced_elem(S, P, r, col) = s;
+  if (lane < g.E && r >= col && !(diag && r == P.nR && col == P.nR))
+    *reduced_elem(S, P, r, col) = s + prep_d2(P, diag, radius, r, col);
 }
 
 // S[i][i] += D_f^2 for the reduced (tag + camera) rows; alignment padding and
@@ -781,7 +814,9 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   }
 }
 
-// Candidate update of the tag and camera slots from the reduced solution.
+// Candidate update of the tag and camera slots from the reduced solution
+// (every f-side slot of xc is written, so xc needs no copy of x first:
+// k_backsub writes every capture slot).
 __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__restrict__ x,
                                                   const double *__restrict__ scale,
                                                   const double *__restrict__ yF,
@@ -791,7 +826,7 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0;
   const long slot = i < P.nR ? P.row_slot[i] : -1;
-  if (slot >= 0) {
+  if (slot >= 0) {   // reduced row i
     const double yv = yF[i];
     const double xo = x[slot];
     const double xn = xo + (-yv * scale[slot]);
@@ -799,6 +834,11 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
     if (P.slot_free[slot]) st = (xo - xn) * (xo - xn);
     bad = isfinite(yv) ? 0.0 : 1.0;
   }
+  if (i < P.nf && P.fslot_row[i] < 0) {   // f-side slot i outside the reduced system: unchanged
+    const long fs = i < 3 ? i : 3 + 6L * P.nc + (i - 3);
+    xc[fs] = x[fs];
+  }
+  if ((long)blockIdx.x * blockDim.x >= P.nR) return;   // (partials: one per 256 reduced rows)
   red[0][threadIdx.x] = st;
   red[1][threadIdx.x] = bad;
   __syncthreads();
@@ -1040,17 +1080,22 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
 }
 
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                  double radius, double *S, hipStream_t s) {
-  if (P.nc == 0) return;
+                  double radius, double *S, hipStream_t s, bool prep) {
+  if (P.nc == 0) {
+    if (prep) launch_prep_reduced(P, diag, radius, S, s);
+    return;
+  }
   const int maxk = P.max_obs_per_cap;
   const int m = 1 + 6 * maxk;
   const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 7L * m + 4 + 28L * maxk) +
                      sizeof(int) * (maxk + 2) + 2 * sizeof(double) + 64;
   hipLaunchKernelGGL(k_schur, dim3(P.nc), dim3(kWave), lds, s, P, scale, diag, radius);
-  if (P.n_items)
-    hipLaunchKernelGGL(k_schur_gather, dim3((unsigned)((P.n_items + 3) / 4)), dim3(256), 0, s, P, S);
+  const double *pd = prep ? diag : nullptr;
+  const unsigned gb = (unsigned)((P.n_items + 3) / 4) + (prep ? (unsigned)((P.N + 255) / 256) : 0u);
+  if (gb) hipLaunchKernelGGL(k_schur_gather, dim3(gb), dim3(256), 0, s, P, S, pd, radius);
   if (P.n_splits)
-    hipLaunchKernelGGL(k_schur_combine, dim3((unsigned)((P.n_splits + 3) / 4)), dim3(256), 0, s, P, S);
+    hipLaunchKernelGGL(k_schur_combine, dim3((unsigned)((P.n_splits + 3) / 4)), dim3(256), 0, s, P, S, pd,
+                       radius);
 }
 
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
@@ -1070,9 +1115,9 @@ void launch_backsub(const DevProblem &P, const double *x, const double *scale, c
 
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,
                      double *xc, double *fparts, hipStream_t s) {
-  if (P.nR == 0) return;
-  hipLaunchKernelGGL(k_update_f, dim3((unsigned)((P.nR + 255) / 256)), dim3(256), 0, s, P, x, scale, yF,
-                     xc, fparts);
+  const long n = std::max<long>(P.nR, P.nf);
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_update_f, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, x, scale, yF, xc, fparts);
 }
 
 void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_t s) {

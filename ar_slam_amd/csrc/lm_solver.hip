@@ -181,7 +181,7 @@ struct arslam_lm {
   DevBuf<double> d_corners, d_x0, d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_S, d_z, d_yF;
   double *d_norms_p = nullptr;   // inside d_red
-  DevBuf<int> d_flag, d_tag_row, d_row_slot;
+  DevBuf<int> d_flag, d_tag_row, d_row_slot, d_fslot_row;
   DevBuf<long> d_cap_off;
   DevBuf<double> d_slab, d_jrows, d_cap_ui;
   DevBuf<int2> d_dest_row;
@@ -436,6 +436,19 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   d_flag.alloc(1);
   d_tag_row.alloc(tag_row.size()); d_tag_row.upload(tag_row.data(), tag_row.size(), stream);
   d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
+  {
+    // f-side slot -> reduced row (camera slots 0..2, then the tag slots)
+    std::vector<int> fslot_row(3 + 6L * nt, -1);
+    for (size_t r = 0; r < row_slot.size(); ++r) {
+      const long sl = row_slot[r];
+      if (sl < 0) continue;
+      if (sl < 3) fslot_row[sl] = (int)r;
+      else if (sl >= 3 + 6L * nc) fslot_row[sl - 6L * nc] = (int)r;
+    }
+    d_fslot_row.alloc(fslot_row.size());
+    d_fslot_row.upload(fslot_row.data(), fslot_row.size(), stream);
+    HIP_CHECK(hipStreamSynchronize(stream));   // (the host vector goes out of scope)
+  }
   int n_dest = 0, n_items = 0, n_splits = 0;
   if (has_f) {
     tp[4] = now_s();
@@ -470,6 +483,8 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nR = nR; P.N = N; P.lda = N; P.cam_row = cam_row;
   P.max_obs_per_cap = std::max(maxk, 1);
   P.swap_roles = elim_used == ARSLAM_ELIM_TAGS ? 1 : 0;
+  P.nf = 3 + 6 * nt;
+  P.fslot_row = d_fslot_row.p;
   P.cap_start = d_cap_start.p; P.obs_tag = d_obs_tag.p; P.obs_lblk = d_obs_lblk.p;
   P.cap_blk_start = d_cap_blk_start.p; P.blk_tag = d_blk_tag.p;
   P.obs_active = d_obs_active.p; P.slot_free = d_slot_free.p;
@@ -697,18 +712,28 @@ void arslam_lm::solve(arslam_lm_summary *s) {
 
     // ---- ComputeTrustRegionStep: LM diagonal, DENSE_SCHUR solve ----
     s->num_linear_solves++;
-    if (!reuse_diag)
-      arslam::launch_lm_diag(P, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal, d_diag.p, stream);
-    reuse_diag = true;
     const bool exec_dag = has_f && opt.factor_executor == 1;
-    if (exec_dag) arslam::launch_exec_reset(plan, d_flag.p, stream);   // flag + executor counters, one launch
-    else HIP_CHECK(hipMemsetAsync(d_flag.p, 0, sizeof(int), stream));
+    if (exec_dag) {
+      // flag + executor counters (+ the LM diagonal when it changed), one launch
+      const arslam::LmDiagArgs ld{reuse_diag ? 0 : n, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal,
+                                  d_diag.p};
+      arslam::launch_exec_reset(plan, d_flag.p, stream, &ld);
+    } else {
+      if (!reuse_diag)
+        arslam::launch_lm_diag(P, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal, d_diag.p, stream);
+      HIP_CHECK(hipMemsetAsync(d_flag.p, 0, sizeof(int), stream));
+    }
+    reuse_diag = true;
     if (has_f) {
       timers[PH_SCHUR].start(stream);
       arslam::launch_zero_tiles(plan, d_S.p, stream);
-      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream);
-      if (nranks > 1) allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ARSLAM_OP_SUM);
-      arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
+      // one rank: the gather writes the final S (D_f^2 and the padding rows
+      // included); several: S is summed over the ranks first
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1);
+      if (nranks > 1) {
+        allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ARSLAM_OP_SUM);
+        arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
+      }
       if (dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull)   // test hook
         arslam::debug_set_reduced_diag(P, d_S.p, P.cam_row >= 0 ? P.cam_row : nR - 1, -1.0, stream);
       timers[PH_SCHUR].stop(stream);
@@ -781,7 +806,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       timers[PH_SOLVE].stop(stream);
     }
     timers[PH_BACK].start(stream);
-    HIP_CHECK(hipMemcpyAsync(xc, x, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
+    // (k_backsub writes every capture slot of xc, k_update_f every other slot)
     arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream, has_f);
     arslam::launch_update_f(P, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
     timers[PH_BACK].stop(stream);
