@@ -338,9 +338,9 @@ __device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *L
 // rest of the trailing update, so the critical chain is the four diag16
 // calls plus one 16-row solve and one 16x16 update per panel.
 // Returns false (uniformly) if a pivot is not positive; inv[c] = 1 / L_cc.
-// idle(w, lane) runs on waves 1-3 while wave 0 factors the first diagonal
-// block (they have no trailing update yet): the persistent executor fetches
-// its fused TRSM's tile there.
+// idle(p, w, lane) runs on waves 1-3 beside wave 0's diagonal block p (after
+// their share of the trailing update): the persistent executor fetches its
+// fused TRSM's tile there.
 template <class Idle>
 __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *bad, int tid, double *colx,
                                      Idle &&idle) {
@@ -354,7 +354,7 @@ __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *b
       if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
       diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane, colx);
     } else if (p == 0) {
-      idle(w, lane);
+      idle(0, w, lane);
     } else {
       // panel p-1's update of blocks (I, C), I >= C >= p, except (p, p)
       const int m = 4 - p, ntl = m * (m + 1) / 2;
@@ -365,6 +365,7 @@ __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *b
         const int bi = 16 * (p + I), bc = 16 * (p + C);
         wave_gemm16_sub(D + bi * LQ + bc, D + bi * LQ + b0 - 16, D + bc * LQ + b0 - 16, 16, lane);
       }
+      idle(p, w, lane);
     }
     __syncthreads();
     STAMP(11 + 4 * p);
@@ -380,7 +381,7 @@ __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *b
 }
 
 __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, int tid, double *colx) {
-  return blocked_potrf64_idle(D, inv, LTd, bad, tid, colx, [](int, int) {});
+  return blocked_potrf64_idle(D, inv, LTd, bad, tid, colx, [](int, int, int) {});
 }
 
 // In-LDS blocked solve X L^T = A for a 64x64 tile X (256 threads), L from
@@ -969,33 +970,62 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // otherwise it is waited for and loaded after L_kk is published.
       const double *pf_src = sub.x >= 0 ? a.S + (long)sub.x * (T64 * T64) : nullptr;
       const int pw0 = sub.y, pw1 = a.wait_off[t + 1];
-      const bool ok = blocked_potrf64_idle(D, inv, LTd, sh + 1, tid, colx, [&](int wv, int ln) {
-        if (wv != 1) return;
-        bool met = false;
-        if (pf_src && pw1 - pw0 <= 64) {
+      // A tile whose waits were not met at panel 0 is polled again by wave 1
+      // beside panels 1 and 2 (the request in sh[6]) and fetched by waves 1-3,
+      // a third each, beside the next panel: on the late elimination-tree chain
+      // the tile's last update lands a few microseconds into the POTRF
+      // (cfg3 k_factor_dag 758 -> 736 us).
+      if (tid == 0) sh[6] = 0;
+      const bool ok = blocked_potrf64_idle(D, inv, LTd, sh + 1, tid, colx, [&](int p, int wv, int ln) {
+        auto poll = [&]() {
+          if (!pf_src || pw1 - pw0 > 64) return false;
           const int q = pw0 + ln;
           const int2 cv = q < pw1 ? a.waits[q] : make_int2(0, 0);
           const int got = q < pw1 ? ld_acquire_relaxed(a.counters + cv.x) : 0;
-          met = __builtin_amdgcn_ballot_w64(q < pw1 && got < cv.y) == 0;
-        }
-        if (met) {
-          int lnl = ln;   // laundered: the 32 prefetch addresses are formed here, not hoisted and spilled
-          asm volatile("" : "+v"(lnl));
+          return __builtin_amdgcn_ballot_w64(q < pw1 && got < cv.y) == 0;
+        };
+        int lnl = ln;   // laundered: the prefetch addresses are formed here, not hoisted and spilled
+        asm volatile("" : "+v"(lnl));
+        if (p == 0) {
+          if (wv != 1) return;
+          const bool met = poll();
+          if (met) {
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
+            for (int g = 0; g < 4; ++g) {
+              const double *p8[8];
+              dbl2 v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * ((g * 8 + u) * 64 + lnl);
+              ld_wt16x8(p8, v);
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int e = (g * 8 + u) * 64 + ln, r = e >> 5, c2 = (e & 31) * 2;
+                *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
+              }
+            }
+          }
+          if (ln == 0) sh[5] = met ? 1 : 0;
+        } else if (sh[5]) {
+          return;
+        } else if (!sh[6]) {   // not requested yet: poll beside panels 1 and 2
+          if (wv == 1 && p < 3 && poll() && ln == 0) sh[6] = p;
+        } else if (sh[6] < p) {   // requested beside an earlier panel: the three thirds
+          // 2048 16-byte elements of the 64x64 tile: wave w takes e in [(w-1)*683, min(w*683, 2048))
+          const int e0 = (wv - 1) * 683, e1 = min(wv * 683, 2048);
+          for (int base = e0; base < e1; base += 8 * 64) {
             const double *p8[8];
             dbl2 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * ((g * 8 + u) * 64 + lnl);
+            for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * min(base + u * 64 + lnl, e1 - 1);
             ld_wt16x8(p8, v);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-              const int e = (g * 8 + u) * 64 + ln, r = e >> 5, c2 = (e & 31) * 2;
-              *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
+              const int e = base + u * 64 + ln, r = e >> 5, c2 = (e & 31) * 2;
+              if (e < e1) *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
             }
           }
+          if (wv == 1 && ln == 0) sh[5] = 1;
         }
-        if (ln == 0) sh[5] = met ? 1 : 0;
       });
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
