@@ -98,3 +98,48 @@ def test_task_graph_is_deadlock_free(L, name):
         info, _ = _plan(L, g, ordering=ordering)
         assert info["n_dag_tasks"] > 0
         assert info["dag_valid"] == 1, info
+
+
+def _brute_force_scalar_flops(g, tag_row, cam_rows=3):
+    """Scalar Cholesky flops of the reduced system's real rows in the solver's order, by a
+    column-by-column symbolic factorization: column j's below-diagonal structure is its own
+    (tags co-visible in some capture, dense 6x6 blocks; the camera rows coupled to every
+    tag) merged with the structures of the earlier columns whose first below-diagonal entry
+    is j (the elimination-tree children).  Per column with c below-diagonal entries:
+    c(c+1) + c + 1 flops (c divisions, c(c+1)/2 multiply-adds of the update, one sqrt)."""
+    used = np.unique(g.obs_tag)
+    order = sorted(used, key=lambda t: tag_row[t])                 # tags in reduced-row order
+    pos = {t: i for i, t in enumerate(order)}
+    n = 6 * len(order) + cam_rows
+    struct = [set() for _ in range(n)]
+    for c in range(g.n_cap):
+        ts = sorted(pos[t] for t in g.obs_tag[g.obs_cap == c])
+        for a in ts:
+            for b in ts:
+                if b > a:
+                    for i in range(6):
+                        struct[6 * a + i].update(range(6 * b, 6 * b + 6))
+    for a in range(len(order)):                                    # inside a tag block, and to the camera
+        for i in range(6):
+            struct[6 * a + i].update(range(6 * a + i + 1, 6 * a + 6))
+            struct[6 * a + i].update(range(6 * len(order), n))
+    for k in range(6 * len(order), n):
+        struct[k].update(range(k + 1, n))
+    flops = 0.0
+    for j in range(n):
+        s = struct[j]
+        c = len(s)
+        flops += c * (c + 1) + c + 1
+        if s:
+            p = min(s)
+            struct[p].update(x for x in s if x > p)
+    return flops
+
+
+@pytest.mark.parametrize("name", ["tiny", "small", "medium"])
+def test_scalar_flops_match_symbolic_factorization(L, name):
+    """summary.factor_scalar_flops (the roofline's algorithmic count) equals a brute-force
+    symbolic Cholesky of the real rows in the same elimination order."""
+    g = synth.config_graph(name)
+    info, tag_row = _plan(L, g)
+    assert info["scalar_flops"] == pytest.approx(_brute_force_scalar_flops(g, tag_row), rel=1e-12)
