@@ -179,20 +179,6 @@ __device__ void inv6(const double *U, double *Ui) {
   }
 }
 
-// Sum of rows[r][i]*rows[r][j] (i, j row columns) over the rows of local block u
-// (u = 0: every row).
-__device__ __forceinline__ double block_dot(const double *rows, const int *lblk, int k, int u,
-                                            int i, int j) {
-  double s = 0.0;
-  for (int q = 0; q < k; ++q) {
-    if (u != 0 && lblk[q] != u) continue;
-    const double *rq = rows + (long)q * 8 * kRowStride;
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + i] * rq[rr * kRowStride + j];
-  }
-  return s;
-}
-
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
@@ -307,7 +293,8 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
 }
 
 // Schur elimination of capture c (ComputeTrustRegionStep's DENSE_SCHUR
-// eliminate step, one capture = one e-block): the packed local reduced system
+// eliminate step, one capture = one e-block; the normal-equation blocks from
+// per-observation Gram matrices on MFMA): the packed local reduced system
 //   [F'F - W' U^-1 W | F'r - W' U^-1 E'r],  U = E'E + D_c^2, W = E'F,
 // over the local f-side columns (f, then 6 per distinct tag of the capture),
 // stored for k_schur_gather.  One wave per capture.
@@ -335,71 +322,56 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   load_rows(P, scale, c, o0, nrows, rows);
   __syncthreads();
   SCHUR_STAMP(0);
-  // U = E'E, E'r, the f column of W (E'F_0), F_0'r and F_0'F_0: one row per
-  // lane, xor-butterfly sums (every lane gets the same bits)
+  // Every product below is an entry of an observation's Gram matrix over its
+  // 8 rows and 14 columns [f | E (capture) | F (tag) | r]: G_q = R_q' R_q, two
+  // v_mfma_f64_16x16x4_f64 per observation (columns padded to 16; lane
+  // (lk, li) supplies row 4s + lk, column li as both operands; the result is
+  // G_q[lk + 4 reg][li]).  The capture-wide sums (U = E'E, E'r, E'f, f'r, f'f)
+  // add the observations' Grams in observation order; the per-tag-block
+  // products (W_u = E'F_u, F_u'r, F_u'F_u, f'F_u) are added into LDS per
+  // observation (a tag seen twice in one capture sums into one block).
   {
-    double prod[35];
+    const int li = lane & 15, lk = lane >> 4;
+    for (int e = lane; e < 6 * m + m + (m & 1) + 28 * nblk; e += kWave) W[e] = 0.0;   // W, Ftr, FF: contiguous
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    typedef double dbl4v __attribute__((ext_vector_type(4)));
+    dbl4v tot = {0, 0, 0, 0};
+    for (int q = 0; q < k; ++q) {
+      dbl4v g = {0, 0, 0, 0};
 #pragma unroll
-    for (int e = 0; e < 35; ++e) prod[e] = 0.0;
-    for (int r = lane; r < nrows; r += kWave) {
-      const double *rr = rows + (long)r * kRowStride;
-      int e = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = i; j < 6; ++j) prod[e++] += rr[1 + i] * rr[1 + j];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) prod[21 + i] += rr[1 + i] * rr[13];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) prod[27 + i] += rr[1 + i] * rr[0];
-      prod[33] += rr[0] * rr[13];
-      prod[34] += rr[0] * rr[0];
-    }
-#pragma unroll
-    for (int e = 0; e < 35; ++e) prod[e] = wave_sum(prod[e]);
-    if (lane == 0) {
-      int e = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = i; j < 6; ++j) {
-          U[6 * i + j] = prod[e];
-          U[6 * j + i] = prod[e];
-          ++e;
-        }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        Etr[i] = prod[21 + i];
-        W[i * m] = prod[27 + i];
+      for (int st = 0; st < 2; ++st) {
+        const double v = li < kRowStride ? rows[(long)(8 * q + 4 * st + lk) * kRowStride + li] : 0.0;
+        g = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, g, 0, 0, 0);
       }
-      Ftr[0] = prod[33];
-      *ff00 = prod[34];
+      tot += g;
+      const int u = lblk[q] - 1;   // the observation's tag block
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int r = lk + 4 * reg, c = li;   // this lane's entry G[r][c]
+        const double v = g[reg];
+        if (r >= 1 && r <= 6 && c >= 7 && c <= 12) W[(r - 1) * m + 1 + 6 * u + (c - 7)] += v;        // E'F_u
+        else if (r >= 7 && r <= 12 && c == 13) Ftr[1 + 6 * u + (r - 7)] += v;                       // F_u'r
+        else if (r >= 7 && r <= 12 && c >= r && c <= 12) {                                           // F_u'F_u
+          const int a = r - 7, b = c - 7;
+          FF[28 * u + a * 6 - a * (a - 1) / 2 + (b - a)] += v;
+        } else if (r == 0 && c >= 7 && c <= 12) FF[28 * u + 21 + (c - 7)] += v;                     // f'F_u
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-  }
-  // per tag block u (its observations' rows): W_u = E'F_u (36), F_u'r (6),
-  // F_u'F_u (21), F_0'F_u (6) -- 69 row dots per block
-  for (int e = lane; e < 69 * nblk; e += kWave) {
-    const int u = e / 69, t = e % 69;
-    int ci, cj;
-    if (t < 36) {
-      ci = 1 + t / 6;
-      cj = 7 + t % 6;
-    } else if (t < 42) {
-      ci = 7 + (t - 36);
-      cj = 13;
-    } else if (t < 63) {
-      int a, b;
-      upper6(t - 42, a, b);
-      ci = 7 + a;
-      cj = 7 + b;
-    } else {
-      ci = 0;
-      cj = 7 + (t - 63);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int r = lk + 4 * reg, c = li;
+      const double v = tot[reg];
+      if (r >= 1 && r <= 6 && c >= 1 && c <= 6) U[6 * (r - 1) + (c - 1)] = v;   // E'E
+      else if (r >= 1 && r <= 6 && c == 13) Etr[r - 1] = v;                     // E'r
+      else if (r >= 1 && r <= 6 && c == 0) W[(r - 1) * m] = v;                  // E'f
+      else if (r == 0 && c == 13) Ftr[0] = v;                                   // f'r
+      else if (r == 0 && c == 0) *ff00 = v;                                     // f'f
     }
-    const double s = block_dot(rows, lblk, k, u + 1, ci, cj);
-    if (t < 36) W[(t / 6) * m + 1 + 6 * u + t % 6] = s;
-    else if (t < 42) Ftr[1 + 6 * u + (t - 36)] = s;
-    else FF[28 * u + (t - 42)] = s;
   }
   __syncthreads();
   SCHUR_STAMP(1);
