@@ -875,13 +875,19 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
   double *colx = LTd + 4 * 16 * LI + 4;   // POTRF pivot scratch (X stays free for the prefetch)
   int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.counters + 2 * a.n_tiles;
+  // claimed continuation targets in flight.  A target is claimed once its
+  // EARLY waits are all drawn; its late waits may name undrawn tickets, so at
+  // most half the grid may hold claimed targets: the other workgroups can
+  // always draw the lowest unfinished ticket, whose producers are all done.
+  int *inflight = ticket + 1;
+  const int cont_cap = (int)(gridDim.x / 2);
   // Continuation targets stay ordinary tickets with a claim flag.  The
   // predecessor's workgroup claims its target (before publishing the tile the
   // target waits for, so it wins whenever it claims) if every task the target
   // waits on has been drawn -- then the target only waits on running tasks --
   // and runs it at once, the folded tile still in LDS.  Otherwise the
   // workgroup that drew the target claims and runs it once its waits are met.
-  int next = -1;
+  int next = -1, prev_k = -1;
   for (;;) {
     // thread coordinates re-derived per task from a laundered threadIdx: the
     // per-lane LDS/tile addresses of every task type are then computed where
@@ -899,7 +905,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       __syncthreads();
     }
     const int t = next;
+    const int pk = prev_k;   // a claimed continuation: the predecessor's column (its L_{k,pk} is in X)
     next = -1;
+    prev_k = -1;
     DAG_PROGRESS(0, t);
     DAG_PROGRESS(1, 1);
     if (t >= a.n_tasks) break;
@@ -942,12 +950,14 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
             for (int reg = 0; reg < 4; ++reg) akk[4 * q + reg] = ld_wt(Akk + (rb + lk + 4 * reg) * T64 + cb + li);
           }
         }
-        if (cont) {
-          // continuation: the fold's one column L_kj is the tile the previous
-          // task just solved, still in X
-          gemm64_nt(X, X, tid, acc);
-        }
-        for (int q = cont ? it.z : it.y; q < it.z; ++q) {
+        // (the same products in the same order whether the task was drawn
+        // or claimed: a claimed continuation takes the term of its
+        // predecessor's column from the tile that task just solved, still in X)
+        for (int q = it.y; q < it.z; ++q) {
+          if (cont && a.ks[q] == pk) {
+            gemm64_nt(X, X, tid, acc);
+            continue;
+          }
           if (q > it.y) __syncthreads();
           load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, a.ks[q]), D, tid);
           __syncthreads();
@@ -1060,13 +1070,18 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         if (tid == 0) {
           // claim the continuation target first: its drawer waits for this
           // tile, so it cannot have claimed it yet
-          sh[4] = (c >= 0 && ld_acquire_relaxed(ticket) > a.maxdep[c] && atomicCAS(a.claimed + c, 0, 1) == 0) ? c
-                                                                                                            : -1;
+          int claim = -1;
+          if (c >= 0 && ld_acquire_relaxed(ticket) > a.maxdep[c]) {
+            if (atomicAdd(inflight, 1) < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0) claim = c;
+            else atomicSub(inflight, 1);
+          }
+          sh[4] = claim;
           __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
         __syncthreads();
         next = sh[4];
+        if (next >= 0) prev_k = k;
       }
     } else if (task.x == 3) {
       // ---- INV k: L_kk^{-1} for the backward solve (off the critical chain) ----
@@ -1215,6 +1230,25 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       }
     }
     DAG_PROGRESS(1, 4);
+    if (cont && tid == 0) atomicSub(inflight, 1);   // this claimed target is done
+    if (task.x != 0 || sub.x < 0) {
+      // the task's designated successor (llt_plan.cpp dag_build), claimed
+      // when every other producer it names has been drawn (the fused POTRF
+      // above claims its parent's POTRF itself)
+      const int c = a.cont[t];
+      if (c >= 0) {
+        if (tid == 0) {
+          int claim = -1;
+          if (ld_acquire_relaxed(ticket) > a.maxdep[c]) {
+            if (atomicAdd(inflight, 1) < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0) claim = c;
+            else atomicSub(inflight, 1);
+          }
+          sh[4] = claim;
+        }
+        __syncthreads();
+        next = sh[4];
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     if (a.trace && tid == 0) a.trace[8L * t + 2] = realtime();
   }

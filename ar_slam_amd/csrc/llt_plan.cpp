@@ -58,7 +58,13 @@ constexpr int kSplitMin = 6;   // k-lists longer than this are split
 // on the elimination tree's critical chain are drawn as soon as their inputs
 // can be ready instead of behind a wave of updates that can wait.  Costs are
 // calibrated on MI355X task traces (tools/dag_critical.py), in microseconds.
-constexpr int kSimWorkers = 512;
+// Simulated with fewer workgroups than the executor's 512: the real tasks run
+// slower than their calibrated costs while ~300 updates contend for the
+// memory system, so a 512-wide simulation hands out tickets ahead of
+// readiness, workgroups block on them, and chain tasks are drawn late.  A
+// narrower simulation orders the chain earlier (cfg3 k_factor_dag 735 -> 716
+// us at 192-256; 160 is worse, 810 us; tools/env_bench.sh).
+constexpr int kSimWorkers = 224;
 // A POTRF node may also carry the TRSM of the column's first off-diagonal
 // tile (sub = its compact tile id): 'late' waits are those of that TRSM,
 // polled after L_kk is published.
@@ -72,7 +78,9 @@ struct DagNode {
   std::vector<int2> late;
 };
 
-static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, long nt, const LltPlan &plan) {
+static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, long nt, const LltPlan &plan,
+                                          std::vector<double> *finish_out = nullptr,
+                                          std::vector<double> *blevel_out = nullptr) {
   const int n = (int)nodes.size();
   std::vector<int> ready_prod(nt, -1);
   std::vector<std::vector<std::pair<int, int>>> by_tile(nt);   // (seq, node) of update items
@@ -163,13 +171,16 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   order.reserve(n);
   int busy = 0;
   double now = 0.0;
+  const char *sw = std::getenv("ARSLAM_SIM_WORKERS");   // (debug: list-schedule width)
+  const int sim_workers = sw ? std::max(1, std::atoi(sw)) : kSimWorkers;
   while ((int)order.size() < n || !events.empty()) {
-    while (busy < kSimWorkers && !heap.empty()) {
+    while (busy < sim_workers && !heap.empty()) {
       std::pop_heap(heap.begin(), heap.end(), cmp);
       const int v = heap.back();
       heap.pop_back();
       order.push_back(v);
       events.push_back({now + cost[v], v});
+      if (finish_out) (*finish_out)[v] = now + cost[v];
       std::push_heap(events.begin(), events.end(), ev_cmp);
       ++busy;
     }
@@ -186,6 +197,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
       }
   }
   if ((int)order.size() != n) throw std::runtime_error("dag_list_schedule: not every task was scheduled");
+  if (blevel_out) *blevel_out = blevel;
   return order;
 }
 
@@ -347,7 +359,8 @@ void dag_build(LltPlan &plan) {
     n.waits.push_back(make_int2(tid(k, k), 1));
     nodes.push_back(std::move(n));
   }
-  std::vector<int> order = dag_list_schedule(nodes, nt, plan);
+  std::vector<double> sim_finish(nodes.size(), 0.0), sim_blevel;
+  std::vector<int> order = dag_list_schedule(nodes, nt, plan, &sim_finish, &sim_blevel);
   plan.h_dag_tasks.clear();
   plan.h_dag_waits.clear();
   plan.h_dag_sub.clear();
@@ -360,9 +373,20 @@ void dag_build(LltPlan &plan) {
     plan.h_dag_wait_off.push_back((int)plan.h_dag_waits.size());
   }
   plan.n_dag_tasks = (long)plan.h_dag_tasks.size();
-  // continuation pairs: POTRF(k) with fused TRSM (par, k) -> POTRF(par) when
-  // POTRF(par)'s folded item is that one tile; maxdep = the largest ticket
-  // the target waits on (a producer of any of its counters)
+  // Continuations: a finished task may claim one designated successor and run
+  // it at once on the same workgroup instead of leaving it to be drawn.  The
+  // 512 workgroups hold drawn tasks that wait (the factorization keeps ~30 %
+  // of them busy), so in the contended first half of the factorization a
+  // ready chain task used to be drawn 10-25 us after its last producer ended.
+  //  * POTRF(k) with fused TRSM (par, k) -> POTRF(par) (the solved tile stays
+  //    in LDS; the fold reuses it for column k's term);
+  //  * otherwise a task's designated successor is the earliest-ticketed task
+  //    whose latest-ticketed early producer it is.
+  // maxdep[c] = the largest ticket among c's early producers other than its
+  // claimers (>= 0 marks a target): a claim needs those drawn.  Late waits (a
+  // POTRF's fused TRSM) are not counted, so a claimed target may wait on
+  // undrawn tickets; the kernel bounds claimed targets in flight to half the
+  // grid, so workgroups stay free to draw (k_factor_dag, dag_simulate).
   {
     const long n = plan.n_dag_tasks;
     plan.h_dag_cont.assign(n, -1);
@@ -376,31 +400,66 @@ void dag_build(LltPlan &plan) {
       if (plan.h_dag_sub[t].x >= 0) ready_tk[plan.h_dag_sub[t].x] = (int)t;
       if (tk.x == 2) apply_tk[tk.w].push_back({tk.z, (int)t});
     }
+    // early producers of every task (the in-order application's predecessor
+    // level included for update items)
+    std::vector<std::vector<int>> prod(n);
     for (long t = 0; t < n; ++t) {
       const int4 tk = plan.h_dag_tasks[t];
+      const int early_end = plan.h_dag_sub[t].x >= 0 ? plan.h_dag_sub[t].y : plan.h_dag_wait_off[t + 1];
+      std::vector<int> &pr = prod[t];
+      for (int q = plan.h_dag_wait_off[t]; q < early_end; ++q) {
+        const int2 w = plan.h_dag_waits[q];
+        if (w.x < nt) {
+          if (ready_tk[w.x] >= 0) pr.push_back(ready_tk[w.x]);
+        } else {
+          for (const auto &sv : apply_tk[w.x - nt])
+            if (sv.first < w.y) pr.push_back(sv.second);
+        }
+      }
+      if (tk.x == 2 && tk.z > 0)
+        for (const auto &sv : apply_tk[tk.w])
+          if (sv.first == tk.z - 1) pr.push_back(sv.second);
+      std::sort(pr.begin(), pr.end());
+      pr.erase(std::unique(pr.begin(), pr.end()), pr.end());
+    }
+    const bool no_cont = std::getenv("ARSLAM_NO_CONT") != nullptr;   // (debug switches)
+    // (measured: the generic successor claims cost ~10 us on cfg3 -- the
+    // claimed successors are often not the ones the chain waits for, and the
+    // claiming workgroup idles on their other producers -- so they are off
+    // unless ARSLAM_GCONT is set)
+    const bool no_gcont = std::getenv("ARSLAM_GCONT") == nullptr;
+    for (long t = 0; t < n && !no_cont; ++t) {
+      const int4 tk = plan.h_dag_tasks[t];
       const int sb = plan.h_dag_sub[t].x;
-      if (tk.x != 0 || sb < 0 || std::getenv("ARSLAM_NO_CONT")) continue;
+      if (tk.x != 0 || sb < 0) continue;
       int par = -1;
       for (int i = tk.y + 1; i < T && par < 0; ++i)
         if (tid(i, tk.y) == sb) par = i;
-      if (par < 0 || potrf_of[par] < 0) continue;
-      const int c = potrf_of[par];
-      const int4 ct = plan.h_dag_tasks[c];
-      if (ct.z < 0) continue;
-      const int4 it = plan.h_items[ct.z];
-      if (it.z - it.y != 1 || plan.h_ks[it.y] != tk.y) continue;
-      int md = -1;
-      for (int q = plan.h_dag_wait_off[c]; q < plan.h_dag_wait_off[c + 1]; ++q) {
-        const int2 w = plan.h_dag_waits[q];
-        if (w.x < nt) {
-          md = std::max(md, ready_tk[w.x]);
-        } else {
-          for (const auto &sv : apply_tk[w.x - nt])
-            if (sv.first < w.y) md = std::max(md, sv.second);
-        }
-      }
-      if (md < 0 || md >= c) continue;   // (topological order: cannot happen)
-      plan.h_dag_cont[t] = c;
+      if (par < 0 || potrf_of[par] < 0 || potrf_of[par] <= t) continue;
+      plan.h_dag_cont[t] = potrf_of[par];
+    }
+    // every other task names as successor the task of the largest bottom
+    // level among those whose last producer (by the list schedule's finish
+    // estimate) it is
+    std::vector<int> best(n, -1);
+    for (long v = 0; v < n && !no_cont && !no_gcont; ++v) {
+      if (plan.h_dag_tasks[v].x == 3 || prod[v].empty()) continue;
+      int u = prod[v][0];
+      for (int p : prod[v])
+        if (sim_finish[order[p]] > sim_finish[order[u]]) u = p;
+      if (u >= v || plan.h_dag_cont[u] >= 0) continue;
+      if (best[u] < 0 || sim_blevel[order[v]] > sim_blevel[order[best[u]]]) best[u] = (int)v;
+    }
+    for (long u = 0; u < n; ++u)
+      if (best[u] >= 0) plan.h_dag_cont[u] = best[u];
+    std::vector<std::vector<int>> claimers(n);
+    for (long t = 0; t < n; ++t)
+      if (plan.h_dag_cont[t] >= 0) claimers[plan.h_dag_cont[t]].push_back((int)t);
+    for (long c = 0; c < n; ++c) {
+      if (claimers[c].empty()) continue;
+      int md = 0;
+      for (int u : prod[c])
+        if (std::find(claimers[c].begin(), claimers[c].end(), u) == claimers[c].end()) md = std::max(md, u);
       plan.h_dag_maxdep[c] = md;
     }
   }
@@ -588,16 +647,19 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
   struct W { long t = -1; int phase = 0; long next = -1; bool cont = false; };
   std::vector<W> ws(n_workers);
   long ticket = 0, finished = 0;
+  int inflight = 0;   // claimed continuations running: at most n_workers / 2 (as k_factor_dag)
   unsigned rng = seed ? seed : 1u;
   auto rnd = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
   auto done = [&](W &w) {
     ++finished;
     const int c = has_cont ? plan.h_dag_cont[w.t] : -1;
     w.next = -1;
-    if (c >= 0 && ticket > maxdep(c) && !claimed[c]) {
+    if (c >= 0 && ticket > maxdep(c) && !claimed[c] && inflight < n_workers / 2) {
       claimed[c] = 1;
       w.next = c;
+      ++inflight;
     }
+    if (w.cont) --inflight;
     w.phase = 0;
   };
   while (finished < n) {
