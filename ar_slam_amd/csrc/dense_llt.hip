@@ -838,6 +838,8 @@ struct DagArgs {
   const int *cont;            // [n_tasks] POTRF task the same workgroup may continue with (or -1)
   const int *maxdep;          // [n_tasks] continuation targets: largest ticket they wait on; else -1
   int *claimed;               // [n_tasks] continuation targets: claimed by the predecessor or the drawer
+  const int2 *cand;           // [n_tasks] ready-claim candidates (LltPlan::dag_cand)
+  const int *fold;            // [n_tasks] TRSM tasks: update item folded in first, or -1
   const int *wait_off;
   const int2 *waits;
   int *counters;              // ready[n_tiles] | applied[n_tiles] | ticket
@@ -916,8 +918,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     if (a.trace && tid == 0) { a.trace[8L * t] = realtime(); a.trace[8L * t + 3] = blockIdx.x; }
     const int2 sub = a.sub[t];
     if (w == 0) {
-      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], sub.x >= 0 ? sub.y : a.wait_off[t + 1], a.flag,
-                               lane, task.x != 2);
+      // (sub.y: the end of the early waits; the late ones are a fused TRSM's,
+      // or a folded TRSM's L_kk)
+      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], sub.y, a.flag, lane, task.x != 2);
       if (lane == 0) {
         if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
         // a drawn continuation target: run it only if its predecessor did not claim it
@@ -1116,7 +1119,44 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // ---- TRSM i,k: L_ik L_kk^T = A_ik, blocked with the 16x16 inverses ----
       const int i = task.y, k = task.z;
       double *Ct = tile_ptr(a.S, a.tid_map, a.T, i, k);
-      load_tile_wt(Ct, X, tid);
+      const int fi = a.fold[t];
+      if (fi >= 0) {
+        // the tile's last update item first: A_ik - sum_j L_ij L_kj^T, the
+        // products summed in the item's order and subtracted once, as the
+        // item's own application does (llt_plan.cpp dag_build)
+        const int4 it = a.items[fi];
+        dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        double av[16];   // A_ik (final but for the item) in the accumulator layout, in flight during the GEMMs
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) av[4 * q + reg] = ld_wt(Ct + (rb + lk + 4 * reg) * T64 + cb + li);
+        }
+        for (int q = it.y; q < it.z; ++q) {
+          const int j = a.ks[q];
+          if (q > it.y) __syncthreads();
+          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, i, j), D, tid);
+          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, j), X, tid);
+          __syncthreads();
+          gemm64_nt(D, X, tid, acc);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) X[(rb + lk + 4 * reg) * LQ + cb + li] = av[4 * q + reg] - acc[q][reg];
+        }
+        // the late wait: L_kk
+        if (w == 0) {
+          const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane, true);
+          if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
+        }
+        __syncthreads();
+      } else {
+        load_tile_wt(Ct, X, tid);
+      }
       load_tile_wt(a.Ld + (long)k * T64 * T64, D, tid);
       {
         const double *ltd_g = a.ltd + (long)k * kLtdSize;
@@ -1244,6 +1284,48 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
             else atomicSub(inflight, 1);
           }
           sh[4] = claim;
+        }
+        __syncthreads();
+        next = sh[4];
+      }
+    }
+    // Ready claim: a candidate successor (largest bottom level first) that is
+    // not drawn yet and whose waits all hold right now runs next on this
+    // workgroup, instead of waiting for its ticket behind blocked workgroups.
+    if (next < 0) {
+      const int2 cd = a.cand[t];
+      if (cd.x >= 0) {
+        if (w == 0) {
+          int tk = 0;
+          if (lane == 0) tk = ld_acquire_relaxed(ticket);
+          tk = __builtin_amdgcn_readfirstlane(tk);
+          int claim = -1;
+          for (int ci = 0; ci < 2; ++ci) {
+            const int c = ci ? cd.y : cd.x;
+            if (c < 0) break;
+            if (tk > c) continue;   // drawn: its drawer runs it
+            const int2 sc = a.sub[c];
+            const int w0 = a.wait_off[c], w1 = sc.x >= 0 ? sc.y : a.wait_off[c + 1];   // w1 - w0 <= 63
+            const int4 tc = a.tasks[c];
+            bool open = false;
+            if (w0 + lane < w1) {
+              const int2 cv = a.waits[w0 + lane];
+              open = ld_acquire_relaxed(a.counters + cv.x) < cv.y;
+            }
+            if (lane == 63 && tc.x == 2) open = ld_acquire_relaxed(applied + tc.w) < tc.z;
+            if (__builtin_amdgcn_ballot_w64(open) != 0) continue;
+            int got = -1;
+            if (lane == 0) {
+              if (atomicAdd(inflight, 1) < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0) got = c;
+              else atomicSub(inflight, 1);
+            }
+            got = __builtin_amdgcn_readfirstlane(got);
+            if (got >= 0) {
+              claim = got;
+              break;
+            }
+          }
+          if (lane == 0) sh[4] = claim;
         }
         __syncthreads();
         next = sh[4];
@@ -1521,7 +1603,7 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
     if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
   }
   DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
-            P.dag_maxdep, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
+            P.dag_maxdep, P.dag_claimed, P.dag_cand, P.dag_fold, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
             P.upd_part, P.upd_cnt, flag, progress, trace};
   const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);

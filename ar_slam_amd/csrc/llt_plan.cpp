@@ -76,6 +76,7 @@ struct DagNode {
   std::vector<int2> waits;
   int sub = -1;
   std::vector<int2> late;
+  int fold = -1;   // TRSM: the update item folded into it
 };
 
 static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, long nt, const LltPlan &plan,
@@ -122,7 +123,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
       const int nk = nd.task.z >= 0 ? plan.h_items[nd.task.z].z - plan.h_items[nd.task.z].y : 0;
       cost[v] = 16.0 + 4.0 * nk + (nd.sub >= 0 ? 5.0 : 0.0);
     } else if (nd.task.x == 1) {
-      cost[v] = 6.0;
+      cost[v] = 6.0 + (nd.fold >= 0 ? 4.0 * (plan.h_items[nd.fold].z - plan.h_items[nd.fold].y) : 0.0);
     } else if (nd.task.x == 3) {
       cost[v] = 5.0;
     } else {
@@ -171,6 +172,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   order.reserve(n);
   int busy = 0;
   double now = 0.0;
+  std::vector<double> through(blevel_out ? n : 0);
   const char *sw = std::getenv("ARSLAM_SIM_WORKERS");   // (debug: list-schedule width)
   const int sim_workers = sw ? std::max(1, std::atoi(sw)) : kSimWorkers;
   while ((int)order.size() < n || !events.empty()) {
@@ -181,6 +183,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
       order.push_back(v);
       events.push_back({now + cost[v], v});
       if (finish_out) (*finish_out)[v] = now + cost[v];
+      if (blevel_out) through[v] = now + blevel[v];   // longest path through v, as scheduled
       std::push_heap(events.begin(), events.end(), ev_cmp);
       ++busy;
     }
@@ -197,7 +200,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
       }
   }
   if ((int)order.size() != n) throw std::runtime_error("dag_list_schedule: not every task was scheduled");
-  if (blevel_out) *blevel_out = blevel;
+  if (blevel_out) *blevel_out = through;
   return order;
 }
 
@@ -317,6 +320,54 @@ void dag_build(LltPlan &plan) {
       if (!drop[m]) kept.push_back(std::move(nodes[m]));
     nodes.swap(kept);
   }
+  // Fold the last update of a TRSM's tile into the TRSM task when that update
+  // is one unsplit item, as for the diagonal: the task computes
+  // A_ik - sum_j L_ij L_kj^T itself before the solve (the same products in
+  // the same order as the item, so the result is unchanged bit for bit).  On
+  // a dense separator, row i's tiles form a chain TRSM(i,k-1) -> update of
+  // (i,k) -> TRSM(i,k); folding removes one task, one hand-off and one
+  // round trip of the tile per link.  Not for the parent-row tiles, which
+  // the next pass fuses into their column's POTRF.  Measured on cfg3: 717 ->
+  // 749 us with L_kk among the early waits (the fold's work then lands on the
+  // chain), 726 us with L_kk as a late wait after the fold's GEMMs; the
+  // folded tasks hold workgroups longer than the hand-offs they save.  Off
+  // unless ARSLAM_TRSM_FOLD is set.
+  if (std::getenv("ARSLAM_TRSM_FOLD")) {
+    std::vector<int> last_item(nt, -1), last_count(nt, 0);
+    for (size_t m = 0; m < nodes.size(); ++m) {
+      if (nodes[m].type != 2) continue;
+      const int tt = nodes[m].task.w, seq = nodes[m].task.z;
+      if (seq + 1 != n_apply[tt]) continue;
+      last_item[tt] = (int)m;
+      last_count[tt]++;
+    }
+    std::vector<char> drop(nodes.size(), 0);
+    for (auto &n : nodes) {
+      if (n.type != 1) continue;
+      const int i = n.task.y, k = n.task.z, tt = n.task.w;
+      int par = -1;
+      for (int r = k + 1; r < T && par < 0; ++r)
+        if (tid(r, k) >= 0) par = r;
+      if (i == par) continue;
+      const int m = last_item[tt];
+      if (m < 0 || last_count[tt] != 1 || plan.h_items[nodes[m].task.y].w >= 0) continue;
+      n.fold = nodes[m].task.y;
+      // early waits: the item's operands and the tile's earlier levels (the
+      // fold's GEMMs run while POTRF(k) is still factoring); late: L_kk
+      std::vector<int2> w;
+      for (const int2 &x : n.waits)
+        if (x.x != (int)nt + tt && x.x != tid(k, k)) w.push_back(x);
+      if (n_apply[tt] > 1) w.push_back(make_int2((int)nt + tt, n_apply[tt] - 1));
+      w.insert(w.end(), nodes[m].waits.begin(), nodes[m].waits.end());
+      n.waits = std::move(w);
+      n.late.assign(1, make_int2(tid(k, k), 1));
+      drop[m] = 1;
+    }
+    std::vector<Node> kept;
+    for (size_t m = 0; m < nodes.size(); ++m)
+      if (!drop[m]) kept.push_back(std::move(nodes[m]));
+    nodes.swap(kept);
+  }
   // Fuse the TRSM of each column's first off-diagonal tile (the elimination
   // tree parent's row) into the column's POTRF task: on a chain of
   // separator columns, POTRF(k) -> TRSM(parent, k) -> POTRF(parent) is the
@@ -359,14 +410,16 @@ void dag_build(LltPlan &plan) {
     n.waits.push_back(make_int2(tid(k, k), 1));
     nodes.push_back(std::move(n));
   }
-  std::vector<double> sim_finish(nodes.size(), 0.0), sim_blevel;
+  std::vector<double> sim_finish(nodes.size(), 0.0), sim_blevel;   // (sim_blevel: start + bottom level)
   std::vector<int> order = dag_list_schedule(nodes, nt, plan, &sim_finish, &sim_blevel);
   plan.h_dag_tasks.clear();
   plan.h_dag_waits.clear();
   plan.h_dag_sub.clear();
+  plan.h_dag_fold.clear();
   plan.h_dag_wait_off.assign(1, 0);
   for (int o : order) {
     plan.h_dag_tasks.push_back(nodes[o].task);
+    plan.h_dag_fold.push_back(nodes[o].fold);
     plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].waits.begin(), nodes[o].waits.end());
     plan.h_dag_sub.push_back(make_int2(nodes[o].sub, (int)plan.h_dag_waits.size()));
     plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].late.begin(), nodes[o].late.end());
@@ -461,6 +514,42 @@ void dag_build(LltPlan &plan) {
       for (int u : prod[c])
         if (std::find(claimers[c].begin(), claimers[c].end(), u) == claimers[c].end()) md = std::max(md, u);
       plan.h_dag_maxdep[c] = md;
+    }
+    // Ready-claim candidates: each task's two successors of the largest
+    // bottom level.  The workgroup ending the task claims one that is not
+    // drawn yet when all of its waits are met right then (polled), so a chain
+    // task whose last input just landed runs at once instead of waiting for
+    // its ticket to come up (k_factor_dag).  Every candidate is a claim target
+    // (maxdep >= 0), so its drawer runs it only if nobody claimed it.
+    plan.h_dag_cand.assign(n, make_int2(-1, -1));
+    if (!no_cont && std::getenv("ARSLAM_RCLAIM")) {
+      // only successors on a near-critical path of the list schedule: polling
+      // at the end of every task cost more workgroup time than it saved
+      double span = 0.0;
+      for (double f : sim_finish) span = std::max(span, f);
+      const double crit = span * (std::getenv("ARSLAM_RCLAIM_FRAC") ? std::atof(std::getenv("ARSLAM_RCLAIM_FRAC")) : 0.9);
+      std::vector<std::vector<int>> succ(n);
+      for (long v = 0; v < n; ++v)
+        if (plan.h_dag_tasks[v].x != 3)
+          for (int u : prod[v])
+            if (u < v) succ[u].push_back((int)v);
+      for (long u = 0; u < n; ++u) {
+        std::vector<int> &sv = succ[u];
+        std::stable_sort(sv.begin(), sv.end(),
+                         [&](int a, int b) { return sim_blevel[order[a]] > sim_blevel[order[b]]; });
+        int2 c = make_int2(-1, -1);
+        for (int v : sv) {
+          if (v == plan.h_dag_cont[u]) continue;   // claimed by the POTRF rule already
+          if (sim_blevel[order[v]] < crit) continue;
+          const int early_end = plan.h_dag_sub[v].x >= 0 ? plan.h_dag_sub[v].y : plan.h_dag_wait_off[v + 1];
+          if (early_end - plan.h_dag_wait_off[v] > 63) continue;   // polled by one wavefront
+          if (c.x < 0) c.x = v;
+          else if (c.y < 0) c.y = v;
+        }
+        plan.h_dag_cand[u] = c;
+        if (c.x >= 0) plan.h_dag_maxdep[c.x] = std::max(plan.h_dag_maxdep[c.x], 0);
+        if (c.y >= 0) plan.h_dag_maxdep[c.y] = std::max(plan.h_dag_maxdep[c.y], 0);
+      }
     }
   }
   long n_potrf = 0, n_trsm = 0;
@@ -659,6 +748,20 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
       w.next = c;
       ++inflight;
     }
+    if (w.next < 0 && !plan.h_dag_cand.empty()) {
+      for (int v : {plan.h_dag_cand[w.t].x, plan.h_dag_cand[w.t].y}) {
+        if (v < 0 || w.next >= 0 || ticket > v || claimed[v] || inflight >= n_workers / 2) continue;
+        const int ee = plan.h_dag_sub[v].x >= 0 ? plan.h_dag_sub[v].y : plan.h_dag_wait_off[v + 1];
+        bool met = true;
+        for (int q = plan.h_dag_wait_off[v]; q < ee && met; ++q) met = cnt[plan.h_dag_waits[q].x] >= plan.h_dag_waits[q].y;
+        const int4 tv = plan.h_dag_tasks[v];
+        if (tv.x == 2 && cnt[nt + tv.w] < tv.z) met = false;
+        if (!met) continue;
+        claimed[v] = 1;
+        w.next = v;
+        ++inflight;
+      }
+    }
     if (w.cont) --inflight;
     w.phase = 0;
   };
@@ -741,6 +844,8 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   plan.dag_sub = upload(plan.h_dag_sub, s);
   plan.dag_cont = upload(plan.h_dag_cont, s);
   plan.dag_maxdep = upload(plan.h_dag_maxdep, s);
+  plan.dag_cand = upload(plan.h_dag_cand, s);
+  plan.dag_fold = upload(plan.h_dag_fold, s);
   check(hipMalloc(&plan.dag_claimed, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int)), "hipMalloc(dag_claimed)");
   check(hipMalloc(&plan.dag_counters, (2 * (size_t)plan.n_tiles + 2) * sizeof(int)), "hipMalloc(dag_counters)");
   check(hipStreamSynchronize(s), "plan sync");
@@ -758,7 +863,7 @@ void llt_plan_free(LltPlan &plan) {
                   (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.bs_counters, (void *)plan.tile_id, (void *)plan.ldiag,
                   (void *)plan.dag_tasks, (void *)plan.dag_wait_off, (void *)plan.dag_waits,
                   (void *)plan.dag_sub, (void *)plan.dag_cont, (void *)plan.dag_maxdep, (void *)plan.dag_claimed,
-                  (void *)plan.dag_counters})
+                  (void *)plan.dag_counters, (void *)plan.dag_cand, (void *)plan.dag_fold})
     if (p) (void)hipFree(p);
   plan = LltPlan{};
 }

@@ -56,7 +56,7 @@ std::string executor_fault_message(int code, int rank, int iteration) {
   const int c = -code;
   if (code == 0) what = "on another rank";
   else if (c >= 4000000) what = "backward-solve column " + std::to_string(c - 4000000) + ": dependency wait timed out";
-  else if (c >= 3000000) what = "ticket " + std::to_string(c - 3000000) + ": fused TRSM late wait timed out";
+  else if (c >= 3000000) what = "ticket " + std::to_string(c - 3000000) + ": late wait (fused TRSM / folded TRSM's L_kk) timed out";
   else if (c >= 2000000) what = "ticket " + std::to_string(c - 2000000) + ": in-order update wait timed out";
   else if (c >= 1000000) what = "ticket " + std::to_string(c - 1000000) + ": dependency wait timed out";
   else what = "code " + std::to_string(code);
