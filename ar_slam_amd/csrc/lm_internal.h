@@ -184,13 +184,15 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
                     double dmax, double *diag, hipStream_t s);
 // (prep = true: k_prep_reduced's diagonal work is done by the gather itself --
 // single rank only, where the gathered S is final)
+// (zero_tiles: the first zero_tiles 64x64 tiles of S are cleared by extra
+// k_schur blocks before the gather writes S)
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                  double radius, double *S, hipStream_t s, bool prep = false);
+                  double radius, double *S, hipStream_t s, bool prep = false, long zero_tiles = 0);
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
                          hipStream_t s);
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
                     double radius, const double *yF, double *xc, double *parts, hipStream_t s,
-                    bool reuse_ui = false);
+                    bool reuse_ui = false, bool with_cost = false);
 // candidate f-side slots: xc = x - s yF on reduced rows, xc = x elsewhere (every
 // f-side slot is written); fparts: 2 per 256 reduced rows
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,

@@ -299,10 +299,22 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
 // over the local f-side columns (f, then 6 per distinct tag of the capture),
 // stored for k_schur_gather.  One wave per capture.
 __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ scale,
-                                                 const double *__restrict__ diag, double radius) {
+                                                 const double *__restrict__ diag, double radius,
+                                                 double *__restrict__ zero_tiles) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   SCHUR_STAMP_INIT;
   const int c = blockIdx.x, lane = threadIdx.x;
+  if (c >= P.nc) {
+    // the blocks past the captures clear one 64x64 tile of S each (the gather
+    // writes only the assembled blocks; the rest of S must be zero): the
+    // stores overlap the latency-bound capture waves instead of a memset
+    // launch of their own
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2 *z = reinterpret_cast<d2 *>(zero_tiles + (long)(c - P.nc) * 4096);
+#pragma unroll 8
+    for (int e = lane; e < 2048; e += kWave) z[e] = d2{0.0, 0.0};
+    return;
+  }
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
   if (k == 0) return;
   const int nrows = 8 * k;
@@ -663,6 +675,62 @@ __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, do
   }
 }
 
+// Cost at x (candidate evaluation) of capture c: active / fixed cost,
+// finiteness.  cap: the capture's 6 parameters (x's slot, or the candidate
+// k_backsub just formed, held in LDS); camera and tags from x.
+__device__ __forceinline__ void capture_cost(const DevProblem &P, const double *__restrict__ x, const double *cap,
+                                             int c, double *__restrict__ parts) {
+  __shared__ double sq[kWave];
+  __shared__ double ocost[kMaxTagsPerCapture];
+  const int lane = threadIdx.x;
+  const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
+  const int nrows = 8 * k;
+  const double *cam = x;
+  const AngleAxis ac = aa_prepare(cap + 3);
+  double bad = 0.0;
+  for (int base = 0; base < nrows; base += kWave) {
+    const int row = base + lane;
+    double r2 = 0.0;
+    if (row < nrows) {
+      const int q = row >> 3, corner = (row >> 1) & 3, comp = row & 1;
+      const int obs = o0 + q;
+      const double *tag = x + slot_tag(P, P.obs_tag[obs]);
+      const AngleAxis at = aa_prepare(tag + 3);
+      const double obsv = P.corners[8L * obs + 2 * corner + comp];
+      const bool sw = P.swap_roles != 0;   // tag elimination: the capture is the f-block
+      const double r = residual_row(sw ? at : ac, sw ? tag : cap, sw ? ac : at, sw ? cap : tag, cam[0], corner,
+                                    comp, obsv, nullptr, nullptr);
+      if (!isfinite(r)) bad = 1.0;
+      r2 = r * r;
+    }
+    sq[lane] = r2;
+    __syncthreads();
+    if (lane < 8 && base / 8 + lane < k) {
+      double s = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) s += sq[8 * lane + rr];
+      ocost[base / 8 + lane] = 0.5 * s;
+    }
+    __syncthreads();
+  }
+  bad = wave_max(bad);
+  if (lane == 0) {
+    double act = 0.0, fix = 0.0;
+    for (int q = 0; q < k; ++q) {
+      if (P.obs_active[o0 + q]) act += ocost[q]; else fix += ocost[q];
+    }
+    parts[(long)P_COST * P.nc + c] = act;
+    parts[(long)P_FIXED * P.nc + c] = fix;
+    parts[(long)P_CBAD * P.nc + c] = bad;
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_cost(DevProblem P, const double *__restrict__ x,
+                                                double *__restrict__ parts) {
+  const int c = blockIdx.x;
+  capture_cost(P, x, x + slot_cap(P, c), c, parts);
+}
+
 // Back substitution for capture c, candidate update of its slots and its
 // share of the model cost change.
 __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *__restrict__ x,
@@ -670,7 +738,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
                                                    const double *__restrict__ diag, double radius,
                                                    const double *__restrict__ yF,
                                                    double *__restrict__ xc,
-                                                   double *__restrict__ parts, int reuse_ui) {
+                                                   double *__restrict__ parts, int reuse_ui, int with_cost) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int c = blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
@@ -681,6 +749,11 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
       parts[(long)P_MODEL * P.nc + c] = 0.0;
       parts[(long)P_STEP2 * P.nc + c] = 0.0;
       parts[(long)P_YBAD * P.nc + c] = 0.0;
+      if (with_cost) {
+        parts[(long)P_COST * P.nc + c] = 0.0;
+        parts[(long)P_FIXED * P.nc + c] = 0.0;
+        parts[(long)P_CBAD * P.nc + c] = 0.0;
+      }
     }
     return;
   }
@@ -768,12 +841,14 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   }
   mpart = wave_sum(mpart);
   double st = 0.0, bad = 0.0;
+  double *capc = v;   // (v is free again: the candidate capture pose, for the cost)
   if (lane < 6) {
     const double yv = yc[lane];
     const double d = -yv * scale[sc + lane];
     const double xo = x[sc + lane];
     const double xn = xo + d;
     xc[sc + lane] = xn;
+    capc[lane] = xn;
     if (P.slot_free[sc + lane]) st = (xo - xn) * (xo - xn);
     bad = isfinite(yv) ? 0.0 : 1.0;
   }
@@ -783,6 +858,12 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
     parts[(long)P_MODEL * P.nc + c] = mpart;
     parts[(long)P_STEP2 * P.nc + c] = st;
     parts[(long)P_YBAD * P.nc + c] = bad;
+  }
+  // the candidate's cost (k_cost fused): camera and tags of xc were written
+  // by k_update_f, launched before this kernel
+  if (with_cost) {
+    __syncthreads();
+    capture_cost(P, xc, capc, c, parts);
   }
 }
 
@@ -824,55 +905,6 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
   if (threadIdx.x == 0) {
     fparts[2L * blockIdx.x] = red[0][0];
     fparts[2L * blockIdx.x + 1] = red[1][0];
-  }
-}
-
-// Cost at x (candidate evaluation): per-capture active / fixed cost, finiteness.
-__global__ __launch_bounds__(kWave) void k_cost(DevProblem P, const double *__restrict__ x,
-                                                double *__restrict__ parts) {
-  __shared__ double sq[kWave];
-  __shared__ double ocost[kMaxTagsPerCapture];
-  const int c = blockIdx.x, lane = threadIdx.x;
-  const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
-  const int nrows = 8 * k;
-  const double *cam = x;
-  const double *cap = x + slot_cap(P, c);
-  const AngleAxis ac = aa_prepare(cap + 3);
-  double bad = 0.0;
-  for (int base = 0; base < nrows; base += kWave) {
-    const int row = base + lane;
-    double r2 = 0.0;
-    if (row < nrows) {
-      const int q = row >> 3, corner = (row >> 1) & 3, comp = row & 1;
-      const int obs = o0 + q;
-      const double *tag = x + slot_tag(P, P.obs_tag[obs]);
-      const AngleAxis at = aa_prepare(tag + 3);
-      const double obsv = P.corners[8L * obs + 2 * corner + comp];
-      const bool sw = P.swap_roles != 0;   // tag elimination: the capture is the f-block
-      const double r = residual_row(sw ? at : ac, sw ? tag : cap, sw ? ac : at, sw ? cap : tag, cam[0], corner,
-                                    comp, obsv, nullptr, nullptr);
-      if (!isfinite(r)) bad = 1.0;
-      r2 = r * r;
-    }
-    sq[lane] = r2;
-    __syncthreads();
-    if (lane < 8 && base / 8 + lane < k) {
-      double s = 0.0;
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr) s += sq[8 * lane + rr];
-      ocost[base / 8 + lane] = 0.5 * s;
-    }
-    __syncthreads();
-  }
-  bad = wave_max(bad);
-  if (lane == 0) {
-    double act = 0.0, fix = 0.0;
-    for (int q = 0; q < k; ++q) {
-      if (P.obs_active[o0 + q]) act += ocost[q]; else fix += ocost[q];
-    }
-    parts[(long)P_COST * P.nc + c] = act;
-    parts[(long)P_FIXED * P.nc + c] = fix;
-    parts[(long)P_CBAD * P.nc + c] = bad;
   }
 }
 
@@ -1052,8 +1084,9 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
 }
 
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                  double radius, double *S, hipStream_t s, bool prep) {
+                  double radius, double *S, hipStream_t s, bool prep, long zero_tiles) {
   if (P.nc == 0) {
+    if (zero_tiles) (void)hipMemsetAsync(S, 0, (size_t)zero_tiles * 4096 * sizeof(double), s);
     if (prep) launch_prep_reduced(P, diag, radius, S, s);
     return;
   }
@@ -1061,7 +1094,7 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
   const int m = 1 + 6 * maxk;
   const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 7L * m + 4 + 28L * maxk) +
                      sizeof(int) * (maxk + 2) + 2 * sizeof(double) + 64;
-  hipLaunchKernelGGL(k_schur, dim3(P.nc), dim3(kWave), lds, s, P, scale, diag, radius);
+  hipLaunchKernelGGL(k_schur, dim3((unsigned)(P.nc + zero_tiles)), dim3(kWave), lds, s, P, scale, diag, radius, S);
   const double *pd = prep ? diag : nullptr;
   const unsigned gb = (unsigned)((P.n_items + 3) / 4) + (prep ? (unsigned)((P.N + 255) / 256) : 0u);
   if (gb) hipLaunchKernelGGL(k_schur_gather, dim3(gb), dim3(256), 0, s, P, S, pd, radius);
@@ -1078,11 +1111,12 @@ void launch_prep_reduced(const DevProblem &P, const double *diag, double radius,
 
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
                     double radius, const double *yF, double *xc, double *parts, hipStream_t s,
-                    bool reuse_ui) {
+                    bool reuse_ui, bool with_cost) {
   if (P.nc == 0) return;
   const int maxk = P.max_obs_per_cap;
   const size_t lds = lds_rows(maxk) + sizeof(double) * (8L * maxk + 36 + 36 + 16);
-  hipLaunchKernelGGL(k_backsub, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts, reuse_ui ? 1 : 0);
+  hipLaunchKernelGGL(k_backsub, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts,
+                     reuse_ui ? 1 : 0, with_cost ? 1 : 0);
 }
 
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,

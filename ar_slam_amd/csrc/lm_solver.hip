@@ -726,10 +726,12 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     reuse_diag = true;
     if (has_f) {
       timers[PH_SCHUR].start(stream);
-      arslam::launch_zero_tiles(plan, d_S.p, stream);
       // one rank: the gather writes the final S (D_f^2 and the padding rows
-      // included); several: S is summed over the ranks first
-      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1);
+      // included); several: S is summed over the ranks first.  k_schur's extra
+      // blocks clear S's tiles first.
+      static const bool memset_s = std::getenv("ARSLAM_MEMSET_S") != nullptr;   // (A/B switch)
+      if (memset_s) arslam::launch_zero_tiles(plan, d_S.p, stream);
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1, memset_s ? 0 : plan.n_tiles);
       if (nranks > 1) {
         allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ARSLAM_OP_SUM);
         arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
@@ -806,12 +808,14 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       timers[PH_SOLVE].stop(stream);
     }
     timers[PH_BACK].start(stream);
-    // (k_backsub writes every capture slot of xc, k_update_f every other slot)
-    arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream, has_f);
+    // (k_update_f writes every f-side slot of xc, k_backsub every capture
+    // slot, then evaluates the candidate's cost per capture: k_cost fused)
+    static const bool split_cost = std::getenv("ARSLAM_SPLIT_COST") != nullptr;   // (A/B switch)
     arslam::launch_update_f(P, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
+    arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream, has_f, !split_cost);
     timers[PH_BACK].stop(stream);
     timers[PH_COST].start(stream);
-    arslam::launch_cost(P, xc, d_parts.p, stream);
+    if (split_cost) arslam::launch_cost(P, xc, d_parts.p, stream);
     arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p);
     if (nranks > 1) {
       // model change, capture step^2, candidate cost, fixed; flags by max
