@@ -1191,9 +1191,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         const int k = a.ks[q];
         if (q > it.y) __syncthreads();
         load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tid);
-        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, tj, k), X, tid);
+        if (ti != tj) load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, tj, k), X, tid);
         __syncthreads();
-        gemm64_nt(D, X, tid, acc);
+        gemm64_nt(D, ti != tj ? X : D, tid, acc);   // a diagonal target: one operand tile, fetched once
       }
       bool apply = true;
       if (sid >= 0) {

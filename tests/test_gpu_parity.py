@@ -279,3 +279,17 @@ def test_cfg3_repeated_solves_are_bit_identical(lm):
         assert [i["trust_region_radius"] for i in s["iterations"]] == \
             [i["trust_region_radius"] for i in ref["iterations"]]
         assert np.array_equal(rp.tag, tags)
+
+
+def test_executor_grid_size_does_not_change_the_result(lm, monkeypatch):
+    """The persistent factorization sums every tile in a fixed order whatever the grid, so any
+    number of workgroups gives bit-identical steps.  Small grids also exercise the claim cap
+    (claimed continuation targets in flight <= half the grid; with one workgroup, none) and the
+    deadlock-freedom of the ticket order with few workers."""
+    g = synth.config_graph("cfg2")
+    cam, cap, tag, ref = lm.solve_graph(g)
+    for grid in ("1", "3", "64"):
+        monkeypatch.setenv("ARSLAM_DAG_GRID", grid)
+        c2, p2, t2, s = lm.solve_graph(g)
+        assert [i["cost"] for i in s["iterations"]] == [i["cost"] for i in ref["iterations"]], grid
+        assert np.array_equal(t2, tag) and np.array_equal(p2, cap) and np.array_equal(c2, cam), grid
