@@ -320,8 +320,12 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   const int nrows = 8 * k;
   const int b0 = P.cap_blk_start[c], nblk = P.cap_blk_start[c + 1] - b0;
   const int m = 1 + 6 * nblk;   // local f-side columns: f, then 6 per distinct tag
-  double *rows = sm;
-  double *U = rows + (long)nrows * kRowStride;   // 36
+  // LDS: no copy of the Jacobian rows (they go from HBM straight into the
+  // MFMA operand registers), so ~8 KB per wave: 4-5 waves per SIMD instead
+  // of the 2.75 the 13.5 KB row-staging layout allowed (latency-bound kernel)
+  double *stage = sm;                            // 6 (m + 1): one block row of the output, staged
+  double *tscale = stage + 6 * (m + 1);          // 6 k: each observation's tag column scales
+  double *U = tscale + 6 * k;                    // 36
   double *Ui = U + 36;                           // 36
   double *Etr = Ui + 36;                         // 8
   double *W = Etr + 8;                           // 6*m
@@ -331,7 +335,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   double *ff00 = reinterpret_cast<double *>(lblk + k + (k & 1));   // F_0'F_0
 
   for (int q = lane; q < k; q += kWave) lblk[q] = P.obs_lblk[o0 + q];
-  load_rows(P, scale, c, o0, nrows, rows);
+  for (int e = lane; e < 6 * k; e += kWave) tscale[e] = scale[slot_tag(P, P.obs_tag[o0 + e / 6]) + e % 6];
   __syncthreads();
   SCHUR_STAMP(0);
   // Every product below is an entry of an observation's Gram matrix over its
@@ -350,11 +354,39 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     typedef double dbl4v __attribute__((ext_vector_type(4)));
     dbl4v tot = {0, 0, 0, 0};
+    // lane (lk, li) reads column li of rows 8q + lk and 8q + 4 + lk from the
+    // capture's column-major Jacobian block (load_rows' layout), eight
+    // observations' loads in flight at once, and scales it as load_rows does
+    // (the same products: the Grams are bit-identical)
+    const double *jb = P.jrows + 8L * o0 * kRowStride;
+    const double *sc = scale + slot_cap(P, c);
+    const double cs = li == 0 ? scale[0] : li <= 6 ? sc[li - 1] : 1.0;   // (tag columns: tscale)
+    const bool tagcol = li >= 7 && li <= 12, valid = li < 14;
+    double jv[16];
     for (int q = 0; q < k; ++q) {
+      if ((q & 7) == 0) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int st = 0; st < 2; ++st)
+            jv[2 * u + st] = (valid && q + u < k) ? jb[(long)li * nrows + 8 * (q + u) + 4 * st + lk] : 0.0;
+      }
       dbl4v g = {0, 0, 0, 0};
+      const double s = tagcol ? tscale[6 * q + li - 7] : cs;
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        const double v = li < kRowStride ? rows[(long)(8 * q + 4 * st + lk) * kRowStride + li] : 0.0;
+        double v = 0.0;
+        switch (q & 7) {   // (register array: constant indices only)
+          case 0: v = jv[0 + st]; break;
+          case 1: v = jv[2 + st]; break;
+          case 2: v = jv[4 + st]; break;
+          case 3: v = jv[6 + st]; break;
+          case 4: v = jv[8 + st]; break;
+          case 5: v = jv[10 + st]; break;
+          case 6: v = jv[12 + st]; break;
+          default: v = jv[14 + st]; break;
+        }
+        v = li == 13 ? v : v * s;   // the residual column is not scaled
         g = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, g, 0, 0, 0);
       }
       tot += g;
@@ -448,7 +480,6 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   // with contiguous stores.
   //   (p, q) = F_p'F_q - W_p' z_q,   (m, q) = F_q'r - (E'r)' z_q
   double *out = P.slab + P.cap_off[c];
-  double *stage = rows;   // <= 6 (m + 1) doubles
   auto make_z = [&](int q, double z[6]) {
     if (q < m) {
       double wq[6];
@@ -1092,7 +1123,7 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
   }
   const int maxk = P.max_obs_per_cap;
   const int m = 1 + 6 * maxk;
-  const size_t lds = lds_rows(maxk) + sizeof(double) * (36 + 36 + 8 + 7L * m + 4 + 28L * maxk) +
+  const size_t lds = sizeof(double) * (6L * (m + 1) + 6L * maxk + 36 + 36 + 8 + 7L * m + 4 + 28L * maxk) +
                      sizeof(int) * (maxk + 2) + 2 * sizeof(double) + 64;
   hipLaunchKernelGGL(k_schur, dim3((unsigned)(P.nc + zero_tiles)), dim3(kWave), lds, s, P, scale, diag, radius, S);
   const double *pd = prep ? diag : nullptr;
