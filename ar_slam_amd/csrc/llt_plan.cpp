@@ -99,6 +99,17 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   std::vector<int> ndep(n, 0);
   std::vector<double> cost(n);
   std::vector<int> pr;
+  // task costs (us): POTRF base, per folded column, fused TRSM; TRSM; update
+  // base, per column; INV (ARSLAM_SIM_COST="p,pk,ps,t,u,uk,i": debug sweeps).
+  // The update items are weighted well above their uncontended run time
+  // (4 + 4 per column): under the ~300 concurrent updates of the wide levels
+  // they run ~2-3x slower and hold the memory system the chain needs, and a
+  // schedule that budgets for that draws the chain tasks ahead of them
+  // (cfg3 k_factor_dag 720 -> ~688 us with 16 + 16 per column; flat from
+  // 12 + 12 to 20 + 12, worse at 24 + 24; tools/env_bench.sh sweeps).
+  double cc[7] = {16.0, 4.0, 5.0, 6.0, 16.0, 16.0, 5.0};
+  if (const char *e = std::getenv("ARSLAM_SIM_COST"))
+    std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf,%lf", &cc[0], &cc[1], &cc[2], &cc[3], &cc[4], &cc[5], &cc[6]);
   for (int v = 0; v < n; ++v) {
     const DagNode &nd = nodes[v];
     pr.clear();
@@ -121,14 +132,14 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
     }
     if (nd.task.x == 0) {
       const int nk = nd.task.z >= 0 ? plan.h_items[nd.task.z].z - plan.h_items[nd.task.z].y : 0;
-      cost[v] = 16.0 + 4.0 * nk + (nd.sub >= 0 ? 5.0 : 0.0);
+      cost[v] = cc[0] + cc[1] * nk + (nd.sub >= 0 ? cc[2] : 0.0);
     } else if (nd.task.x == 1) {
-      cost[v] = 6.0 + (nd.fold >= 0 ? 4.0 * (plan.h_items[nd.fold].z - plan.h_items[nd.fold].y) : 0.0);
+      cost[v] = cc[3] + (nd.fold >= 0 ? cc[5] * (plan.h_items[nd.fold].z - plan.h_items[nd.fold].y) : 0.0);
     } else if (nd.task.x == 3) {
-      cost[v] = 5.0;
+      cost[v] = cc[6];
     } else {
       const int4 it = plan.h_items[nd.task.y];
-      cost[v] = 4.0 + 4.0 * (it.z - it.y);
+      cost[v] = cc[4] + cc[5] * (it.z - it.y);
     }
   }
   // bottom levels (nodes are created producers-first: a reverse sweep is a valid order)
