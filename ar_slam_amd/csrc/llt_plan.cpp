@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include "lm_internal.h"
 
 #include <algorithm>
@@ -27,14 +28,6 @@ void check(hipError_t e, const char *what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-template <class T>
-T *upload(const std::vector<T> &h, hipStream_t s) {
-  if (h.empty()) return nullptr;
-  T *d = nullptr;
-  check(hipMalloc(&d, h.size() * sizeof(T)), "hipMalloc(plan)");
-  check(hipMemcpyAsync(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s), "plan upload");
-  return d;
-}
 
 }  // namespace
 
@@ -573,7 +566,7 @@ void dag_build(LltPlan &plan) {
 }
 
 void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) {
-  llt_plan_free(plan);
+  llt_plan_reset(plan);
   plan.T = T;
   plan.lda = lda;
   // compact tile numbering: assembled tiles (the input pattern + diagonal) first
@@ -832,34 +825,66 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
 
 void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   const int T = plan.T;
-  plan.panel = upload(plan.h_panel, s);
-  plan.upd_targets = upload(plan.h_targets, s);
-  plan.upd_kstart = upload(plan.h_kstart, s);
-  plan.upd_ks = upload(plan.h_ks, s);
-  plan.upd_items = upload(plan.h_items, s);
-  plan.upd_split = upload(plan.h_split, s);
   plan.n_split = (long)plan.h_split.size();
-  check(hipMalloc(&plan.upd_cnt, std::max<size_t>(plan.h_split.size(), 1) * sizeof(int)), "hipMalloc(upd_cnt)");
-  check(hipMalloc(&plan.upd_part, std::max<long>(plan.n_part, 1) * 4096 * sizeof(double)), "hipMalloc(upd_part)");
-  plan.bs_cols = upload(plan.h_bcols, s);
-  plan.bs_gather = upload(plan.h_gather, s);
-  plan.bs_gbeg = upload(plan.h_gbeg, s);
-  check(hipMalloc(&plan.bs_part, std::max<size_t>(plan.h_gather.size(), 1) * 64 * sizeof(double)), "hipMalloc(bs_part)");
-  check(hipMalloc(&plan.bs_counters, ((size_t)T + 1) * sizeof(int)), "hipMalloc(bs_counters)");
-  plan.tile_id = upload(plan.h_tile_id, s);
+  // lay the arrays out in one arena (256-byte aligned), stage the host ones in
+  // one buffer, and copy them with one transfer
+  struct Piece { void **dst; const void *src; size_t bytes; };
+  std::vector<Piece> pieces;
+  auto add = [&](void **dst, const void *src, size_t bytes) { pieces.push_back({dst, src, bytes}); };
+  auto addv = [&](auto **dst, const auto &v) { add(reinterpret_cast<void **>(dst), v.data(), v.size() * sizeof(v[0])); };
+  addv(&plan.panel, plan.h_panel);
+  addv(&plan.upd_targets, plan.h_targets);
+  addv(&plan.upd_kstart, plan.h_kstart);
+  addv(&plan.upd_ks, plan.h_ks);
+  addv(&plan.upd_items, plan.h_items);
+  addv(&plan.upd_split, plan.h_split);
+  add(reinterpret_cast<void **>(&plan.upd_cnt), nullptr, std::max<size_t>(plan.h_split.size(), 1) * sizeof(int));
+  add(reinterpret_cast<void **>(&plan.upd_part), nullptr, std::max<long>(plan.n_part, 1) * 4096 * sizeof(double));
+  addv(&plan.bs_cols, plan.h_bcols);
+  addv(&plan.bs_gather, plan.h_gather);
+  addv(&plan.bs_gbeg, plan.h_gbeg);
+  add(reinterpret_cast<void **>(&plan.bs_part), nullptr, std::max<size_t>(plan.h_gather.size(), 1) * 64 * sizeof(double));
+  add(reinterpret_cast<void **>(&plan.bs_counters), nullptr, ((size_t)T + 1) * sizeof(int));
+  addv(&plan.tile_id, plan.h_tile_id);
   // L_kk, L_kk^{-1}, and the 16x16 block inverses (4 x 16 x 18) of each column
-  check(hipMalloc(&plan.ldiag, ((size_t)2 * T * 64 * 64 + (size_t)T * 1152) * sizeof(double)), "hipMalloc(ldiag)");
-  plan.dag_tasks = upload(plan.h_dag_tasks, s);
-  plan.dag_wait_off = upload(plan.h_dag_wait_off, s);
-  plan.dag_waits = upload(plan.h_dag_waits, s);
-  plan.dag_sub = upload(plan.h_dag_sub, s);
-  plan.dag_cont = upload(plan.h_dag_cont, s);
-  plan.dag_maxdep = upload(plan.h_dag_maxdep, s);
-  plan.dag_cand = upload(plan.h_dag_cand, s);
-  plan.dag_fold = upload(plan.h_dag_fold, s);
-  check(hipMalloc(&plan.dag_claimed, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int)), "hipMalloc(dag_claimed)");
-  check(hipMalloc(&plan.dag_counters, (2 * (size_t)plan.n_tiles + 2) * sizeof(int)), "hipMalloc(dag_counters)");
-  check(hipStreamSynchronize(s), "plan sync");
+  add(reinterpret_cast<void **>(&plan.ldiag), nullptr, ((size_t)2 * T * 64 * 64 + (size_t)T * 1152) * sizeof(double));
+  addv(&plan.dag_tasks, plan.h_dag_tasks);
+  addv(&plan.dag_wait_off, plan.h_dag_wait_off);
+  addv(&plan.dag_waits, plan.h_dag_waits);
+  addv(&plan.dag_sub, plan.h_dag_sub);
+  addv(&plan.dag_cont, plan.h_dag_cont);
+  addv(&plan.dag_maxdep, plan.h_dag_maxdep);
+  addv(&plan.dag_cand, plan.h_dag_cand);
+  addv(&plan.dag_fold, plan.h_dag_fold);
+  add(reinterpret_cast<void **>(&plan.dag_claimed), nullptr, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int));
+  add(reinterpret_cast<void **>(&plan.dag_counters), nullptr, (2 * (size_t)plan.n_tiles + 2) * sizeof(int));
+  size_t total = 0, staged = 0;
+  std::vector<size_t> off(pieces.size());
+  for (size_t i = 0; i < pieces.size(); ++i) {   // host arrays first: one contiguous copy
+    if (!pieces[i].src || !pieces[i].bytes) continue;
+    off[i] = total;
+    total += (pieces[i].bytes + 255) & ~size_t(255);
+  }
+  staged = total;
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    if (pieces[i].src && pieces[i].bytes) continue;
+    off[i] = total;
+    total += (pieces[i].bytes + 255) & ~size_t(255);
+  }
+  if (total > plan.arena_bytes) {
+    if (plan.arena) (void)hipFree(plan.arena);
+    plan.arena = nullptr;
+    plan.arena_bytes = 0;
+    check(hipMalloc(&plan.arena, total), "hipMalloc(plan arena)");
+    plan.arena_bytes = total;
+  }
+  std::vector<char> host(staged);
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    *pieces[i].dst = pieces[i].bytes ? plan.arena + off[i] : nullptr;
+    if (pieces[i].src && pieces[i].bytes) std::memcpy(host.data() + off[i], pieces[i].src, pieces[i].bytes);
+  }
+  if (staged) check(hipMemcpyAsync(plan.arena, host.data(), staged, hipMemcpyHostToDevice, s), "plan upload");
+  check(hipStreamSynchronize(s), "plan sync");   // (the staging buffer goes out of scope)
 }
 
 void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hipStream_t s) {
@@ -867,15 +892,16 @@ void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hip
   llt_plan_upload(plan, s);
 }
 
+void llt_plan_reset(LltPlan &plan) {
+  char *arena = plan.arena;
+  const size_t bytes = plan.arena_bytes;
+  plan = LltPlan{};
+  plan.arena = arena;
+  plan.arena_bytes = bytes;
+}
+
 void llt_plan_free(LltPlan &plan) {
-  for (void *p : {(void *)plan.panel, (void *)plan.upd_targets, (void *)plan.upd_kstart,
-                  (void *)plan.upd_ks, (void *)plan.upd_items, (void *)plan.upd_split,
-                  (void *)plan.upd_cnt, (void *)plan.upd_part, (void *)plan.bs_cols, (void *)plan.bs_gather,
-                  (void *)plan.bs_gbeg, (void *)plan.bs_part, (void *)plan.bs_counters, (void *)plan.tile_id, (void *)plan.ldiag,
-                  (void *)plan.dag_tasks, (void *)plan.dag_wait_off, (void *)plan.dag_waits,
-                  (void *)plan.dag_sub, (void *)plan.dag_cont, (void *)plan.dag_maxdep, (void *)plan.dag_claimed,
-                  (void *)plan.dag_counters, (void *)plan.dag_cand, (void *)plan.dag_fold})
-    if (p) (void)hipFree(p);
+  if (plan.arena) (void)hipFree(plan.arena);
   plan = LltPlan{};
 }
 

@@ -88,6 +88,10 @@ __device__ inline double *reduced_elem(double *S, const DevProblem &P, long r, l
 // Tile plan of the reduced-system Cholesky (dense_llt.hip), level-scheduled
 // over the tile elimination tree.  Device arrays, host per-level offsets.
 struct LltPlan {
+  // every device array of the plan lives in one grow-only arena (one
+  // allocation and one host->device copy per load; kept across re-plans)
+  char *arena = nullptr;
+  size_t arena_bytes = 0;
   int T = 0;
   long lda = 0;
   int nlev = 0;
@@ -170,7 +174,8 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed);
 void llt_plan_upload(LltPlan &plan, hipStream_t s);
 // llt_plan_symbolic + llt_plan_upload
 void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern, hipStream_t s);
-void llt_plan_free(LltPlan &plan);
+void llt_plan_free(LltPlan &plan);                 // device arrays and the arena
+void llt_plan_reset(LltPlan &plan);                // host side only; the arena is kept for the next plan
 
 
 // ---- lm_kernels.hip ----
