@@ -6,6 +6,7 @@
 #include "host_structure.h"
 
 #include <algorithm>
+#include <chrono>
 #include <iterator>
 #include <cstdio>
 #include <cstdlib>
@@ -610,6 +611,9 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
                              const ReduceMaxU8 &pattern_max,
                              const std::vector<int> *reuse_tag_row, long reuse_edges) {
+  static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: layout phases
+  auto clk = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double tl[5] = {prof ? clk() : 0.0, 0, 0, 0, 0};
   // Rows exist only for free tags and a free camera (constant / unused blocks
   // are not parameters).  Tags are ordered natural, RCM or by nested
   // dissection; with ND every part starts on a tile boundary so the tile
@@ -633,17 +637,32 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
         for (int b = 0; b < nt; ++b)
           if (bm[(size_t)a * nt + b] && tfree[a] && tfree[b]) adj[a].push_back(b);
     } else {
+      // per tag, the distinct tags of the captures observing it (a stamp
+      // array dedupes them before the sort: the pairs repeat in every
+      // capture that sees both)
+      std::vector<int> obs_cap(h.cap_start.empty() ? 0 : h.cap_start[nc]);
       for (int c = 0; c < nc; ++c)
-        for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a)
-          for (int b = h.cap_blk_start[c]; b < h.cap_blk_start[c + 1]; ++b)
-            if (a != b && tfree[h.blk_tag[a]] && tfree[h.blk_tag[b]]) adj[h.blk_tag[a]].push_back(h.blk_tag[b]);
-      for (auto &v : adj) {
+        for (int o = h.cap_start[c]; o < h.cap_start[c + 1]; ++o) obs_cap[o] = c;
+      std::vector<int> stamp(nt, -1);
+      for (int a = 0; a < nt; ++a) {
+        if (!tfree[a]) continue;
+        std::vector<int> &v = adj[a];
+        for (int q = h.tag_start[a]; q < h.tag_start[a + 1]; ++q) {
+          const int c = obs_cap[h.tag_obs[q]];
+          for (int bb = h.cap_blk_start[c]; bb < h.cap_blk_start[c + 1]; ++bb) {
+            const int b = h.blk_tag[bb];
+            if (b != a && tfree[b] && stamp[b] != a) {
+              stamp[b] = a;
+              v.push_back(b);
+            }
+          }
+        }
         std::sort(v.begin(), v.end());
-        v.erase(std::unique(v.begin(), v.end()), v.end());
       }
     }
   }
   for (auto &v : adj) L.n_edges += (long)v.size();
+  if (prof) tl[1] = clk();
   bool reuse = reuse_tag_row && (int)reuse_tag_row->size() == std::max(nt, 1) && 10 * L.n_edges <= 11 * reuse_edges;
   L.order_edges = reuse ? reuse_edges : L.n_edges;
   for (int t = 0; reuse && t < nt; ++t) reuse = ((*reuse_tag_row)[t] >= 0) == (tfree[t] != 0);
@@ -697,7 +716,9 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
     row += 3;
   }
   L.nR = row;
+  if (prof) tl[2] = clk();
   L.scalar_flops = scalar_cholesky_flops(adj, L.tag_row, L.cam_row >= 0);
+  if (prof) tl[3] = clk();
   if (L.nR == 0) return L;
   L.N = round_up(L.nR + 1, kTileRows);
   const int T = L.T = (int)(L.N / kTileRows);
@@ -728,6 +749,9 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   const int rhs = (int)(L.nR / kTileRows);
   for (int j = 0; j <= rhs; ++j) L.pattern[(size_t)rhs * T + j] = 1;
   if (pattern_max) pattern_max(L.pattern);
+  if (prof)
+    std::fprintf(stderr, "arslam layout: adj %.3f order %.3f flops %.3f pattern %.3f ms\n", tl[1] - tl[0],
+                 tl[2] - tl[1], tl[3] - tl[2], clk() - tl[3]);
   return L;
 }
 
