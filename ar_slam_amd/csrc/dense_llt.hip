@@ -852,6 +852,7 @@ struct DagArgs {
   double *part;
   int *split_cnt;
   int *flag;
+  int cu_yield;               // update items pause while a POTRF runs on their CU (per-CU flags after the counters)
   int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
   unsigned long long *trace;  // debug: [n_tasks][8] s_memrealtime at draw / waits met / end, workgroup, sub-phases
 };
@@ -883,6 +884,23 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // always draw the lowest unfinished ticket, whose producers are all done.
   int *inflight = ticket + 1;
   const int cont_cap = (int)(gridDim.x / 2);
+  // Per-CU "POTRF running" flags (performance only: a wrong or stale flag
+  // costs a bounded pause, never a result).  The 64x64 POTRF is a chain of
+  // dependent LDS/VALU steps on one wave; the other workgroup on its CU runs
+  // update GEMMs that take SIMD issue and LDS bandwidth from it (the POTRF
+  // phase takes ~11 us in the contended half of the factorization, 8.5
+  // beside idle neighbours), so updates on that CU hold their next GEMM
+  // (at most ~55 us) while the flag is up: cfg3 k_factor_dag 689 -> ~675 us.
+  // A flag held across the POTRF task's late wait made it 2x slower (the
+  // wait can need an update the flag holds).
+  int *cu_flag = inflight + 1;
+  int cu_key = 0;
+  if (a.cu_yield) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    cu_key = (int)(((xcc & 7u) << 8) | ((hw >> 8) & 0xffu));   // XCC, SE, SH, CU
+  }
   // Continuation targets stay ordinary tickets with a claim flag.  The
   // predecessor's workgroup claims its target (before publishing the tile the
   // target waits for, so it wins whenever it claims) if every task the target
@@ -937,6 +955,11 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // ---- POTRF k: publish L_kk and its 16x16 block inverses, then (off the
       // critical path) the full inverse for the backward solve ----
       const int k = task.y;
+      // this CU's flag is up from the fold to the end of the factorization,
+      // never across a wait (an update held on this CU may be what a wait
+      // needs; the early waits are met here, the late ones come after)
+      if (a.cu_yield && tid == 0)
+        __hip_atomic_store(cu_flag + cu_key, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (task.z >= 0) {
         // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
         const int4 it = a.items[task.z];
@@ -1040,6 +1063,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           if (wv == 1 && ln == 0) sh[5] = 1;
         }
       });
+      if (a.cu_yield && tid == 0)
+        __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
         int first = 0;
@@ -1190,6 +1215,15 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       for (int q = it.y; q < it.z; ++q) {
         const int k = a.ks[q];
         if (q > it.y) __syncthreads();
+        if (a.cu_yield) {   // hold the GEMM while a POTRF runs on this CU (bounded)
+          if (tid == 0) {
+            for (int spin = 0; spin < 256 &&
+                               __hip_atomic_load(cu_flag + cu_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                 ++spin)
+              __builtin_amdgcn_s_sleep(8);
+          }
+          __syncthreads();
+        }
         load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tid);
         if (ti != tj) load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, tj, k), X, tid);
         __syncthreads();
@@ -1559,7 +1593,7 @@ __global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c
 }  // namespace
 
 void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagArgs *ld) {
-  const long na = P.n_dag_tasks ? 2 * P.n_tiles + 2 : 0, nb = P.n_dag_tasks, nc = P.n_split,
+  const long na = P.n_dag_tasks ? 2 * P.n_tiles + 2 + kCuFlags : 0, nb = P.n_dag_tasks, nc = P.n_split,
              nd = P.h_bcols.empty() ? 0 : (long)P.T + 1;
   LmDiagArgs l{};
   if (ld) l = *ld;
@@ -1598,14 +1632,14 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
                           unsigned long long *trace, bool reset) {
   if (P.n_dag_tasks == 0) return;
   if (reset) {
-    (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2) * sizeof(int), s);
+    (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2 + kCuFlags) * sizeof(int), s);
     (void)hipMemsetAsync(P.dag_claimed, 0, (size_t)P.n_dag_tasks * sizeof(int), s);
     if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
   }
   DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
             P.dag_maxdep, P.dag_claimed, P.dag_cand, P.dag_fold, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
-            P.upd_part, P.upd_cnt, flag, progress, trace};
+            P.upd_part, P.upd_cnt, flag, std::getenv("ARSLAM_NO_CU_YIELD") ? 0 : 1, progress, trace};
   const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
 }

@@ -857,7 +857,7 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   addv(&plan.dag_cand, plan.h_dag_cand);
   addv(&plan.dag_fold, plan.h_dag_fold);
   add(reinterpret_cast<void **>(&plan.dag_claimed), nullptr, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int));
-  add(reinterpret_cast<void **>(&plan.dag_counters), nullptr, (2 * (size_t)plan.n_tiles + 2) * sizeof(int));
+  add(reinterpret_cast<void **>(&plan.dag_counters), nullptr, (2 * (size_t)plan.n_tiles + 2 + kCuFlags) * sizeof(int));
   size_t total = 0, staged = 0;
   std::vector<size_t> off(pieces.size());
   for (size_t i = 0; i < pieces.size(); ++i) {   // host arrays first: one contiguous copy

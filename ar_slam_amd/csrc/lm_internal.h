@@ -17,6 +17,7 @@
 #include "host_structure.h"
 
 namespace arslam {
+constexpr int kCuFlags = 2048;   // k_factor_dag's per-CU flags: 8 XCCs x 256 (SE, SH, CU) ids
 
 constexpr int kWave = 64;
 constexpr int kTile = 64;          // reduced-system Cholesky tile
@@ -148,6 +149,7 @@ struct LltPlan {
   int *dag_fold = nullptr;
   std::vector<int> h_dag_fold;
   int *dag_wait_off = nullptr;
+  // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags])
   int2 *dag_waits = nullptr;
   int *dag_counters = nullptr;
   long n_dag_tasks = 0;
