@@ -1510,20 +1510,28 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
 #pragma unroll
       for (int m = 0; m < 16; ++m) lv[m] = Lik[(w + 4 * m) * T64 + lane];
       if (w == 0) {
-        if (lane == 0) {
-          long spins = 0;
-          while (ld_acquire_relaxed(done + i) < 1) {
-            __builtin_amdgcn_s_sleep(ARSLAM_BSOLVE_SLEEP);
-            if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(flag) != 0)) {
-              atomicCAS(flag, 0, -(4000000 + b));
-              ok = false;
-              break;
-            }
+        // y_i is its own ready flag: the entries are kYSentinel until column
+        // i's task stores them (8-byte write-through stores, never torn), so
+        // the wait is the load itself -- no counter, no drain before it
+        double yv = 0.0;
+        bool mine = ri + lane < nR;
+        long spins = 0;
+        for (;;) {
+          if (mine) {
+            yv = ld_wt(yF + ri + lane);
+            mine = (unsigned long long)__double_as_longlong(yv) == kYSentinel;
           }
-          sh[1] = ok;
+          if (__builtin_amdgcn_ballot_w64(mine) == 0) break;
+          __builtin_amdgcn_s_sleep(ARSLAM_BSOLVE_SLEEP);
+          if (++spins > kSpinCap || (((spins & 255) == 0) &&
+                                     __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) != 0)) {
+            if (lane == 0) atomicCAS(flag, 0, -(4000000 + b));
+            ok = false;
+            break;
+          }
         }
-        asm volatile("" ::: "memory");   // y_i is loaded after the wait
-        ys[lane] = (ri + lane < nR) ? ld_wt(yF + ri + lane) : 0.0;
+        if (lane == 0) sh[1] = ok;
+        ys[lane] = (ri + lane < nR) ? yv : 0.0;
       }
       __syncthreads();
       if (!sh[1]) break;
@@ -1548,11 +1556,8 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
     for (int rr = 0; rr < 16; ++rr) s += xv[rr] * ys[16 * w + rr];
     red[w][lane] = s;
     __syncthreads();
-    if (w == 0) {
-      if (row0 + lane < nR) st_wt(yF + row0 + lane, ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(done + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (w == 0 && row0 + lane < nR)   // (published by the store itself; see the gathers)
+      st_wt(yF + row0 + lane, ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
   }
 }
 
@@ -1577,6 +1582,8 @@ namespace {
 __global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c, long nc, int *d, long nd,
                              LmDiagArgs ld) {
   const long n = na + nb + nc + nd;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < ld.nys; e += (long)gridDim.x * blockDim.x)
+    ld.ysent[e] = __longlong_as_double((long long)kYSentinel);
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n + ld.n; e += (long)gridDim.x * blockDim.x) {
     if (e < na) a[e] = 0;
     else if (e < na + nb) b[e - na] = 0;
@@ -1597,7 +1604,7 @@ void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagA
              nd = P.h_bcols.empty() ? 0 : (long)P.T + 1;
   LmDiagArgs l{};
   if (ld) l = *ld;
-  const long n = na + nb + nc + nd + l.n;
+  const long n = std::max(na + nb + nc + nd + l.n, l.nys);
   const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 1024));
   hipLaunchKernelGGL(k_exec_reset, dim3(grid), dim3(256), 0, s, flag, P.dag_counters, na, P.dag_claimed, nb,
                      P.upd_cnt, nc, P.bs_counters, nd, l);
@@ -1648,7 +1655,13 @@ void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, dou
                                  hipStream_t s, int n_workgroups, bool reset) {
   const int ncols = (int)P.h_bcols.size();
   if (ncols == 0) return;
-  if (reset) (void)hipMemsetAsync(P.bs_counters, 0, ((size_t)P.T + 1) * sizeof(int), s);
+  if (reset) {
+    (void)hipMemsetAsync(P.bs_counters, 0, ((size_t)P.T + 1) * sizeof(int), s);
+    // y to the "not solved" pattern (both 32-bit halves of kYSentinel are equal)
+    static_assert((kYSentinel >> 32) == (kYSentinel & 0xffffffffull), "kYSentinel halves");
+    if (nR > 0) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(yF), (int)(kYSentinel & 0xffffffffull),
+                                        2 * (size_t)nR, s);
+  }
   const int grid = std::min(n_workgroups, ncols);
   hipLaunchKernelGGL(k_bsolve_dag, dim3((unsigned)grid), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag, nR, P.bs_cols,
                      P.bs_gather, P.bs_gbeg, ncols, yF, P.bs_counters, flag);

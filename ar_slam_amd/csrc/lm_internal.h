@@ -244,7 +244,12 @@ struct LmDiagArgs {
   const double *scale, *colnorm;
   double dmin, dmax;
   double *diag;
+  double *ysent = nullptr;   // (also: the backward solve's y, nys rows, to kYSentinel)
+  long nys = 0;
 };
+// k_bsolve_dag's "not solved yet" value of a y entry: a signalling-NaN bit
+// pattern no arithmetic produces (those NaNs are quiet)
+constexpr unsigned long long kYSentinel = 0x7ff47ff47ff47ff4ull;
 // *flag and every counter of the two persistent executors to zero, one launch
 // (with ld: the LM diagonal in the same launch)
 void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagArgs *ld = nullptr);

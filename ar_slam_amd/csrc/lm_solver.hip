@@ -716,7 +716,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     if (exec_dag) {
       // flag + executor counters (+ the LM diagonal when it changed), one launch
       const arslam::LmDiagArgs ld{reuse_diag ? 0 : n, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal,
-                                  d_diag.p};
+                                  d_diag.p, d_yF.p, nR};
       arslam::launch_exec_reset(plan, d_flag.p, stream, &ld);
     } else {
       if (!reuse_diag)
