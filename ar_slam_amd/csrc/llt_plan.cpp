@@ -656,7 +656,9 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
       // split a long k-list into ~sqrt(m) chunks: chunk GEMMs run in parallel,
       // the last arriver reads ~sqrt(m) partial tiles
       const int m = (int)lks[t].size();
-      if (m > kSplitMin) {
+      static const int split_min = std::getenv("ARSLAM_SPLIT_MIN") ? std::atoi(std::getenv("ARSLAM_SPLIT_MIN"))
+                                                                   : kSplitMin;   // (debug sweeps)
+      if (m > split_min) {
         int nch = std::min(255, (int)std::ceil(std::sqrt((double)m)));
         const int ch = (m + nch - 1) / nch;
         nch = (m + ch - 1) / ch;
