@@ -395,21 +395,13 @@ __device__ void blocked_trsm64(double *X, const double *D, const double *inv, co
     const int b0 = 16 * p;
     if (p > 0)   // X[:, b0:b0+16] -= X[:, 0:b0] L[b0:b0+16, 0:b0]^T  (wave w: rows 16w..)
       wave_gemm16_sub(X + 16 * w * LQ + b0, X + 16 * w * LQ, D + b0 * LQ, b0, lane);
-#ifdef ARSLAM_TRSM_SYNC
-    __syncthreads();
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
     wave_apply_inv16(X + 16 * w * LQ + b0, LTd + p * 16 * LI, lane);
-#ifdef ARSLAM_TRSM_SYNC
-    __syncthreads();
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
   }
   __syncthreads();
 }
@@ -653,6 +645,11 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
 //               target's earlier levels, so the summation order is fixed.
 // ---------------------------------------------------------------------------
 constexpr int kLtdSize = 4 * 16 * LI;   // 1152 doubles
+// Spins before a dependency wait counts as a device fault.  One spin is a
+// memory-side atomic round trip (~1 us under load) plus the task type's sleep
+// below (one s_sleep unit = 64 cycles, ~27 ns): ~0.07 s for the chain tasks and
+// the backward solve (1 unit), ~0.1 s for the update tasks (16 units) -- far
+// beyond any legitimate wait (a whole factorization is < 1 ms).
 constexpr long kSpinCap = 1L << 16;
 // s_sleep units (64 cycles) between two polls of a dependency counter.  Every
 // poll is a device-scope atomic performed at the memory side; with a few
@@ -661,15 +658,9 @@ constexpr long kSpinCap = 1L << 16;
 // polls): cfg3 k_factor_dag 796 -> 757 us with the update tasks polling
 // every 16 units, flat from 16 to 32, worse at 64 (tools/variant_bench.sh).
 // The chain tasks (POTRF, TRSM) and the backward solve keep polling fast.
-#ifndef ARSLAM_POLL_SLEEP
-#define ARSLAM_POLL_SLEEP 16   // update tasks
-#endif
-#ifndef ARSLAM_CHAIN_SLEEP
-#define ARSLAM_CHAIN_SLEEP 1   // POTRF / TRSM tasks
-#endif
-#ifndef ARSLAM_BSOLVE_SLEEP
-#define ARSLAM_BSOLVE_SLEEP 1  // k_bsolve_dag (its waits are all on the chain)
-#endif   // ~0.1 s of polling: far beyond any legitimate wait
+constexpr int kPollSleep = 16;     // update tasks
+constexpr int kChainSleep = 1;     // POTRF / TRSM tasks
+constexpr int kBsolveSleep = 1;    // k_bsolve_dag (its waits are all on the chain)
 
 // Poll a dependency counter with an atomic read-modify-write (+0): counters
 // are advanced by device-scope atomic adds, and an RMW is performed where
@@ -780,19 +771,12 @@ __device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *
     const bool mine = w < w1;
     const int2 cv = mine ? waits[w] : make_int2(0, 0);
     long spins = 0;
-#ifdef ARSLAM_POLL_ONCE
-    bool open = mine;   // lanes whose counter has reached its value stop polling (counters only grow)
-    for (;;) {
-      if (open) open = ld_acquire_relaxed(counters + cv.x) < cv.y;
-      if (__builtin_amdgcn_ballot_w64(open) == 0) break;
-#else
     for (;;) {
       // (every lane re-polls each round: no loop-carried per-lane state)
       const int got = mine ? ld_acquire_relaxed(counters + cv.x) : 0;
       if (__builtin_amdgcn_ballot_w64(mine && got < cv.y) == 0) break;
-#endif
-      if (chain) __builtin_amdgcn_s_sleep(ARSLAM_CHAIN_SLEEP);
-      else __builtin_amdgcn_s_sleep(ARSLAM_POLL_SLEEP);
+      if (chain) __builtin_amdgcn_s_sleep(kChainSleep);
+      else __builtin_amdgcn_s_sleep(kPollSleep);
       if (++spins > kSpinCap) return false;
       if ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0) return false;
     }
@@ -838,8 +822,6 @@ struct DagArgs {
   const int *cont;            // [n_tasks] POTRF task the same workgroup may continue with (or -1)
   const int *maxdep;          // [n_tasks] continuation targets: largest ticket they wait on; else -1
   int *claimed;               // [n_tasks] continuation targets: claimed by the predecessor or the drawer
-  const int2 *cand;           // [n_tasks] ready-claim candidates (LltPlan::dag_cand)
-  const int *fold;            // [n_tasks] TRSM tasks: update item folded in first, or -1
   const int *wait_off;
   const int2 *waits;
   int *counters;              // ready[n_tiles] | applied[n_tiles] | ticket
@@ -852,7 +834,6 @@ struct DagArgs {
   double *part;
   int *split_cnt;
   int *flag;
-  int cu_yield;               // update items pause while a POTRF runs on their CU (per-CU flags after the counters)
   int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
   unsigned long long *trace;  // debug: [n_tasks][8] s_memrealtime at draw / waits met / end, workgroup, sub-phases
 };
@@ -895,7 +876,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // wait can need an update the flag holds).
   int *cu_flag = inflight + 1;
   int cu_key = 0;
-  if (a.cu_yield) {
+  {
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -958,7 +939,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // this CU's flag is up from the fold to the end of the factorization,
       // never across a wait (an update held on this CU may be what a wait
       // needs; the early waits are met here, the late ones come after)
-      if (a.cu_yield && tid == 0)
+      if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (task.z >= 0) {
         // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
@@ -1063,7 +1044,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           if (wv == 1 && ln == 0) sh[5] = 1;
         }
       });
-      if (a.cu_yield && tid == 0)
+      if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
@@ -1144,44 +1125,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // ---- TRSM i,k: L_ik L_kk^T = A_ik, blocked with the 16x16 inverses ----
       const int i = task.y, k = task.z;
       double *Ct = tile_ptr(a.S, a.tid_map, a.T, i, k);
-      const int fi = a.fold[t];
-      if (fi >= 0) {
-        // the tile's last update item first: A_ik - sum_j L_ij L_kj^T, the
-        // products summed in the item's order and subtracted once, as the
-        // item's own application does (llt_plan.cpp dag_build)
-        const int4 it = a.items[fi];
-        dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-        double av[16];   // A_ik (final but for the item) in the accumulator layout, in flight during the GEMMs
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg) av[4 * q + reg] = ld_wt(Ct + (rb + lk + 4 * reg) * T64 + cb + li);
-        }
-        for (int q = it.y; q < it.z; ++q) {
-          const int j = a.ks[q];
-          if (q > it.y) __syncthreads();
-          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, i, j), D, tid);
-          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, j), X, tid);
-          __syncthreads();
-          gemm64_nt(D, X, tid, acc);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg) X[(rb + lk + 4 * reg) * LQ + cb + li] = av[4 * q + reg] - acc[q][reg];
-        }
-        // the late wait: L_kk
-        if (w == 0) {
-          const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane, true);
-          if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
-        }
-        __syncthreads();
-      } else {
-        load_tile_wt(Ct, X, tid);
-      }
+      load_tile_wt(Ct, X, tid);
       load_tile_wt(a.Ld + (long)k * T64 * T64, D, tid);
       {
         const double *ltd_g = a.ltd + (long)k * kLtdSize;
@@ -1215,7 +1159,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       for (int q = it.y; q < it.z; ++q) {
         const int k = a.ks[q];
         if (q > it.y) __syncthreads();
-        if (a.cu_yield) {   // hold the GEMM while a POTRF runs on this CU (bounded)
+        {   // hold the GEMM while a POTRF runs on this CU (bounded)
           if (tid == 0) {
             for (int spin = 0; spin < 256 &&
                                __hip_atomic_load(cu_flag + cu_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1270,7 +1214,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           long spins = 0;
           bool ok = true;
           while (ld_acquire_relaxed(applied + task.w) < task.z) {
-            __builtin_amdgcn_s_sleep(ARSLAM_POLL_SLEEP);
+            __builtin_amdgcn_s_sleep(kPollSleep);
             if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(a.flag) < 0)) {
               ok = false;
               break;
@@ -1305,66 +1249,6 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     }
     DAG_PROGRESS(1, 4);
     if (cont && tid == 0) atomicSub(inflight, 1);   // this claimed target is done
-    if (task.x != 0 || sub.x < 0) {
-      // the task's designated successor (llt_plan.cpp dag_build), claimed
-      // when every other producer it names has been drawn (the fused POTRF
-      // above claims its parent's POTRF itself)
-      const int c = a.cont[t];
-      if (c >= 0) {
-        if (tid == 0) {
-          int claim = -1;
-          if (ld_acquire_relaxed(ticket) > a.maxdep[c]) {
-            if (atomicAdd(inflight, 1) < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0) claim = c;
-            else atomicSub(inflight, 1);
-          }
-          sh[4] = claim;
-        }
-        __syncthreads();
-        next = sh[4];
-      }
-    }
-    // Ready claim: a candidate successor (largest bottom level first) that is
-    // not drawn yet and whose waits all hold right now runs next on this
-    // workgroup, instead of waiting for its ticket behind blocked workgroups.
-    if (next < 0) {
-      const int2 cd = a.cand[t];
-      if (cd.x >= 0) {
-        if (w == 0) {
-          int tk = 0;
-          if (lane == 0) tk = ld_acquire_relaxed(ticket);
-          tk = __builtin_amdgcn_readfirstlane(tk);
-          int claim = -1;
-          for (int ci = 0; ci < 2; ++ci) {
-            const int c = ci ? cd.y : cd.x;
-            if (c < 0) break;
-            if (tk > c) continue;   // drawn: its drawer runs it
-            const int2 sc = a.sub[c];
-            const int w0 = a.wait_off[c], w1 = sc.x >= 0 ? sc.y : a.wait_off[c + 1];   // w1 - w0 <= 63
-            const int4 tc = a.tasks[c];
-            bool open = false;
-            if (w0 + lane < w1) {
-              const int2 cv = a.waits[w0 + lane];
-              open = ld_acquire_relaxed(a.counters + cv.x) < cv.y;
-            }
-            if (lane == 63 && tc.x == 2) open = ld_acquire_relaxed(applied + tc.w) < tc.z;
-            if (__builtin_amdgcn_ballot_w64(open) != 0) continue;
-            int got = -1;
-            if (lane == 0) {
-              if (atomicAdd(inflight, 1) < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0) got = c;
-              else atomicSub(inflight, 1);
-            }
-            got = __builtin_amdgcn_readfirstlane(got);
-            if (got >= 0) {
-              claim = got;
-              break;
-            }
-          }
-          if (lane == 0) sh[4] = claim;
-        }
-        __syncthreads();
-        next = sh[4];
-      }
-    }
     __builtin_amdgcn_s_setprio(0);
     if (a.trace && tid == 0) a.trace[8L * t + 2] = realtime();
   }
@@ -1485,7 +1369,7 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
   __shared__ int sh[2];
   if (*flag) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  int *done = counters, *ticket = counters + T;
+  int *ticket = counters + T;   // (counters[0..T) are unused: y entries are their own flags)
   const double *Xinv = Ld + (long)T * T64 * T64;
   const long kr = nR / T64;
   for (;;) {
@@ -1522,7 +1406,7 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
             mine = (unsigned long long)__double_as_longlong(yv) == kYSentinel;
           }
           if (__builtin_amdgcn_ballot_w64(mine) == 0) break;
-          __builtin_amdgcn_s_sleep(ARSLAM_BSOLVE_SLEEP);
+          __builtin_amdgcn_s_sleep(kBsolveSleep);
           if (++spins > kSpinCap || (((spins & 255) == 0) &&
                                      __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) != 0)) {
             if (lane == 0) atomicCAS(flag, 0, -(4000000 + b));
@@ -1644,9 +1528,9 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
     if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
   }
   DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
-            P.dag_maxdep, P.dag_claimed, P.dag_cand, P.dag_fold, P.dag_wait_off, P.dag_waits, P.dag_counters,
+            P.dag_maxdep, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
-            P.upd_part, P.upd_cnt, flag, std::getenv("ARSLAM_NO_CU_YIELD") ? 0 : 1, progress, trace};
+            P.upd_part, P.upd_cnt, flag, progress, trace};
   const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
 }

@@ -56,10 +56,7 @@ int peripheral(int start, const std::vector<std::vector<int>> &adj, const std::v
   return best;
 }
 
-double nd_beta() {   // (ARSLAM_ND_BETA: tuning knob, debug)
-  static const double b = std::getenv("ARSLAM_ND_BETA") ? std::atof(std::getenv("ARSLAM_ND_BETA")) : 0.6;
-  return b;
-}
+double nd_beta() { return 0.6; }
 
 // Elimination-tree height, in tile columns, of a dissection step: the
 // separator's tiles plus the larger child's height, which grows about as
@@ -229,8 +226,7 @@ struct Dissector {
     std::vector<std::pair<double, int>> pr(m);
     double best_score = -1;
     std::vector<int> best_side;
-    static const int n_dir = std::getenv("ARSLAM_ND_DIRS") ? std::atoi(std::getenv("ARSLAM_ND_DIRS")) : 6;
-    static const int n_q = std::getenv("ARSLAM_ND_QSTEPS") ? std::atoi(std::getenv("ARSLAM_ND_QSTEPS")) : 20;
+    constexpr int n_dir = 6, n_q = 20;
     for (int k = 0; k < n_dir; ++k) {
       // cut directions in the plane of the two principal axes
       const double ang = M_PI * k / n_dir, ca = std::cos(ang), sa = std::sin(ang);
@@ -676,7 +672,7 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
       for (int a = 0; a < 3; ++a) xyz[3L * t + a] = h.x0[3 + 6L * nc + 6L * t + a];
     // leaves of up to 32 tags (192 rows = 3 whole tiles): a smaller dissection
     // would not shorten the elimination tree, only add padding and parts
-    parts = nd_parts(nt, adj, std::getenv("ARSLAM_ND_LEAF") ? std::atoi(std::getenv("ARSLAM_ND_LEAF")) : 32, xyz);
+    parts = nd_parts(nt, adj, 32, xyz);
   } else {
     std::vector<int> order;
     if (ordering == 1 && nt > 1) order = rcm_order(nt, adj);

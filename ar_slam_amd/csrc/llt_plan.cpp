@@ -69,7 +69,6 @@ struct DagNode {
   std::vector<int2> waits;
   int sub = -1;
   std::vector<int2> late;
-  int fold = -1;   // TRSM: the update item folded into it
 };
 
 static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, long nt, const LltPlan &plan,
@@ -93,16 +92,13 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   std::vector<double> cost(n);
   std::vector<int> pr;
   // task costs (us): POTRF base, per folded column, fused TRSM; TRSM; update
-  // base, per column; INV (ARSLAM_SIM_COST="p,pk,ps,t,u,uk,i": debug sweeps).
-  // The update items are weighted well above their uncontended run time
-  // (4 + 4 per column): under the ~300 concurrent updates of the wide levels
-  // they run ~2-3x slower and hold the memory system the chain needs, and a
-  // schedule that budgets for that draws the chain tasks ahead of them
-  // (cfg3 k_factor_dag 720 -> ~688 us with 16 + 16 per column; flat from
-  // 12 + 12 to 20 + 12, worse at 24 + 24; tools/env_bench.sh sweeps).
-  double cc[7] = {16.0, 4.0, 5.0, 6.0, 16.0, 16.0, 5.0};
-  if (const char *e = std::getenv("ARSLAM_SIM_COST"))
-    std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf,%lf", &cc[0], &cc[1], &cc[2], &cc[3], &cc[4], &cc[5], &cc[6]);
+  // base, per column; INV.  The update items are weighted well above their
+  // uncontended run time (4 + 4 per column): under the ~300 concurrent updates
+  // of the wide levels they run ~2-3x slower and hold the memory system the
+  // chain needs, and a schedule that budgets for that draws the chain tasks
+  // ahead of them (cfg3 k_factor_dag 720 -> ~688 us with 16 + 16 per column;
+  // flat from 12 + 12 to 20 + 12, worse at 24 + 24; round-2 sweeps).
+  const double cc[7] = {16.0, 4.0, 5.0, 6.0, 16.0, 16.0, 5.0};
   for (int v = 0; v < n; ++v) {
     const DagNode &nd = nodes[v];
     pr.clear();
@@ -127,7 +123,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
       const int nk = nd.task.z >= 0 ? plan.h_items[nd.task.z].z - plan.h_items[nd.task.z].y : 0;
       cost[v] = cc[0] + cc[1] * nk + (nd.sub >= 0 ? cc[2] : 0.0);
     } else if (nd.task.x == 1) {
-      cost[v] = cc[3] + (nd.fold >= 0 ? cc[5] * (plan.h_items[nd.fold].z - plan.h_items[nd.fold].y) : 0.0);
+      cost[v] = cc[3];
     } else if (nd.task.x == 3) {
       cost[v] = cc[6];
     } else {
@@ -177,8 +173,7 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   int busy = 0;
   double now = 0.0;
   std::vector<double> through(blevel_out ? n : 0);
-  const char *sw = std::getenv("ARSLAM_SIM_WORKERS");   // (debug: list-schedule width)
-  const int sim_workers = sw ? std::max(1, std::atoi(sw)) : kSimWorkers;
+  const int sim_workers = kSimWorkers;
   while ((int)order.size() < n || !events.empty()) {
     while (busy < sim_workers && !heap.empty()) {
       std::pop_heap(heap.begin(), heap.end(), cmp);
@@ -324,61 +319,13 @@ void dag_build(LltPlan &plan) {
       if (!drop[m]) kept.push_back(std::move(nodes[m]));
     nodes.swap(kept);
   }
-  // Fold the last update of a TRSM's tile into the TRSM task when that update
-  // is one unsplit item, as for the diagonal: the task computes
-  // A_ik - sum_j L_ij L_kj^T itself before the solve (the same products in
-  // the same order as the item, so the result is unchanged bit for bit).  On
-  // a dense separator, row i's tiles form a chain TRSM(i,k-1) -> update of
-  // (i,k) -> TRSM(i,k); folding removes one task, one hand-off and one
-  // round trip of the tile per link.  Not for the parent-row tiles, which
-  // the next pass fuses into their column's POTRF.  Measured on cfg3: 717 ->
-  // 749 us with L_kk among the early waits (the fold's work then lands on the
-  // chain), 726 us with L_kk as a late wait after the fold's GEMMs; the
-  // folded tasks hold workgroups longer than the hand-offs they save.  Off
-  // unless ARSLAM_TRSM_FOLD is set.
-  if (std::getenv("ARSLAM_TRSM_FOLD")) {
-    std::vector<int> last_item(nt, -1), last_count(nt, 0);
-    for (size_t m = 0; m < nodes.size(); ++m) {
-      if (nodes[m].type != 2) continue;
-      const int tt = nodes[m].task.w, seq = nodes[m].task.z;
-      if (seq + 1 != n_apply[tt]) continue;
-      last_item[tt] = (int)m;
-      last_count[tt]++;
-    }
-    std::vector<char> drop(nodes.size(), 0);
-    for (auto &n : nodes) {
-      if (n.type != 1) continue;
-      const int i = n.task.y, k = n.task.z, tt = n.task.w;
-      int par = -1;
-      for (int r = k + 1; r < T && par < 0; ++r)
-        if (tid(r, k) >= 0) par = r;
-      if (i == par) continue;
-      const int m = last_item[tt];
-      if (m < 0 || last_count[tt] != 1 || plan.h_items[nodes[m].task.y].w >= 0) continue;
-      n.fold = nodes[m].task.y;
-      // early waits: the item's operands and the tile's earlier levels (the
-      // fold's GEMMs run while POTRF(k) is still factoring); late: L_kk
-      std::vector<int2> w;
-      for (const int2 &x : n.waits)
-        if (x.x != (int)nt + tt && x.x != tid(k, k)) w.push_back(x);
-      if (n_apply[tt] > 1) w.push_back(make_int2((int)nt + tt, n_apply[tt] - 1));
-      w.insert(w.end(), nodes[m].waits.begin(), nodes[m].waits.end());
-      n.waits = std::move(w);
-      n.late.assign(1, make_int2(tid(k, k), 1));
-      drop[m] = 1;
-    }
-    std::vector<Node> kept;
-    for (size_t m = 0; m < nodes.size(); ++m)
-      if (!drop[m]) kept.push_back(std::move(nodes[m]));
-    nodes.swap(kept);
-  }
   // Fuse the TRSM of each column's first off-diagonal tile (the elimination
   // tree parent's row) into the column's POTRF task: on a chain of
   // separator columns, POTRF(k) -> TRSM(parent, k) -> POTRF(parent) is the
   // critical path, and the fused task solves the tile against the L_kk it
   // still holds in LDS (no draw, no hand-off, no reload of L_kk).  The
   // TRSM's own waits become the task's late waits.
-  if (!std::getenv("ARSLAM_NO_TRSM_FUSION")) {   // (debug switch)
+  {
     std::vector<int> trsm_node(nt, -1);
     for (size_t m = 0; m < nodes.size(); ++m)
       if (nodes[m].type == 1) trsm_node[nodes[m].task.w] = (int)m;
@@ -414,16 +361,13 @@ void dag_build(LltPlan &plan) {
     n.waits.push_back(make_int2(tid(k, k), 1));
     nodes.push_back(std::move(n));
   }
-  std::vector<double> sim_finish(nodes.size(), 0.0), sim_blevel;   // (sim_blevel: start + bottom level)
-  std::vector<int> order = dag_list_schedule(nodes, nt, plan, &sim_finish, &sim_blevel);
+  std::vector<int> order = dag_list_schedule(nodes, nt, plan);
   plan.h_dag_tasks.clear();
   plan.h_dag_waits.clear();
   plan.h_dag_sub.clear();
-  plan.h_dag_fold.clear();
   plan.h_dag_wait_off.assign(1, 0);
   for (int o : order) {
     plan.h_dag_tasks.push_back(nodes[o].task);
-    plan.h_dag_fold.push_back(nodes[o].fold);
     plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].waits.begin(), nodes[o].waits.end());
     plan.h_dag_sub.push_back(make_int2(nodes[o].sub, (int)plan.h_dag_waits.size()));
     plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].late.begin(), nodes[o].late.end());
@@ -435,10 +379,8 @@ void dag_build(LltPlan &plan) {
   // 512 workgroups hold drawn tasks that wait (the factorization keeps ~30 %
   // of them busy), so in the contended first half of the factorization a
   // ready chain task used to be drawn 10-25 us after its last producer ended.
-  //  * POTRF(k) with fused TRSM (par, k) -> POTRF(par) (the solved tile stays
-  //    in LDS; the fold reuses it for column k's term);
-  //  * otherwise a task's designated successor is the earliest-ticketed task
-  //    whose latest-ticketed early producer it is.
+  // POTRF(k) with fused TRSM (par, k) -> POTRF(par) (the solved tile stays
+  // in LDS; the fold reuses it for column k's term).
   // maxdep[c] = the largest ticket among c's early producers other than its
   // claimers (>= 0 marks a target): a claim needs those drawn.  Late waits (a
   // POTRF's fused TRSM) are not counted, so a claimed target may wait on
@@ -479,13 +421,7 @@ void dag_build(LltPlan &plan) {
       std::sort(pr.begin(), pr.end());
       pr.erase(std::unique(pr.begin(), pr.end()), pr.end());
     }
-    const bool no_cont = std::getenv("ARSLAM_NO_CONT") != nullptr;   // (debug switches)
-    // (measured: the generic successor claims cost ~10 us on cfg3 -- the
-    // claimed successors are often not the ones the chain waits for, and the
-    // claiming workgroup idles on their other producers -- so they are off
-    // unless ARSLAM_GCONT is set)
-    const bool no_gcont = std::getenv("ARSLAM_GCONT") == nullptr;
-    for (long t = 0; t < n && !no_cont; ++t) {
+    for (long t = 0; t < n; ++t) {
       const int4 tk = plan.h_dag_tasks[t];
       const int sb = plan.h_dag_sub[t].x;
       if (tk.x != 0 || sb < 0) continue;
@@ -495,20 +431,11 @@ void dag_build(LltPlan &plan) {
       if (par < 0 || potrf_of[par] < 0 || potrf_of[par] <= t) continue;
       plan.h_dag_cont[t] = potrf_of[par];
     }
-    // every other task names as successor the task of the largest bottom
-    // level among those whose last producer (by the list schedule's finish
-    // estimate) it is
-    std::vector<int> best(n, -1);
-    for (long v = 0; v < n && !no_cont && !no_gcont; ++v) {
-      if (plan.h_dag_tasks[v].x == 3 || prod[v].empty()) continue;
-      int u = prod[v][0];
-      for (int p : prod[v])
-        if (sim_finish[order[p]] > sim_finish[order[u]]) u = p;
-      if (u >= v || plan.h_dag_cont[u] >= 0) continue;
-      if (best[u] < 0 || sim_blevel[order[v]] > sim_blevel[order[best[u]]]) best[u] = (int)v;
-    }
-    for (long u = 0; u < n; ++u)
-      if (best[u] >= 0) plan.h_dag_cont[u] = best[u];
+    // (generic successor claims -- every task claiming the successor it is the
+    // last producer of -- and ready claims of near-critical successors were
+    // measured slower in round 2 and removed: the claimed successors were
+    // often not the ones the chain waited for, and the extra polling cost more
+    // workgroup time than the late draws it saved)
     std::vector<std::vector<int>> claimers(n);
     for (long t = 0; t < n; ++t)
       if (plan.h_dag_cont[t] >= 0) claimers[plan.h_dag_cont[t]].push_back((int)t);
@@ -518,42 +445,6 @@ void dag_build(LltPlan &plan) {
       for (int u : prod[c])
         if (std::find(claimers[c].begin(), claimers[c].end(), u) == claimers[c].end()) md = std::max(md, u);
       plan.h_dag_maxdep[c] = md;
-    }
-    // Ready-claim candidates: each task's two successors of the largest
-    // bottom level.  The workgroup ending the task claims one that is not
-    // drawn yet when all of its waits are met right then (polled), so a chain
-    // task whose last input just landed runs at once instead of waiting for
-    // its ticket to come up (k_factor_dag).  Every candidate is a claim target
-    // (maxdep >= 0), so its drawer runs it only if nobody claimed it.
-    plan.h_dag_cand.assign(n, make_int2(-1, -1));
-    if (!no_cont && std::getenv("ARSLAM_RCLAIM")) {
-      // only successors on a near-critical path of the list schedule: polling
-      // at the end of every task cost more workgroup time than it saved
-      double span = 0.0;
-      for (double f : sim_finish) span = std::max(span, f);
-      const double crit = span * (std::getenv("ARSLAM_RCLAIM_FRAC") ? std::atof(std::getenv("ARSLAM_RCLAIM_FRAC")) : 0.9);
-      std::vector<std::vector<int>> succ(n);
-      for (long v = 0; v < n; ++v)
-        if (plan.h_dag_tasks[v].x != 3)
-          for (int u : prod[v])
-            if (u < v) succ[u].push_back((int)v);
-      for (long u = 0; u < n; ++u) {
-        std::vector<int> &sv = succ[u];
-        std::stable_sort(sv.begin(), sv.end(),
-                         [&](int a, int b) { return sim_blevel[order[a]] > sim_blevel[order[b]]; });
-        int2 c = make_int2(-1, -1);
-        for (int v : sv) {
-          if (v == plan.h_dag_cont[u]) continue;   // claimed by the POTRF rule already
-          if (sim_blevel[order[v]] < crit) continue;
-          const int early_end = plan.h_dag_sub[v].x >= 0 ? plan.h_dag_sub[v].y : plan.h_dag_wait_off[v + 1];
-          if (early_end - plan.h_dag_wait_off[v] > 63) continue;   // polled by one wavefront
-          if (c.x < 0) c.x = v;
-          else if (c.y < 0) c.y = v;
-        }
-        plan.h_dag_cand[u] = c;
-        if (c.x >= 0) plan.h_dag_maxdep[c.x] = std::max(plan.h_dag_maxdep[c.x], 0);
-        if (c.y >= 0) plan.h_dag_maxdep[c.y] = std::max(plan.h_dag_maxdep[c.y], 0);
-      }
     }
   }
   long n_potrf = 0, n_trsm = 0;
@@ -656,9 +547,7 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
       // split a long k-list into ~sqrt(m) chunks: chunk GEMMs run in parallel,
       // the last arriver reads ~sqrt(m) partial tiles
       const int m = (int)lks[t].size();
-      static const int split_min = std::getenv("ARSLAM_SPLIT_MIN") ? std::atoi(std::getenv("ARSLAM_SPLIT_MIN"))
-                                                                   : kSplitMin;   // (debug sweeps)
-      if (m > split_min) {
+      if (m > kSplitMin) {
         int nch = std::min(255, (int)std::ceil(std::sqrt((double)m)));
         const int ch = (m + nch - 1) / nch;
         nch = (m + ch - 1) / ch;
@@ -678,12 +567,6 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
     plan.h_item_off.push_back((int)items.size());
     plan.h_upd_off.push_back((int)targets.size());
     plan.h_upd_flops.push_back(fl);
-    if (std::getenv("ARSLAM_PLAN_STATS")) {
-      size_t mx = 0, tot = 0;
-      for (size_t t = 0; t < lt.size(); ++t) { mx = std::max(mx, lks[t].size()); tot += lks[t].size(); }
-      std::fprintf(stderr, "level %d: panel %d targets %zu ks %zu max_ks %zu\n", l,
-                   plan.h_panel_off[l + 1] - plan.h_panel_off[l], lt.size(), tot, mx);
-    }
     plan.total_upd_flops += fl;
   }
   // backward solve: levels from the root down; each column gathers from its
@@ -753,20 +636,6 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
       claimed[c] = 1;
       w.next = c;
       ++inflight;
-    }
-    if (w.next < 0 && !plan.h_dag_cand.empty()) {
-      for (int v : {plan.h_dag_cand[w.t].x, plan.h_dag_cand[w.t].y}) {
-        if (v < 0 || w.next >= 0 || ticket > v || claimed[v] || inflight >= n_workers / 2) continue;
-        const int ee = plan.h_dag_sub[v].x >= 0 ? plan.h_dag_sub[v].y : plan.h_dag_wait_off[v + 1];
-        bool met = true;
-        for (int q = plan.h_dag_wait_off[v]; q < ee && met; ++q) met = cnt[plan.h_dag_waits[q].x] >= plan.h_dag_waits[q].y;
-        const int4 tv = plan.h_dag_tasks[v];
-        if (tv.x == 2 && cnt[nt + tv.w] < tv.z) met = false;
-        if (!met) continue;
-        claimed[v] = 1;
-        w.next = v;
-        ++inflight;
-      }
     }
     if (w.cont) --inflight;
     w.phase = 0;
@@ -856,8 +725,6 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   addv(&plan.dag_sub, plan.h_dag_sub);
   addv(&plan.dag_cont, plan.h_dag_cont);
   addv(&plan.dag_maxdep, plan.h_dag_maxdep);
-  addv(&plan.dag_cand, plan.h_dag_cand);
-  addv(&plan.dag_fold, plan.h_dag_fold);
   add(reinterpret_cast<void **>(&plan.dag_claimed), nullptr, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int));
   add(reinterpret_cast<void **>(&plan.dag_counters), nullptr, (2 * (size_t)plan.n_tiles + 2 + kCuFlags) * sizeof(int));
   size_t total = 0, staged = 0;

@@ -139,15 +139,6 @@ struct LltPlan {
   // dag_claimed[t]: taken by the predecessor's workgroup or by the drawer
   int *dag_cont = nullptr, *dag_maxdep = nullptr, *dag_claimed = nullptr;
   std::vector<int> h_dag_cont, h_dag_maxdep;
-  // dag_cand[t]: up to two successors of task t (largest bottom level first)
-  // that t's workgroup claims when they are not drawn yet and their waits are
-  // all met at the moment t ends (-1: none)
-  int2 *dag_cand = nullptr;
-  std::vector<int2> h_dag_cand;
-  // dag_fold[t]: for a TRSM task, the update item it applies to its tile
-  // before the solve (the tile's last level), else -1
-  int *dag_fold = nullptr;
-  std::vector<int> h_dag_fold;
   int *dag_wait_off = nullptr;
   // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags])
   int2 *dag_waits = nullptr;

@@ -313,6 +313,17 @@ struct arslam_lm {
   }
   void solve(arslam_lm_summary *s);
   void write_back(const double *d_src);
+  // the pointer-keyed solve in progress: its (unswapped) staging problem, whose
+  // arrays soa aliases; write_back also scatters them into the caller's blocks
+  const arslam_soa_problem *pk_stage = nullptr;
+  void scatter_to_blocks();
+  // arslam_lm_debug_break_dependency: the patched wait entry, restored after the next solve
+  int dbg_patched_wait = -1;
+  void restore_patched_wait();
+  // multi-rank: does any rank have an iteration callback (agreed once per solve)
+  bool any_iter_cb = false;
+  DevBuf<double> d_cb;
+  int agree_callback(int r);
 };
 
 namespace {
@@ -577,6 +588,39 @@ void arslam_lm::write_back(const double *d_src) {
   std::memcpy(soa.camera, h, 3 * sizeof(double));
   if (nc) std::memcpy(soa.cap, h + 3, 6L * nc * sizeof(double));
   if (nt) std::memcpy(soa.tag, h + 3 + 6L * nc, 6L * nt * sizeof(double));
+  if (pk_stage) scatter_to_blocks();
+}
+
+// Pointer-keyed path: the staging arrays (which soa aliases, role-swapped or
+// not) -> the caller's parameter blocks, as Ceres writes the user's blocks.
+void arslam_lm::scatter_to_blocks() {
+  const arslam_soa_problem &p = *pk_stage;
+  std::memcpy(camera_ptr, p.camera, 3 * sizeof(double));
+  for (size_t c = 0; c < cap_ptrs.size(); ++c) std::memcpy(cap_ptrs[c], p.cap + 6 * c, 6 * sizeof(double));
+  for (size_t t = 0; t < tag_ptrs.size(); ++t) std::memcpy(tag_ptrs[t], p.tag + 6 * t, 6 * sizeof(double));
+}
+
+void arslam_lm::restore_patched_wait() {
+  if (dbg_patched_wait < 0) return;
+  const int w = dbg_patched_wait;
+  dbg_patched_wait = -1;
+  plan.h_dag_waits[w].y -= 1 << 28;
+  HIP_CHECK(hipMemcpyAsync(plan.dag_waits + w, &plan.h_dag_waits[w], sizeof(int2), hipMemcpyHostToDevice, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+// Several ranks: every rank takes the same branch on the callbacks' answers
+// (MAX over the ranks of continue 0 < terminate successfully 1 < abort 2).
+int arslam_lm::agree_callback(int r) {
+  if (nranks <= 1) return r;
+  const double v = r == ARSLAM_SOLVER_ABORT ? 2.0 : r == ARSLAM_SOLVER_TERMINATE_SUCCESSFULLY ? 1.0 : 0.0;
+  d_cb.alloc(1);
+  HIP_CHECK(hipMemcpyAsync(d_cb.p, &v, sizeof(double), hipMemcpyHostToDevice, stream));
+  allreduce(d_cb.p, 1, ARSLAM_OP_MAX);
+  double m = 0.0;
+  HIP_CHECK(hipMemcpyAsync(&m, d_cb.p, sizeof(double), hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  return m >= 2.0 ? ARSLAM_SOLVER_ABORT : m >= 1.0 ? ARSLAM_SOLVER_TERMINATE_SUCCESSFULLY : ARSLAM_SOLVER_CONTINUE;
 }
 
 namespace {
@@ -615,6 +659,25 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   HIP_CHECK(hipMemcpyAsync(d_xbest.p, d_x0.p, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
   const bool root = rank == 0;
   if (o.minimizer_progress_to_stdout && root) print_header();
+  // the patched dependency of arslam_lm_debug_break_dependency lasts one solve
+  struct RestoreWait {
+    arslam_lm *h;
+    ~RestoreWait() {
+      try { h->restore_patched_wait(); } catch (...) {}
+    }
+  } restore_wait{this};
+  any_iter_cb = iter_cb != nullptr;
+  if (nranks > 1) {   // a callback on any rank: every rank joins the per-iteration agreement
+    const double mine = iter_cb ? 1.0 : 0.0;
+    d_cb.alloc(1);
+    HIP_CHECK(hipMemcpyAsync(d_cb.p, &mine, sizeof(double), hipMemcpyHostToDevice, stream));
+    allreduce(d_cb.p, 1, ARSLAM_OP_MAX);
+    double m = 0.0;
+    HIP_CHECK(hipMemcpyAsync(&m, d_cb.p, sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    any_iter_cb = m > 0.0;
+    comm_bytes = 0.0;   // (the per-step exchange count starts here)
+  }
 
   // ---- iteration 0 ----
   double x_cost, fixed_cost, gmax, gnorm, x_norm;
@@ -676,8 +739,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     t_iter = tn;
     if (s->n_iters <= ARSLAM_LM_MAX_ITERS) s->iters[s->n_iters++] = it;
     if (o.minimizer_progress_to_stdout && root) print_row(it);
-    if (iter_cb) {   // Ceres RunCallbacks: after the record, before the stop rules
-      const int r = iter_cb(iter_cb_ctx, &it);
+    if (iter_cb || any_iter_cb) {   // Ceres RunCallbacks: after the record, before the stop rules
+      const int r = agree_callback(iter_cb ? iter_cb(iter_cb_ctx, &it) : ARSLAM_SOLVER_CONTINUE);
       if (r == ARSLAM_SOLVER_ABORT) {
         s->termination = ARSLAM_USER_FAILURE; s->rule = ARSLAM_RULE_USER_CALLBACK; return true;
       }
@@ -729,9 +792,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       // one rank: the gather writes the final S (D_f^2 and the padding rows
       // included); several: S is summed over the ranks first.  k_schur's extra
       // blocks clear S's tiles first.
-      static const bool memset_s = std::getenv("ARSLAM_MEMSET_S") != nullptr;   // (A/B switch)
-      if (memset_s) arslam::launch_zero_tiles(plan, d_S.p, stream);
-      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1, memset_s ? 0 : plan.n_tiles);
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1, plan.n_tiles);
       if (nranks > 1) {
         allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ARSLAM_OP_SUM);
         arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
@@ -810,12 +871,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     timers[PH_BACK].start(stream);
     // (k_update_f writes every f-side slot of xc, k_backsub every capture
     // slot, then evaluates the candidate's cost per capture: k_cost fused)
-    static const bool split_cost = std::getenv("ARSLAM_SPLIT_COST") != nullptr;   // (A/B switch)
     arslam::launch_update_f(P, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
-    arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream, has_f, !split_cost);
+    arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream, has_f, true);
     timers[PH_BACK].stop(stream);
     timers[PH_COST].start(stream);
-    if (split_cost) arslam::launch_cost(P, xc, d_parts.p, stream);
     arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p);
     if (nranks > 1) {
       // model change, capture step^2, candidate cost, fixed; flags by max
@@ -846,8 +905,9 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     const double model_cost_change = red[arslam::P_MODEL];
     const bool valid = !lin_fail && !ybad && model_cost_change > 0.0;
     if (!valid) {
-      ++n_invalid;
-      if (n_invalid > o.max_num_consecutive_invalid_steps) {
+      // Ceres 2.0 HandleInvalidStep: ++num_consecutive_invalid_steps_ >= max -> FAILURE
+      // (the 5th consecutive invalid step at the default 5, not recorded)
+      if (++n_invalid >= o.max_num_consecutive_invalid_steps) {
         s->termination = ARSLAM_FAILURE; s->rule = ARSLAM_RULE_INVALID_STEPS; break;
       }
       radius = radius / decrease_factor;   // StepIsInvalid
@@ -1108,6 +1168,10 @@ int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
     p.corners = h->pk_corners.data();
     p.camera_const = h->constant.count(h->camera_ptr) ? 1 : 0;
     p.cap_const = cc.data(); p.tag_const = tc.data();
+    struct StageGuard {   // (the staging arrays go out of scope; the device problem stays)
+      arslam_lm *h;
+      ~StageGuard() { h->pk_stage = nullptr; h->soa = arslam_soa_problem{}; h->reuse_order = false; }
+    } stage_guard{h};
     if (h->loaded && h->pk_loaded && !h->pk_dirty) {
       h->reload_values(&p);   // same problem, new values: no host rebuild, no re-upload of observations
     } else {
@@ -1117,12 +1181,10 @@ int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
       h->pk_loaded = true;
       h->pk_dirty = false;
     }
+    h->pk_stage = &p;
+    // the final write_back also writes the caller's blocks (Ceres writes parameters back;
+    // every iteration under update_state_every_iteration)
     h->solve(summary);
-    // write the final state into the caller's blocks (Ceres writes parameters back)
-    std::memcpy(h->camera_ptr, cam.data(), 3 * sizeof(double));
-    for (int c = 0; c < nc; ++c) std::memcpy(h->cap_ptrs[c], &cap[6L * c], 6 * sizeof(double));
-    for (int t = 0; t < nt; ++t) std::memcpy(h->tag_ptrs[t], &tag[6L * t], 6 * sizeof(double));
-    h->soa = arslam_soa_problem{};   // (the arrays above go out of scope; the device problem stays)
   });
 }
 
@@ -1146,6 +1208,8 @@ int arslam_lm_load_soa(arslam_lm *h, const arslam_soa_problem *p) {
   return guarded([&] {
     h->pk_loaded = false;
     h->pk_dirty = true;
+    h->reuse_order = false;   // a bulk load never reuses a pointer-keyed problem's order
+    h->prev_tag_row.clear();
     h->load(p);
   });
 }
@@ -1243,7 +1307,9 @@ int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken) {
     while (t < pl.n_dag_tasks && pl.h_dag_wait_off[t] == pl.h_dag_wait_off[t + 1]) ++t;
     fail_if(t >= pl.n_dag_tasks, ARSLAM_E_INVALID_ARG, "no task at or after this ticket waits on anything");
     const int w = pl.h_dag_wait_off[t];
-    pl.h_dag_waits[w].y += 1 << 28;   // a count no task ever reaches
+    h->restore_patched_wait();
+    pl.h_dag_waits[w].y += 1 << 28;   // a count no task ever reaches (for the next solve only)
+    h->dbg_patched_wait = w;
     HIP_CHECK(hipMemcpyAsync(pl.dag_waits + w, &pl.h_dag_waits[w], sizeof(int2), hipMemcpyHostToDevice,
                              h->stream));
     HIP_CHECK(hipStreamSynchronize(h->stream));

@@ -414,7 +414,8 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
         valid = model > 0.0;
       }
       if (!valid) {
-        if (++n_invalid > p.max_invalid) { res.status = ARSLAM_FAILURE; res.rule = ARSLAM_RULE_INVALID_STEPS; break; }
+        // Ceres 2.0 HandleInvalidStep: ++num_consecutive_invalid_steps_ >= max -> FAILURE
+        if (++n_invalid >= p.max_invalid) { res.status = ARSLAM_FAILURE; res.rule = ARSLAM_RULE_INVALID_STEPS; break; }
         radius = radius / decrease;
         decrease *= 2.0;
         succ = false;

@@ -313,38 +313,34 @@ std::optional<CaptureHandle> ArSlamSolver::addDetections(const Detections &d) { 
     rect.corners = det.corners;
     addBlock(rect, capture.handle, aruco.handle);
   }
-  unsolved_captures_.push_back(capture.handle.idx);
+  unsolved_captures_.insert(capture.handle);
   return capture.handle;
 }
 
 void ArSlamSolver::solveIncremental() {   // :629-678
-  // The reference keeps unsolved captures in an unordered_set<CaptureHandle>
-  // (hash = index), so its visiting order is the standard library's bucket
-  // order; this mirror visits them in ascending capture index (deterministic).
-  std::sort(unsolved_captures_.begin(), unsolved_captures_.end());
+  // make sure at least one capture is solved: the seed is the set's begin()
+  // (libstdc++ bucket order, as in the reference)
   if (!unsolved_captures_.empty() && unsolved_captures_.size() == captures_.size()) {
-    const unsigned idx = unsolved_captures_.front();
-    unsolved_captures_.erase(unsolved_captures_.begin());
-    solveCapture(captures_[idx], std::nullopt);
+    const CaptureHandle ch = *unsolved_captures_.begin();
+    unsolved_captures_.erase(ch);
+    solveCapture(at(ch), std::nullopt);
   }
   bool repeat_solve;
   do {
     repeat_solve = false;
-    for (size_t i = 0; i < unsolved_captures_.size(); ++i) {
-      Capture &capture = captures_[unsolved_captures_[i]];
-      bool erased = false;
+    for (auto itr = unsolved_captures_.begin(); itr != unsolved_captures_.end(); ++itr) {
+      Capture &capture = at(*itr);
       for (BlockHandle bh : capture.blocks) {
         if (at(at(bh).aruco).initialized) {
           repeat_solve = true;
-          unsolved_captures_.erase(unsolved_captures_.begin() + i);   // itr = erase(itr)
-          erased = true;
+          itr = unsolved_captures_.erase(itr);
           solveCapture(capture, bh);
           break;
         }
       }
-      // as in the reference, the element after an erased one is skipped by the
-      // loop increment (it is revisited on the next pass)
-      if (erased && i >= unsolved_captures_.size()) break;
+      // as in the reference, the element after an erased one is skipped by
+      // the loop increment (it is revisited on the next pass)
+      if (itr == unsolved_captures_.end()) break;
     }
   } while (repeat_solve);
 }
@@ -473,6 +469,7 @@ void ArSlamSolver::optimize(const Capture &capture) {   // :1001-1018
   check(arslam_lm_set_options(problem_, &o));
   SolveRecord rec;
   rec.capture_uid = capture.uid;
+  rec.capture_idx = capture.handle.idx;
   check(arslam_lm_solve(problem_, &rec.summary));
   solve_log_.push_back(rec);
 }

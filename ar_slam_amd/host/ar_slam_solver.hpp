@@ -22,6 +22,7 @@
 #include <ostream>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace arslam {
@@ -47,7 +48,13 @@ struct PoseParams {   // :81-94 -- translation then angle-axis
   std::array<double, 6> params{0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 };
 
-struct CaptureHandle { unsigned idx = ~0u; };
+struct CaptureHandle {
+  unsigned idx = ~0u;
+  bool operator==(const CaptureHandle &o) const { return idx == o.idx; }
+};
+struct CaptureHandleHash {   // std::hash<CaptureHandle>, ar_slam_util.hpp:140-145
+  size_t operator()(const CaptureHandle &h) const { return h.idx; }
+};
 struct ArucoHandle { unsigned idx = ~0u; };
 struct BlockHandle { unsigned idx = ~0u; };
 
@@ -116,6 +123,7 @@ struct CameraInfo {
 // Ceres summary of the last optimize() (the reference prints progress only)
 struct SolveRecord {
   std::string capture_uid;
+  unsigned capture_idx = ~0u;
   arslam_lm_summary summary;
 };
 
@@ -156,6 +164,7 @@ class ArSlamSolver {
   std::optional<CaptureHandle> findCapture(const std::string &uid) const;
   std::optional<ArucoHandle> findAruco(const std::string &id) const;
   const std::vector<SolveRecord> &solveLog() const { return solve_log_; }
+  const std::unordered_set<CaptureHandle, CaptureHandleHash> &unsolvedCaptures() const { return unsolved_captures_; }
   void setVerbose(bool v) { verbose_ = v; }
 
   // data-store builders (protected in the reference; public here so a host
@@ -181,7 +190,9 @@ class ArSlamSolver {
   std::vector<Block> blocks_;
   std::unordered_map<std::string, unsigned> capture_map_;
   std::unordered_map<std::string, unsigned> aruco_map_;
-  std::vector<unsigned> unsolved_captures_;   // ascending handle order (see solveIncremental)
+  // the reference's container and hash (ar_slam_util.hpp:140-145, 492): solveIncremental
+  // visits the unsolved captures in its iteration (bucket) order
+  std::unordered_set<CaptureHandle, CaptureHandleHash> unsolved_captures_;
   std::vector<SolveRecord> solve_log_;
   bool verbose_ = false;
 };

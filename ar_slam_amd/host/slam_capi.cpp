@@ -136,6 +136,23 @@ int arslam_slam_solve_summary(const arslam_slam *h, int i, arslam_lm_summary *s)
   return ARSLAM_OK;
 }
 
+int arslam_slam_solve_capture(const arslam_slam *h, int i, int *capture_idx) {
+  if (!h || !capture_idx || i < 0 || i >= (int)h->s.solveLog().size()) return ARSLAM_E_INVALID_ARG;
+  *capture_idx = (int)h->s.solveLog()[i].capture_idx;
+  return ARSLAM_OK;
+}
+
+int arslam_slam_unsolved_captures(const arslam_slam *h, int *out, int cap, int *n) {
+  if (!h || !n || (cap > 0 && !out)) return ARSLAM_E_INVALID_ARG;
+  int k = 0;
+  for (const arslam::CaptureHandle &ch : h->s.unsolvedCaptures()) {
+    if (k < cap) out[k] = (int)ch.idx;
+    ++k;
+  }
+  *n = k;
+  return ARSLAM_OK;
+}
+
 int arslam_slam_capture(const arslam_slam *h, int c, char *uid, int cap, double inv_pose[6]) {
   if (!h || c < 0 || c >= (int)h->s.numCaptures()) return ARSLAM_E_INVALID_ARG;
   const arslam::Capture &cp = h->s.at(arslam::CaptureHandle{(unsigned)c});

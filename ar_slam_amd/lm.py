@@ -55,7 +55,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_slam_solve", "arslam_slam_solve_incremental", "arslam_slam_localize_many",
            "arslam_slam_num_captures", "arslam_slam_num_arucos", "arslam_slam_num_blocks",
            "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_solve_summary",
-           "arslam_slam_capture", "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
+           "arslam_slam_solve_capture", "arslam_slam_unsolved_captures", "arslam_slam_capture", "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
            "arslam_slam_block", "arslam_slam_camera", "arslam_slam_set_camera",
            "arslam_slam_get_transforms", "arslam_slam_camera_info"]
 
@@ -166,7 +166,7 @@ def lib():
                "arslam_slam_solve", "arslam_slam_solve_incremental", "arslam_slam_localize_many",
                "arslam_slam_num_captures", "arslam_slam_num_arucos", "arslam_slam_num_blocks",
                "arslam_slam_num_solves", "arslam_slam_last_summary", "arslam_slam_solve_summary",
-               "arslam_slam_capture",
+               "arslam_slam_solve_capture", "arslam_slam_unsolved_captures", "arslam_slam_capture",
                "arslam_slam_set_capture_pose", "arslam_slam_aruco", "arslam_slam_set_aruco_pose",
                "arslam_slam_block", "arslam_slam_camera", "arslam_slam_set_camera",
                "arslam_slam_get_transforms", "arslam_slam_camera_info"):
@@ -651,6 +651,23 @@ class SlamSolver:
         s = Summary()
         _check(lib().arslam_slam_solve_summary(self._h, C.c_int(i), C.byref(s)))
         return s.to_dict()
+
+    def solve_capture(self, i):
+        """Index of the capture whose optimize() was call i (the drivers' visiting order)."""
+        c = C.c_int(-1)
+        _check(lib().arslam_slam_solve_capture(self._h, C.c_int(i), C.byref(c)))
+        return c.value
+
+    def solve_order(self):
+        return [self.solve_capture(i) for i in range(self.num_solves)]
+
+    def unsolved_captures(self):
+        """The unsolved-capture set in its iteration order (begin() first)."""
+        n = C.c_int(0)
+        _check(lib().arslam_slam_unsolved_captures(self._h, None, C.c_int(0), C.byref(n)))
+        out = (C.c_int * max(n.value, 1))()
+        _check(lib().arslam_slam_unsolved_captures(self._h, out, C.c_int(n.value), C.byref(n)))
+        return [int(out[i]) for i in range(n.value)]
 
     def capture(self, c):
         buf = C.create_string_buffer(256)

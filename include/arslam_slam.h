@@ -58,6 +58,13 @@ int arslam_slam_last_summary(const arslam_slam *h, arslam_lm_summary *s);
 /* the summary of optimize() call i (0 <= i < arslam_slam_num_solves) */
 int arslam_slam_solve_summary(const arslam_slam *h, int i, arslam_lm_summary *s);
 
+/* the capture whose optimize() was call i (the visiting order of solve /
+ * solveIncremental) */
+int arslam_slam_solve_capture(const arslam_slam *h, int i, int *capture_idx);
+/* the unsolved captures (std::unordered_set<CaptureHandle>, ar_slam_util.hpp:492)
+ * in the set's iteration order, begin() first; *n = count (writes <= cap) */
+int arslam_slam_unsolved_captures(const arslam_slam *h, int *out, int cap, int *n);
+
 /* capture c: uid (copied, NUL-terminated, truncated to cap), inv_pose[6] */
 int arslam_slam_capture(const arslam_slam *h, int c, char *uid, int cap, double inv_pose[6]);
 int arslam_slam_set_capture_pose(arslam_slam *h, int c, const double inv_pose[6]);

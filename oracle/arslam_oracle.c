@@ -843,8 +843,13 @@ int or_solve(or_problem *p, const or_options *o, or_summary *s, const or_comm *c
       }
     }
     if (!valid) {
-      ++n_invalid;
-      if (n_invalid > o->max_num_consecutive_invalid_steps) {
+      /* Ceres 2.0 TrustRegionMinimizer::HandleInvalidStep (trust_region_minimizer.cc):
+       *   if (++num_consecutive_invalid_steps_ >= options_.max_num_consecutive_invalid_steps)
+       *     { termination_type = FAILURE; return false; }
+       * i.e. the 5th consecutive invalid step (default 5) ends the solve, unrecorded
+       * (its message reads "more than", the test is >=).  Restated from the upstream
+       * source as recalled (Ceres is not in this image); round 2 had `>` here. */
+      if (++n_invalid >= o->max_num_consecutive_invalid_steps) {
         s->termination = OR_FAILURE; s->rule = OR_RULE_INVALID_STEPS; break;
       }
       radius = radius / decrease_factor;   /* StepIsInvalid == StepRejected */

@@ -8,15 +8,64 @@ optimizer:
   * the initialisers initCapturePose / initArPose            :98-128
 The problem grows exactly as ceres::Problem does in the reference: every
 optimize() solves all residual blocks added so far, parameter blocks in
-first-use order.  Unsolved captures are visited in ascending index (the
-reference's unordered_set order is the standard library's), as the C++
-mirror does.  Used only by tests/ to check ar_slam_amd/host against it.
+first-use order.  Unsolved captures live in the reference's own container,
+std::unordered_set<CaptureHandle> with hash = index (ar_slam_util.hpp:140-145,
+492; oracle/stl_uset.cpp), so solveIncremental visits them in libstdc++'s
+bucket order and seeds with its begin() (ar_slam_util.cpp:643, 657-676), as
+the C++ mirror does.  Used only by tests/ to check ar_slam_amd/host against it.
 """
 from __future__ import annotations
+
+import ctypes as C
+import os
 
 import numpy as np
 
 from . import oracle as O
+
+_STL = None
+
+
+def _stl():
+    global _STL
+    if _STL is None:
+        O.build()
+        L = C.CDLL(os.path.join(O.HERE, "liboracle_stl.so"))
+        L.or_uset_new.restype = C.c_void_p
+        L.or_uset_free.argtypes = [C.c_void_p]
+        L.or_uset_insert.argtypes = [C.c_void_p, C.c_uint]
+        L.or_uset_erase.argtypes = [C.c_void_p, C.c_uint]
+        L.or_uset_size.argtypes = [C.c_void_p]
+        L.or_uset_list.argtypes = [C.c_void_p, C.POINTER(C.c_uint)]
+        _STL = L
+    return _STL
+
+
+class UnorderedHandleSet:
+    """std::unordered_set<CaptureHandle> (ar_slam_util.hpp:492), through oracle/stl_uset.cpp."""
+
+    def __init__(self):
+        self._L = _stl()
+        self._h = self._L.or_uset_new()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.or_uset_free(self._h)
+
+    def insert(self, idx):
+        self._L.or_uset_insert(self._h, idx)
+
+    def erase(self, idx):
+        return self._L.or_uset_erase(self._h, idx)
+
+    def __len__(self):
+        return self._L.or_uset_size(self._h)
+
+    def items(self):
+        """The elements in iteration order, begin() first."""
+        out = (C.c_uint * max(len(self), 1))()
+        n = self._L.or_uset_list(self._h, out)
+        return [int(out[i]) for i in range(n)]
 
 
 class OracleSlam:
@@ -26,9 +75,10 @@ class OracleSlam:
         self.arucos = []      # dict(id, blocks, initialized, pose)
         self.blocks = []      # dict(rect, cap, ar, added)
         self.aruco_map = {}
-        self.unsolved = []
+        self.unsolved = UnorderedHandleSet()
         self.opts = opts
         self.order = []       # added blocks, in AddResidualBlock order
+        self.solve_order = []  # the capture of each optimize() call
         self.n_solves = 0
 
     def add_detections(self, uid, ids, corners):
@@ -43,7 +93,7 @@ class OracleSlam:
             self.blocks.append(dict(rect=np.asarray(corners[i], np.float64), cap=c, ar=a, added=False))
             self.captures[c]["blocks"].append(b)
             self.arucos[a]["blocks"].append(b)
-        self.unsolved.append(c)
+        self.unsolved.insert(c)
         return c
 
     # ---- problem ----
@@ -58,6 +108,7 @@ class OracleSlam:
             assert not blk["added"], "block for capture was somehow already added?"
             blk["added"] = True
             self.order.append(b)
+        self.solve_order.append(c)
 
     def _optimize(self):
         caps, tags = [], []
@@ -111,18 +162,21 @@ class OracleSlam:
                         self.captures[cc]["init_block"] = b
                         open_.append(cc)
 
-    def solve_incremental(self):
-        self.unsolved.sort()
-        if self.unsolved and len(self.unsolved) == len(self.captures):
-            c = self.unsolved.pop(0)
+    def solve_incremental(self):   # ar_slam_util.cpp:629-678
+        if len(self.unsolved) and len(self.unsolved) == len(self.captures):
+            c = self.unsolved.items()[0]      # *unsolved_captures_.begin()
+            self.unsolved.erase(c)
             self._add_blocks(c)
             self._optimize()
         repeat = True
         while repeat:
             repeat = False
+            # the set's iteration order; nothing is inserted during the loop, so
+            # an erase only removes the element (the rest keep their order)
+            order = self.unsolved.items()
             i = 0
-            while i < len(self.unsolved):
-                c = self.unsolved[i]
+            while i < len(order):
+                c = order[i]
                 hit = None
                 for b in self.captures[c]["blocks"]:
                     if self.arucos[self.blocks[b]["ar"]]["initialized"]:
@@ -130,10 +184,11 @@ class OracleSlam:
                         break
                 if hit is not None:
                     repeat = True
-                    self.unsolved.pop(i)
+                    self.unsolved.erase(c)     # itr = unsolved_captures_.erase(itr)
+                    order.pop(i)
                     self._init_capture(c, hit)
                     self._add_blocks(c)
                     self._optimize()
-                    if i >= len(self.unsolved):
+                    if i >= len(order):        # itr == end()
                         break
-                i += 1   # after an erase this skips the next element, as the reference's loop does
+                i += 1   # ++itr: after an erase this skips the next element, as the reference's loop does

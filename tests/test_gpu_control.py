@@ -15,10 +15,14 @@ Tolerances (fp64; the device sums in another order than the oracle):
     iteration to 20x the distance between the oracle's own Schur trace and
     its full-normal-equation trace (two exact arithmetics of the same step,
     committed as alt_* in the fixture) where the trajectory itself amplifies
-    rounding: a rejected candidate far from the optimum (tiny_reject's
-    iteration 2 at cost 5.9e11 differs by 1e-7 between the two), or a
-    radius set by a rho whose cost change is at the rounding level
-    (medium_gradient's last radius differs by 60% between the two);
+    rounding (tiny_reject's iteration 2, a rejected candidate at cost 5.9e11,
+    differs by 1.4e-7 between the two: tolerance 2.8e-6), and never wider
+    than 1e-3;
+  * one entry is exempt from the value comparison (UNCONSTRAINED, each with
+    its reason): medium_gradient's last radius, set by a rho whose cost
+    change is at the rounding level of the cost (the two exact arithmetics
+    differ by 55%).  For it the device's radius must follow from the
+    device's own rho by Ceres' update rule, to 1e-12;
   * final cost 1e-8, focal 1e-8 relative.
 
 Also here: the executor-fault path (a broken task-graph dependency must be
@@ -41,15 +45,29 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CONTROL = sorted(os.path.basename(p)[7:-5] for p in glob.glob(os.path.join(GOLDEN, "lm_ctl_*.json")))
 EPS = np.finfo(np.float64).eps
 SENSITIVITY_FACTOR = 20.0
+MAX_TOLERANCE = 1e-3
+# (trace, key, iteration) -> why the value itself is not constrained
+UNCONSTRAINED = {
+    ("medium_gradient", "trust_region_radius", 7):
+        "accepted step whose cost change (~1e-13 relative) is at the cost's rounding level: rho, and "
+        "with it radius / max(1/3, 1 - (2 rho - 1)^3), differs by 55% between the oracle's Schur and "
+        "full-normal-equation arithmetics; checked through the update rule instead",
+}
 
 
 def _tolerance(ref, alt):
     """Per-iteration relative tolerance: 1e-9, or SENSITIVITY_FACTOR times the distance between
     the oracle's Schur trace and its full-normal-equation trace (two exact arithmetics of the
-    same Ceres step) where that trajectory amplifies rounding more -- e.g. a rejected
-    candidate far from the optimum, or a radius set by a rho computed from a cost change at
-    the rounding level."""
-    return np.maximum(1e-9, SENSITIVITY_FACTOR * np.abs(alt - ref) / np.abs(ref))
+    same Ceres step) where that trajectory amplifies rounding more (a rejected candidate far
+    from the optimum), capped at MAX_TOLERANCE."""
+    return np.minimum(MAX_TOLERANCE, np.maximum(1e-9, SENSITIVITY_FACTOR * np.abs(alt - ref) / np.abs(ref)))
+
+
+def _radius_from_rule(its, i, max_radius=1e16):
+    """Ceres' LM radius after a successful step i, from the device's own rho
+    (LevenbergMarquardtStrategy::StepAccepted)."""
+    q = 2.0 * its[i]["relative_decrease"] - 1.0
+    return min(max_radius, its[i - 1]["trust_region_radius"] / max(1.0 / 3.0, 1.0 - q * q * q))
 
 
 def _solve_control(lm, gold):
@@ -77,10 +95,19 @@ def test_control_trace_matches_oracle(lm, name):
     for key in ("cost", "trust_region_radius"):
         ours = np.array([it[key] for it in its])
         ref = np.array(gold[key])
+        alt = np.array(gold["alt_" + key])
         d = np.abs(ours - ref) / np.abs(ref)
-        tol = _tolerance(ref, np.array(gold["alt_" + key]))
-        print(f"{name} {key}: max rel diff {d.max():.1e}, max allowed {tol.max():.1e}")
-        assert np.all(d <= tol), (key, d, tol)
+        tol = _tolerance(ref, alt)
+        free = np.array([(name, key, i) in UNCONSTRAINED for i in range(len(ref))])
+        # every entry the sensitivity rule would open past the cap is listed, with its reason
+        wide = SENSITIVITY_FACTOR * np.abs(alt - ref) / np.abs(ref) > MAX_TOLERANCE
+        assert np.array_equal(wide, free), (key, np.where(wide)[0], np.where(free)[0])
+        print(f"{name} {key}: max rel diff {d[~free].max():.1e}, max allowed {tol[~free].max():.1e}")
+        assert np.all(d[~free] <= tol[~free]), (key, d, tol)
+        for i in np.where(free)[0]:
+            assert key == "trust_region_radius" and its[i]["step_is_successful"]
+            want = _radius_from_rule(its, i)
+            assert abs(ours[i] - want) <= 1e-12 * want, (i, ours[i], want)
     assert abs(s["final_cost"] - gold["final_cost"]) <= 1e-8 * gold["final_cost"]
     assert abs(cam[0] - gold["final_focal"]) <= 1e-8 * gold["final_focal"]
 
@@ -112,6 +139,29 @@ def test_iteration_callback(lm):
     assert rp.solve()["termination"] == "CONVERGENCE"
 
 
+def test_pointer_keyed_blocks_are_written_back_every_iteration(lm):
+    """update_state_every_iteration on the pointer-keyed Problem (the path ArSlamSolver uses):
+    the callback sees the caller's own parameter blocks already updated, as Ceres writes the
+    user's blocks after every accepted step (ar_slam_util.cpp:1006-1009), under both
+    elimination sides (tag elimination solves the role-swapped problem)."""
+    g = synth.config_graph("small")
+    for side in (lm.ELIM_CAPTURES, lm.ELIM_TAGS):
+        cam = g.camera.copy()
+        caps = [g.cap[c].copy() for c in range(g.n_cap)]
+        tags = [g.tag[t].copy() for t in range(g.n_tag)]
+        pr = lm.Problem(update_state_every_iteration=1, elimination=side)
+        for b in range(g.n_obs):
+            pr.add_residual_block(g.corners[b], cam, caps[g.obs_cap[b]], tags[g.obs_tag[b]])
+        seen = []
+        pr.set_iteration_callback(lambda it: seen.append((it["iteration"], cam[0], caps[3].copy(), tags[5].copy())))
+        s = pr.solve()
+        assert [i for i, _, _, _ in seen] == [it["iteration"] for it in s["iterations"]]
+        assert seen[0][1] == g.camera[0] and np.array_equal(seen[0][2], g.cap[3])
+        assert seen[1][1] != g.camera[0] and not np.array_equal(seen[1][2], g.cap[3])   # after iteration 1
+        assert not np.array_equal(seen[1][3], g.tag[5])
+        assert seen[-1][1] == cam[0] and np.array_equal(seen[-1][2], caps[3])
+
+
 def test_broken_dependency_is_a_device_error(lm):
     """A task-graph wait that can never be met ends the solve with ARSLAM_E_DEVICE naming the
     ticket (it used to become an invalid LM step); a fresh load solves normally again."""
@@ -124,6 +174,8 @@ def test_broken_dependency_is_a_device_error(lm):
         rp.solve()
     assert e.value.code == -8
     assert "executor fault" in str(e.value) and "timed out" in str(e.value)
+    # the broken wait lasts one solve: the same handle then solves normally again
+    assert [i["cost"] for i in rp.solve()["iterations"]] == [i["cost"] for i in ok["iterations"]]
     rp2 = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
     s = rp2.solve()
     assert [i["cost"] for i in s["iterations"]] == [i["cost"] for i in ok["iterations"]]

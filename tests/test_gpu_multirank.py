@@ -30,7 +30,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, name, q):
+def _worker(rank, world, port, name, q, abort_rank=-1):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -46,6 +46,9 @@ def _worker(rank, world, port, name, q):
                             op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
 
         rp = lm.ResidentProblem(**part, comm=(rank, world, allreduce), device=0)
+        if abort_rank >= 0:   # only this rank's callback asks to stop, at iteration 2
+            rp.set_iteration_callback(
+                lambda it: lm.SOLVER_ABORT if rank == abort_rank and it["iteration"] == 2 else None)
         s = rp.solve()
         q.put((rank, rp.camera.copy(), rp.cap.copy(), rp.tag.copy(),
                [it["cost"] for it in s["iterations"]], s["termination"], s["rule"], s["final_cost"],
@@ -65,12 +68,12 @@ def _align_rigid(P, Q):
     return (R @ (P - pc).T).T + qc
 
 
-def _run_ranks(name, world):
+def _run_ranks(name, world, abort_rank=-1):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q, abort_rank)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -140,3 +143,16 @@ def test_sharded_cfg3_matches_golden_trace():
     print(f"cfg3 x2 ranks: {xbytes / 1e6:.1f} MB all-reduced per rank per LM iteration "
           f"({g.n_tag} tags, reduced system {6 * g.n_tag + 3} rows)")
     assert 0 < xbytes < 200e6
+
+
+def test_iteration_callback_decision_is_agreed_across_ranks():
+    """One rank's iteration callback returns SOLVER_ABORT at iteration 2, the other's CONTINUE:
+    the ranks take the same branch (the callbacks' answers are MAX-all-reduced), so every rank
+    ends with USER_FAILURE after the same three recorded iterations instead of one rank leaving
+    while the other blocks in the next step's exchange."""
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    res = _run_ranks("medium", 2, abort_rank=1)
+    for r in res:
+        assert (r[5], r[6]) == ("USER_FAILURE", "user_callback"), r[5:7]
+        assert len(r[4]) == 3 and r[4] == res[0][4]

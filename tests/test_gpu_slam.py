@@ -71,10 +71,37 @@ def test_bfs_solve_from_reference_default_focal(lm):
 
 
 def test_incremental_solve_matches_oracle_driver(lm):
+    """All 50 captures unsolved at once: the seed is the unordered_set's begin() and the rest are
+    visited in its bucket order (ar_slam_util.cpp:643, 657-676) -- the same sequence of solves
+    as the oracle's driver over the reference's own container."""
     g = synth.config_graph("small")
     s, o = _run_both(lm, g, "solve_incremental", camera=g.camera)
+    assert s.solve_order() == o.solve_order
+    assert s.solve_order()[0] != 0            # begin() of the set, not the lowest index
     _compare(s, o)
     assert s.num_solves == g.n_cap          # every capture got connected and solved once
+
+
+def test_incremental_cfg2_batches_match_oracle_driver(lm):
+    """cfg2's captures arriving in batches (several unsolved at once at every solveIncremental,
+    some only connectable after later batches): the same visiting order, the same number of
+    solves and the same final state as the oracle's driver."""
+    from oracle.driver import OracleSlam
+    g = synth.config_graph("cfg2")
+    s, o = lm.SlamSolver(), OracleSlam()
+    s.set_camera(g.camera)
+    o.camera = np.array(g.camera, np.float64)
+    batches = [range(0, 12), range(40, 52), range(12, 24), range(52, 60)]
+    for caps in batches:
+        for uid, ids, corners in _detections(g, caps):
+            s.add_detections(uid, ids, corners)
+            o.add_detections(uid, ids, corners)
+        assert s.unsolved_captures() == o.unsolved.items()
+        s.solve_incremental()
+        o.solve_incremental()
+        assert s.solve_order() == o.solve_order
+        assert s.unsolved_captures() == o.unsolved.items()
+    _compare(s, o)
 
 
 def test_localize_many_after_mapping(lm, oracle):

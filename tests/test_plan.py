@@ -143,18 +143,3 @@ def test_scalar_flops_match_symbolic_factorization(L, name):
     g = synth.config_graph(name)
     info, tag_row = _plan(L, g)
     assert info["scalar_flops"] == pytest.approx(_brute_force_scalar_flops(g, tag_row), rel=1e-12)
-
-
-@pytest.mark.parametrize("env", ["ARSLAM_TRSM_FOLD", "ARSLAM_RCLAIM", "ARSLAM_GCONT"])
-def test_task_graph_variants_are_deadlock_free(L, env, monkeypatch):
-    """The opt-in executor variants (update items folded into TRSM tasks, ready claims, generic
-    successor claims; llt_plan.cpp dag_build) keep the ticket order valid and deadlock-free."""
-    g = synth.config_graph("medium")
-    base = _plan(L, g)[0]["n_dag_tasks"]
-    monkeypatch.setenv(env, "1")
-    info, _ = _plan(L, g)
-    assert info["dag_valid"] == 1, info
-    if env == "ARSLAM_TRSM_FOLD":
-        assert info["n_dag_tasks"] < base   # folded update items are no tasks of their own
-    else:
-        assert info["n_dag_tasks"] == base

@@ -139,3 +139,19 @@ def test_transforms_and_camera_info(L):
     k, p = s.camera_info()
     np.testing.assert_allclose(k, [[3000, 0, 510], [0, 3000, 384], [0, 0, 1]])
     np.testing.assert_allclose(p[:, :3], k)
+
+
+def test_unsolved_set_iterates_in_the_reference_containers_order(L):
+    """The mirror keeps unsolved captures in std::unordered_set<CaptureHandle> with hash = index
+    (ar_slam_util.hpp:140-145, 492): its iteration order -- which seeds and orders
+    solveIncremental -- equals the oracle's instance of that container, across rehashes."""
+    from oracle.driver import UnorderedHandleSet
+    s = L.SlamSolver()
+    ref = UnorderedHandleSet()
+    rect = np.array([[-10.0, -10.0, 10.0, -10.0, 10.0, 10.0, -10.0, 10.0]])
+    for c in range(300):
+        assert s.add_detections(f"cap{c}", [f"tag_{c % 7}"], rect) == c
+        ref.insert(c)
+        if c in (0, 1, 10, 11, 12, 29, 30, 97, 98, 299):
+            assert s.unsolved_captures() == ref.items(), c
+    assert s.unsolved_captures()[0] != 0
