@@ -228,6 +228,47 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
   }
 }
 
+extern "C" int arslam_debug_rank_split(const arslam_soa_problem *p, int nranks, int rank, arslam_split_info *info,
+                                       int *cap_owner) {
+  if (!p || !info || nranks < 1 || rank < 0 || rank >= nranks) return ARSLAM_E_INVALID_ARG;
+  try {
+    std::memset(info, 0, sizeof(*info));
+    const arslam::HostProblem h = arslam::host_problem(p, nullptr);
+    arslam::ReducedLayout L = arslam::reduced_layout(h, 2, true, nullptr, nullptr);
+    const arslam::RankSplit split = arslam::rank_split(h, L, nranks);
+    info->tiles_per_side = L.T;
+    info->top_work = split.top_work;
+    info->max_rank_work = split.max_rank_work;
+    info->total_work = split.total_work;
+    for (int c = 0; c < h.nc; ++c) {
+      if (cap_owner) cap_owner[c] = split.cap_owner[c];
+      info->n_owned_captures += split.cap_owner[c] == rank;
+    }
+    if (L.nR > 0) {
+      const std::vector<int> cls = split.col_class(rank);
+      for (int k = 0; k < L.T; ++k) {
+        info->n_top_cols += cls[k] == 1;
+        info->n_own_cols += cls[k] == 0;
+      }
+      arslam::LltPlan plan;
+      arslam::llt_plan_symbolic(plan, L.T, L.N, L.pattern, nranks > 1 ? &cls : nullptr);
+      info->n_top_tiles = plan.n_top_tiles;
+      info->n_tiles = plan.n_tiles;
+      info->n_dag_tasks = plan.n_dag_tasks;
+      info->phase_split = plan.phase_split;
+      info->dag_valid = arslam::dag_check(plan) ? 1 : 0;
+      for (int wk : {1, 2, 7, 64, 512})
+        for (unsigned seed = 1; seed <= 3 && info->dag_valid; ++seed)
+          if (!arslam::dag_simulate(plan, wk, seed)) info->dag_valid = -wk;
+    }
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}
+
 extern "C" int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[4]) {
   if (!p || !out) return ARSLAM_E_INVALID_ARG;
   try {

@@ -834,6 +834,8 @@ struct DagArgs {
   double *part;
   int *split_cnt;
   int *flag;
+  int t_begin, t_end;         // this launch's tickets (one phase of a multi-rank plan, or all)
+  int *ticket;                // its ticket counter
   int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
   unsigned long long *trace;  // debug: [n_tasks][8] s_memrealtime at draw / waits met / end, workgroup, sub-phases
 };
@@ -858,12 +860,12 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [5] fused TRSM tile prefetched
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
   double *colx = LTd + 4 * 16 * LI + 4;   // POTRF pivot scratch (X stays free for the prefetch)
-  int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.counters + 2 * a.n_tiles;
+  int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.ticket;
   // claimed continuation targets in flight.  A target is claimed once its
   // EARLY waits are all drawn; its late waits may name undrawn tickets, so at
   // most half the grid may hold claimed targets: the other workgroups can
   // always draw the lowest unfinished ticket, whose producers are all done.
-  int *inflight = ticket + 1;
+  int *inflight = a.counters + 2 * a.n_tiles + 1;
   const int cont_cap = (int)(gridDim.x / 2);
   // Per-CU "POTRF running" flags (performance only: a wrong or stale flag
   // costs a bounded pause, never a result).  The 64x64 POTRF is a chain of
@@ -900,7 +902,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     const int li = lane & 15, lk = lane >> 4;
     const bool cont = next >= 0;
     if (!cont) {
-      if (tid == 0) sh[0] = atomicAdd(ticket, 1);
+      if (tid == 0) sh[0] = a.t_begin + atomicAdd(ticket, 1);
       __syncthreads();
       next = sh[0];
       __syncthreads();
@@ -911,7 +913,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     prev_k = -1;
     DAG_PROGRESS(0, t);
     DAG_PROGRESS(1, 1);
-    if (t >= a.n_tasks) break;
+    if (t >= a.t_end) break;
     const int4 task = a.tasks[t];
     DAG_PROGRESS(2, task.x);
     if (a.trace && tid == 0) { a.trace[8L * t] = realtime(); a.trace[8L * t + 3] = blockIdx.x; }
@@ -1080,7 +1082,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           // claim the continuation target first: its drawer waits for this
           // tile, so it cannot have claimed it yet
           int claim = -1;
-          if (c >= 0 && ld_acquire_relaxed(ticket) > a.maxdep[c]) {
+          if (c >= 0 && a.t_begin + ld_acquire_relaxed(ticket) > a.maxdep[c]) {
             if (atomicAdd(inflight, 1) < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0) claim = c;
             else atomicSub(inflight, 1);
           }
@@ -1484,7 +1486,7 @@ __global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c
 }  // namespace
 
 void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagArgs *ld) {
-  const long na = P.n_dag_tasks ? 2 * P.n_tiles + 2 + kCuFlags : 0, nb = P.n_dag_tasks, nc = P.n_split,
+  const long na = P.n_dag_tasks ? 2 * P.n_tiles + kDagCounterExtra : 0, nb = P.n_dag_tasks, nc = P.n_split,
              nd = P.h_bcols.empty() ? 0 : (long)P.T + 1;
   LmDiagArgs l{};
   if (ld) l = *ld;
@@ -1520,18 +1522,21 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
 }
 
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
-                          unsigned long long *trace, bool reset) {
-  if (P.n_dag_tasks == 0) return;
+                          unsigned long long *trace, bool reset, int phase) {
+  const int t_begin = phase == 1 ? (int)P.phase_split : 0;
+  const int t_end = phase == 0 ? (int)P.phase_split : (int)P.n_dag_tasks;
+  if (t_end <= t_begin) return;
   if (reset) {
-    (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + 2 + kCuFlags) * sizeof(int), s);
+    (void)hipMemsetAsync(P.dag_counters, 0, (2 * (size_t)P.n_tiles + kDagCounterExtra) * sizeof(int), s);
     (void)hipMemsetAsync(P.dag_claimed, 0, (size_t)P.n_dag_tasks * sizeof(int), s);
     if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
   }
   DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
             P.dag_maxdep, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
-            P.upd_part, P.upd_cnt, flag, progress, trace};
-  const int grid = (int)std::min<long>(n_workgroups, P.n_dag_tasks);
+            P.upd_part, P.upd_cnt, flag, t_begin, t_end,
+            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagCounterExtra - 1 : 0), progress, trace};
+  const int grid = (int)std::min<long>(n_workgroups, t_end - t_begin);
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
 

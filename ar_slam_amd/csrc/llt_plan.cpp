@@ -62,7 +62,7 @@ constexpr int kSimWorkers = 224;
 // tile (sub = its compact tile id): 'late' waits are those of that TRSM,
 // polled after L_kk is published.
 struct DagNode {
-  double est;
+  int phase = 0;   // multi-rank plans: 0 this rank's subtree columns, 1 the replicated top
   int type;
   int idx;
   int4 task;
@@ -208,7 +208,12 @@ void dag_build(LltPlan &plan) {
   const long nt = plan.n_tiles;
   auto tid = [&](int i, int j) { return plan.h_tile_id[(long)i * T + j]; };
   const int nlev = plan.nlev;
-  // applications per target tile and per-(target, level) sequence number
+  // the phase of a level (multi-rank plans: phase 0 = this rank's subtree
+  // columns, phase 1 = the replicated top separators, llt_plan_symbolic)
+  const int lev_per_phase = plan.n_phases > 1 ? nlev / plan.n_phases : nlev;
+  auto phase_of_level = [&](int l) { return l / lev_per_phase; };
+  // applications per target tile and per-(target, level) sequence number,
+  // over both phases in order (a top tile's phase-1 items follow its phase-0 ones)
   std::vector<int> n_apply(nt, 0);
   std::vector<int> item_seq(plan.h_items.size(), 0);
   for (int l = 0; l < nlev; ++l) {
@@ -223,73 +228,50 @@ void dag_build(LltPlan &plan) {
   }
   typedef DagNode Node;
   std::vector<Node> nodes;
-  const double c_potrf = 12.0, c_trsm = 3.0, eps = 1e-3;
-  std::vector<double> potrf_done(T, 0.0), trsm_done(nt, 0.0), last_apply(nt, 0.0), last_chunk_start(nt, -1.0);
-  std::vector<double> level_apply(nt, 0.0);
   for (int l = 0; l < nlev; ++l) {
     // factor tasks of the level's columns
     for (int p = plan.h_panel_off[l]; p < plan.h_panel_off[l + 1]; ++p) {
       const int2 pk = plan.h_panel[p];
       const int i = pk.x, k = pk.y;
       Node n;
+      n.phase = phase_of_level(l);
       if (i == k) {
         n.type = 0;
         n.task = make_int4(0, k, -1, tid(k, k));
-        n.est = last_apply[tid(k, k)];
         if (n_apply[tid(k, k)]) n.waits.push_back(make_int2((int)nt + tid(k, k), n_apply[tid(k, k)]));
-        potrf_done[k] = n.est + c_potrf;
       } else {
         n.type = 1;
         n.task = make_int4(1, i, k, tid(i, k));
         n.waits.push_back(make_int2(tid(k, k), 1));
         if (n_apply[tid(i, k)]) n.waits.push_back(make_int2((int)nt + tid(i, k), n_apply[tid(i, k)]));
-        n.est = 0.0;   // fixed below once the column's POTRF time is known
       }
       n.idx = p;
       nodes.push_back(std::move(n));
     }
-    for (size_t m = nodes.size() - (plan.h_panel_off[l + 1] - plan.h_panel_off[l]); m < nodes.size(); ++m)
-      if (nodes[m].type == 1) {
-        const int i = nodes[m].task.y, k = nodes[m].task.z;
-        nodes[m].est = std::max(potrf_done[k], last_apply[tid(i, k)]);
-        trsm_done[tid(i, k)] = nodes[m].est + c_trsm;
-      }
     // update items of the level
-    std::vector<double> apply_ready(nt, 0.0);
-    std::vector<int> touched;
     for (int it = plan.h_item_off[l]; it < plan.h_item_off[l + 1]; ++it) {
       const int4 item = plan.h_items[it];
       const int2 tg = plan.h_targets[item.x];
       const int tt = tid(tg.x, tg.y);
       Node n;
+      n.phase = phase_of_level(l);
       n.type = 2;
       n.idx = it;
       n.task = make_int4(2, it, item_seq[it], tt);
-      double e = last_chunk_start[tt] + eps;   // after every chunk of the target's earlier levels
       for (int q = item.y; q < item.z; ++q) {
         const int k = plan.h_ks[q];
         n.waits.push_back(make_int2(tid(tg.x, k), 1));
-        e = std::max(e, trsm_done[tid(tg.x, k)]);
-        if (tg.y != tg.x) {
-          n.waits.push_back(make_int2(tid(tg.y, k), 1));
-          e = std::max(e, trsm_done[tid(tg.y, k)]);
-        }
+        if (tg.y != tg.x) n.waits.push_back(make_int2(tid(tg.y, k), 1));
       }
-      n.est = e;
-      const double fin = e + 2.0 * (item.z - item.y);
-      if (apply_ready[tt] == 0.0) touched.push_back(tt);
-      apply_ready[tt] = std::max(apply_ready[tt], fin);
-      level_apply[tt] = std::max(level_apply[tt], e);
       nodes.push_back(std::move(n));
-    }
-    for (int tt : touched) {
-      last_apply[tt] = std::max(apply_ready[tt], last_apply[tt]) + 2.0;
-      last_chunk_start[tt] = level_apply[tt];
     }
   }
   // Fold the last update of each diagonal tile into its POTRF task when that
-  // update is one unsplit item: the POTRF then computes A_kk - sum L_kj L_kj^T
-  // itself, taking a task and a hand-off off the critical chain.
+  // update is one unsplit item of the same phase: the POTRF then computes
+  // A_kk - sum L_kj L_kj^T itself, taking a task and a hand-off off the
+  // critical chain.  (A multi-rank top tile's phase-0 items are this rank's
+  // share of a sum that is all-reduced between the phases: never folded into
+  // a phase-1 POTRF.)
   {
     std::vector<int> last_item(nt, -1), last_count(nt, 0);
     for (size_t m = 0; m < nodes.size(); ++m) {
@@ -304,7 +286,8 @@ void dag_build(LltPlan &plan) {
       if (n.type != 0) continue;
       const int tt = n.task.w;
       const int m = last_item[tt];
-      if (m < 0 || last_count[tt] != 1 || plan.h_items[nodes[m].task.y].w >= 0) continue;
+      if (m < 0 || last_count[tt] != 1 || plan.h_items[nodes[m].task.y].w >= 0 || nodes[m].phase != n.phase)
+        continue;
       n.task.z = nodes[m].task.y;   // item folded into the POTRF
       std::vector<int2> w;
       for (const int2 &x : n.waits)
@@ -324,7 +307,7 @@ void dag_build(LltPlan &plan) {
   // separator columns, POTRF(k) -> TRSM(parent, k) -> POTRF(parent) is the
   // critical path, and the fused task solves the tile against the L_kk it
   // still holds in LDS (no draw, no hand-off, no reload of L_kk).  The
-  // TRSM's own waits become the task's late waits.
+  // TRSM's own waits become the task's late waits.  (Same column: same phase.)
   {
     std::vector<int> trsm_node(nt, -1);
     for (size_t m = 0; m < nodes.size(); ++m)
@@ -356,18 +339,32 @@ void dag_build(LltPlan &plan) {
     Node n;
     n.type = 3;
     n.idx = k;
-    n.est = 0.0;
+    n.phase = plan.h_col_class.empty() ? 0 : (plan.h_col_class[k] == 1 ? 1 : 0);
     n.task = make_int4(3, k, 0, tid(k, k));
     n.waits.push_back(make_int2(tid(k, k), 1));
     nodes.push_back(std::move(n));
   }
-  std::vector<int> order = dag_list_schedule(nodes, nt, plan);
+  // tickets: each phase list-scheduled on its own (phase 1 runs in a later
+  // launch, after the multi-rank exchange), phase 0 first
+  std::vector<int> order;
+  for (int ph = 0; ph < std::max(plan.n_phases, 1); ++ph) {
+    std::vector<int> idx;
+    for (int v = 0; v < (int)nodes.size(); ++v)
+      if (nodes[v].phase == ph) idx.push_back(v);
+    std::vector<Node> sub;
+    sub.reserve(idx.size());
+    for (int v : idx) sub.push_back(nodes[v]);
+    for (int o : dag_list_schedule(sub, nt, plan)) order.push_back(idx[o]);
+    if (ph == 0) plan.phase_split = (long)order.size();
+  }
   plan.h_dag_tasks.clear();
   plan.h_dag_waits.clear();
   plan.h_dag_sub.clear();
+  plan.h_dag_phase.clear();
   plan.h_dag_wait_off.assign(1, 0);
   for (int o : order) {
     plan.h_dag_tasks.push_back(nodes[o].task);
+    plan.h_dag_phase.push_back(nodes[o].phase);
     plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].waits.begin(), nodes[o].waits.end());
     plan.h_dag_sub.push_back(make_int2(nodes[o].sub, (int)plan.h_dag_waits.size()));
     plan.h_dag_waits.insert(plan.h_dag_waits.end(), nodes[o].late.begin(), nodes[o].late.end());
@@ -429,6 +426,7 @@ void dag_build(LltPlan &plan) {
       for (int i = tk.y + 1; i < T && par < 0; ++i)
         if (tid(i, tk.y) == sb) par = i;
       if (par < 0 || potrf_of[par] < 0 || potrf_of[par] <= t) continue;
+      if (plan.h_dag_phase[potrf_of[par]] != plan.h_dag_phase[t]) continue;   // never across the exchange
       plan.h_dag_cont[t] = potrf_of[par];
     }
     // (generic successor claims -- every task claiming the successor it is the
@@ -456,18 +454,9 @@ void dag_build(LltPlan &plan) {
   plan.total_factor_flops = plan.total_upd_flops + n_potrf * (t3 / 3.0 + t3 / 3.0) + n_trsm * 2.0 * t3;
 }
 
-void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) {
-  llt_plan_reset(plan);
-  plan.T = T;
-  plan.lda = lda;
-  // compact tile numbering: assembled tiles (the input pattern + diagonal) first
-  plan.h_tile_id.assign((size_t)T * T, -1);
-  long nid = 0;
-  for (int i = 0; i < T; ++i)
-    for (int j = 0; j <= i; ++j)
-      if (P[(long)i * T + j] || i == j) plan.h_tile_id[(long)i * T + j] = (int)nid++;
-  plan.n_assembled = nid;
-  // symbolic factorization at tile level
+// Symbolic Cholesky fill of a lower tile pattern (in place, diagonal set) and
+// the tile elimination tree (parent[k]: the first row below the diagonal).
+void tile_fill(int T, std::vector<uint8_t> &P, std::vector<int> &parent) {
   std::vector<int> rows;
   for (int k = 0; k < T; ++k) {
     P[(long)k * T + k] = 1;
@@ -477,18 +466,60 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
     for (size_t a = 0; a < rows.size(); ++a)
       for (size_t b = 0; b <= a; ++b) P[(long)rows[a] * T + rows[b]] = 1;
   }
-  // tile elimination tree and heights
-  std::vector<int> parent(T, -1), height(T, 0);
+  parent.assign(T, -1);
   for (int k = 0; k < T; ++k)
     for (int i = k + 1; i < T; ++i)
       if (P[(long)i * T + k]) { parent[k] = i; break; }
+}
+
+void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, const std::vector<int> *col_class) {
+  llt_plan_reset(plan);
+  plan.T = T;
+  plan.lda = lda;
+  const bool multi = col_class != nullptr;
+  std::vector<int> cls = multi ? *col_class : std::vector<int>(T, 0);
+  plan.h_col_class.assign(cls.begin(), cls.end());
+  plan.n_phases = multi ? 2 : 1;
+  const std::vector<uint8_t> assembled = P;
+  std::vector<int> parent;
+  tile_fill(T, P, parent);
+  // compact tile numbering.  One rank: the assembled tiles (the input pattern
+  // + diagonal) first, then the fill.  Several ranks: the top columns' tiles
+  // first (the prefix all-reduced between the two phases), then this rank's
+  // own subtree columns'; another rank's tiles are not stored here.
+  plan.h_tile_id.assign((size_t)T * T, -1);
+  long nid = 0;
+  if (multi) {
+    for (int want : {1, 0})
+      for (int i = 0; i < T; ++i)
+        for (int j = 0; j <= i; ++j)
+          if (P[(long)i * T + j] && cls[j] == want) plan.h_tile_id[(long)i * T + j] = (int)nid++;
+    plan.n_top_tiles = 0;
+    for (int i = 0; i < T; ++i)
+      for (int j = 0; j <= i; ++j)
+        if (P[(long)i * T + j] && cls[j] == 1) plan.n_top_tiles++;
+    plan.n_assembled = plan.n_top_tiles;
+  } else {
+    for (int i = 0; i < T; ++i)
+      for (int j = 0; j <= i; ++j)
+        if (assembled[(long)i * T + j] || i == j) plan.h_tile_id[(long)i * T + j] = (int)nid++;
+    plan.n_assembled = nid;
+    for (int i = 0; i < T; ++i)   // fill tiles numbered after the assembled ones
+      for (int j = 0; j <= i; ++j)
+        if (P[(long)i * T + j] && plan.h_tile_id[(long)i * T + j] < 0) plan.h_tile_id[(long)i * T + j] = (int)nid++;
+  }
+  plan.n_tiles = nid;
+  // tile elimination tree heights
+  std::vector<int> height(T, 0);
   for (int k = 0; k < T; ++k)
     if (parent[k] >= 0) height[parent[k]] = std::max(height[parent[k]], height[k] + 1);
   int nlev = 0;
   for (int k = 0; k < T; ++k) nlev = std::max(nlev, height[k] + 1);
   std::vector<std::vector<int>> levcols(nlev);
   for (int k = 0; k < T; ++k) levcols[height[k]].push_back(k);
-  plan.nlev = nlev;
+  // levels of each phase (phase 0: class-0 columns, phase 1: class-1), one
+  // set of level lists per phase
+  plan.nlev = nlev * plan.n_phases;
 
   std::vector<int2> &panel = plan.h_panel, &targets = plan.h_targets, &gather = plan.h_gather,
                     &split = plan.h_split;
@@ -506,9 +537,14 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
   plan.total_upd_tiles = 0;
   const double t3 = 64.0 * 64.0 * 64.0;
   std::vector<int> tgt_id((size_t)T * T, -1);
-  for (int l = 0; l < nlev; ++l) {
+  std::vector<int> rows;
+  for (int lp = 0; lp < plan.nlev; ++lp) {
+    const int l = lp % nlev, phase = lp / nlev;
+    std::vector<int> cols;
+    for (int k : levcols[l])
+      if (cls[k] == phase) cols.push_back(k);
     // panel tasks
-    for (int k : levcols[l]) {
+    for (int k : cols) {
       panel.push_back(make_int2(k, k));
       for (int i = k + 1; i < T; ++i)
         if (P[(long)i * T + k]) panel.push_back(make_int2(i, k));
@@ -518,7 +554,7 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
     std::vector<int2> lt;
     std::vector<std::vector<int>> lks;
     double fl = 0.0;
-    for (int k : levcols[l]) {
+    for (int k : cols) {
       rows.clear();
       for (int i = k + 1; i < T; ++i)
         if (P[(long)i * T + k]) rows.push_back(i);
@@ -570,9 +606,12 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
     plan.total_upd_flops += fl;
   }
   // backward solve: levels from the root down; each column gathers from its
-  // tile rows below the diagonal (ancestors, solved in earlier launches)
+  // tile rows below the diagonal (ancestors, solved in earlier launches).
+  // Several ranks: the top columns and this rank's own (their ancestors are
+  // own or top columns).
   for (int l = nlev - 1; l >= 0; --l) {
     for (int k : levcols[l]) {
+      if (cls[k] == 2) continue;
       bcols.push_back(k);
       for (int i = k + 1; i < T; ++i)
         if (P[(long)i * T + k]) gather.push_back(make_int2(i, k));
@@ -581,11 +620,125 @@ void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P) 
     plan.h_bs_off.push_back((int)bcols.size());
     plan.h_bsg_off.push_back((int)gather.size());
   }
-  for (int i = 0; i < T; ++i)   // fill tiles numbered after the assembled ones
-    for (int j = 0; j <= i; ++j)
-      if (P[(long)i * T + j] && plan.h_tile_id[(long)i * T + j] < 0) plan.h_tile_id[(long)i * T + j] = (int)nid++;
-  plan.n_tiles = nid;
   dag_build(plan);
+}
+
+RankSplit rank_split(const HostProblem &h, const ReducedLayout &L, int nranks) {
+  RankSplit out;
+  const int T = L.T, nc = h.nc;
+  out.cap_owner.assign(nc, 0);
+  out.col_owner.assign(T, -1);
+  std::vector<long> rank_obs(nranks, 0);
+  auto least_loaded = [&]() {
+    int r = 0;
+    for (int q = 1; q < nranks; ++q)
+      if (rank_obs[q] < rank_obs[r]) r = q;
+    return r;
+  };
+  if (L.nR == 0 || T == 0 || nranks <= 1) {
+    for (int c = 0; c < nc; ++c) {
+      const int r = nranks <= 1 ? 0 : least_loaded();
+      out.cap_owner[c] = r;
+      rank_obs[r] += h.cap_start[c + 1] - h.cap_start[c];
+    }
+    if (nranks <= 1) out.col_owner.assign(T, 0);
+    return out;
+  }
+  std::vector<uint8_t> P = L.pattern;
+  std::vector<int> parent;
+  tile_fill(T, P, parent);
+  std::vector<std::vector<int>> ch(T);
+  for (int k = 0; k < T; ++k)
+    if (parent[k] >= 0) ch[parent[k]].push_back(k);
+  // work of a column: its tile tasks (POTRF, TRSMs, update pairs); of a subtree: the sum
+  std::vector<double> w(T), W(T);
+  for (int k = 0; k < T; ++k) {
+    double c = 0;
+    for (int i = k + 1; i < T; ++i) c += P[(long)i * T + k];
+    w[k] = W[k] = (c + 1.0) * (c + 2.0) / 2.0;
+  }
+  for (int k = 0; k < T; ++k)
+    if (parent[k] >= 0) W[parent[k]] += W[k];
+  for (int k = 0; k < T; ++k) out.total_work += w[k];
+  // Grow the replicated top from the root: repeatedly move the heaviest
+  // subtree root of the frontier into the top (descending a separator chain
+  // one column at a time), and keep the state with the least estimated
+  // makespan = top work (every rank) + the heaviest rank's subtrees (largest
+  // first onto the least loaded rank).
+  std::vector<char> top(T, 0);
+  std::vector<int> frontier;
+  for (int k = 0; k < T; ++k)
+    if (parent[k] < 0) frontier.push_back(k);
+  double best = -1.0, topw = 0.0;
+  std::vector<char> best_top;
+  std::vector<int> best_front, best_asg;
+  for (int iter = 0; iter <= T; ++iter) {
+    if ((int)frontier.size() >= nranks) {
+      std::vector<int> ord = frontier;
+      std::sort(ord.begin(), ord.end(), [&](int a, int b) { return W[a] != W[b] ? W[a] > W[b] : a > b; });
+      std::vector<double> bins(nranks, 0.0);
+      std::vector<int> asg(ord.size());
+      for (size_t q = 0; q < ord.size(); ++q) {
+        int r = 0;
+        for (int x = 1; x < nranks; ++x)
+          if (bins[x] < bins[r]) r = x;
+        asg[q] = r;
+        bins[r] += W[ord[q]];
+      }
+      const double mx = *std::max_element(bins.begin(), bins.end());
+      if (best < 0 || topw + mx < best * (1.0 - 1e-12)) {
+        best = topw + mx;
+        best_top = top;
+        best_front = ord;
+        best_asg = asg;
+        out.top_work = topw;
+        out.max_rank_work = mx;
+      }
+    }
+    int v = -1;
+    for (int f : frontier)
+      if (v < 0 || W[f] > W[v] || (W[f] == W[v] && f > v)) v = f;
+    if (v < 0 || ch[v].empty()) break;
+    top[v] = 1;
+    topw += w[v];
+    frontier.erase(std::find(frontier.begin(), frontier.end(), v));
+    frontier.insert(frontier.end(), ch[v].begin(), ch[v].end());
+  }
+  if (best < 0) {   // fewer subtrees than ranks: some ranks own none
+    best_top = top;
+    best_front = frontier;
+    best_asg.assign(frontier.size(), 0);
+    for (size_t q = 0; q < frontier.size(); ++q) best_asg[q] = (int)q % nranks;
+    out.top_work = topw;
+  }
+  std::vector<int> root_rank(T, -1);
+  for (size_t q = 0; q < best_front.size(); ++q) root_rank[best_front[q]] = best_asg[q];
+  for (int k = T - 1; k >= 0; --k) {
+    if (best_top[k]) out.col_owner[k] = -1, out.n_top_cols++;
+    else if (root_rank[k] >= 0) out.col_owner[k] = root_rank[k];
+    else out.col_owner[k] = parent[k] >= 0 ? out.col_owner[parent[k]] : 0;
+  }
+  // captures: the owner of the lowest tile column among their tags' rows
+  std::vector<int> top_only;
+  for (int c = 0; c < nc; ++c) {
+    int low = T;
+    for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a) {
+      const int r0 = L.tag_row[h.blk_tag[a]];
+      if (r0 >= 0) low = std::min(low, r0 / kTileRows);
+    }
+    if (low < T && out.col_owner[low] >= 0) {
+      out.cap_owner[c] = out.col_owner[low];
+      rank_obs[out.col_owner[low]] += h.cap_start[c + 1] - h.cap_start[c];
+    } else {
+      top_only.push_back(c);
+    }
+  }
+  for (int c : top_only) {
+    const int r = least_loaded();
+    out.cap_owner[c] = r;
+    rank_obs[r] += h.cap_start[c + 1] - h.cap_start[c];
+  }
+  return out;
 }
 
 bool dag_check(const LltPlan &plan) {
@@ -717,6 +870,9 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   add(reinterpret_cast<void **>(&plan.bs_part), nullptr, std::max<size_t>(plan.h_gather.size(), 1) * 64 * sizeof(double));
   add(reinterpret_cast<void **>(&plan.bs_counters), nullptr, ((size_t)T + 1) * sizeof(int));
   addv(&plan.tile_id, plan.h_tile_id);
+  std::vector<signed char> cls(plan.h_col_class.begin(), plan.h_col_class.end());
+  if (cls.empty()) cls.assign(T, 0);
+  addv(&plan.tile_class, cls);
   // L_kk, L_kk^{-1}, and the 16x16 block inverses (4 x 16 x 18) of each column
   add(reinterpret_cast<void **>(&plan.ldiag), nullptr, ((size_t)2 * T * 64 * 64 + (size_t)T * 1152) * sizeof(double));
   addv(&plan.dag_tasks, plan.h_dag_tasks);
@@ -726,7 +882,7 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   addv(&plan.dag_cont, plan.h_dag_cont);
   addv(&plan.dag_maxdep, plan.h_dag_maxdep);
   add(reinterpret_cast<void **>(&plan.dag_claimed), nullptr, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int));
-  add(reinterpret_cast<void **>(&plan.dag_counters), nullptr, (2 * (size_t)plan.n_tiles + 2 + kCuFlags) * sizeof(int));
+  add(reinterpret_cast<void **>(&plan.dag_counters), nullptr, (2 * (size_t)plan.n_tiles + kDagCounterExtra) * sizeof(int));
   size_t total = 0, staged = 0;
   std::vector<size_t> off(pieces.size());
   for (size_t i = 0; i < pieces.size(); ++i) {   // host arrays first: one contiguous copy
@@ -756,8 +912,9 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   check(hipStreamSynchronize(s), "plan sync");   // (the staging buffer goes out of scope)
 }
 
-void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hipStream_t s) {
-  llt_plan_symbolic(plan, T, lda, P);
+void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &P, hipStream_t s,
+                    const std::vector<int> *col_class) {
+  llt_plan_symbolic(plan, T, lda, P, col_class);
   llt_plan_upload(plan, s);
 }
 

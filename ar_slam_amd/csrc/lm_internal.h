@@ -18,6 +18,9 @@
 
 namespace arslam {
 constexpr int kCuFlags = 2048;   // k_factor_dag's per-CU flags: 8 XCCs x 256 (SE, SH, CU) ids
+// dag_counters after ready[n_tiles] | applied[n_tiles]: the phase-0 ticket,
+// the claimed-continuation count, the per-CU flags, the phase-1 ticket
+constexpr int kDagCounterExtra = 2 + kCuFlags + 1;
 
 constexpr int kWave = 64;
 constexpr int kTile = 64;          // reduced-system Cholesky tile
@@ -77,6 +80,9 @@ struct DevProblem {
   const int4 *gather_splits; // [n_splits] {destination, first partial slot, pieces, 0}
   double *gather_part;       // [n_pslots * 36]
   int n_items, n_splits;
+  // multi-rank: class of each tile column (0 this rank's subtree, 1 the
+  // replicated top, 2 another rank's; LltPlan::tile_class), null on one rank
+  const signed char *tile_class;
   double *jrows;             // [8 nb kRowStride] unscaled Jacobian rows + residual at the linearization point
   double *cap_ui;            // [36 nc] (U_c + D_c^2)^{-1} of the current step (k_schur -> k_backsub)
 };
@@ -117,7 +123,16 @@ struct LltPlan {
   int *tile_id = nullptr;       // [T*T] compact index of tile (i,j), -1 if structurally zero
   std::vector<int> h_tile_id;
   long n_tiles = 0;             // tiles of the factor (compact storage = n_tiles * 4096 doubles)
-  long n_assembled = 0;         // tiles the Schur assembly writes (numbered first)
+  long n_assembled = 0;         // tiles the Schur assembly writes (numbered first; multi-rank: = n_top_tiles)
+  // multi-rank plans (llt_plan_symbolic with column classes): phase 0 factors
+  // this rank's subtree columns, phase 1 the replicated top columns after the
+  // exchange of the top tiles (numbered first: tiles [0, n_top_tiles))
+  int n_phases = 1;
+  long phase_split = 0;         // tickets [0, phase_split) are phase 0
+  long n_top_tiles = 0;
+  std::vector<int> h_col_class; // [T] 0 own subtree, 1 top, 2 another rank's (not stored)
+  std::vector<int> h_dag_phase; // [n_dag_tasks]
+  signed char *tile_class = nullptr;   // [T] device copy of h_col_class
   double *ldiag = nullptr;      // 2T x 64 x 64: diagonal factors L_kk, then their inverses (row-major)
   std::vector<int> h_panel_off;     // [nlev+1]
   std::vector<int> h_upd_off;       // [nlev+1]
@@ -140,7 +155,7 @@ struct LltPlan {
   int *dag_cont = nullptr, *dag_maxdep = nullptr, *dag_claimed = nullptr;
   std::vector<int> h_dag_cont, h_dag_maxdep;
   int *dag_wait_off = nullptr;
-  // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags])
+  // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags | phase-1 ticket])
   int2 *dag_waits = nullptr;
   int *dag_counters = nullptr;
   long n_dag_tasks = 0;
@@ -158,7 +173,30 @@ struct LltPlan {
 
 // Symbolic tile fill of the lower pattern (T*T bytes, in/out) and the host
 // task lists (no HIP calls: usable without a device).
-void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern);
+// (col_class: null = one rank; else per tile column 0 this rank's subtree,
+// 1 the replicated top, 2 another rank's -- a two-phase plan, see LltPlan)
+void llt_plan_symbolic(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern,
+                       const std::vector<int> *col_class = nullptr);
+// symbolic tile-level Cholesky fill (in place) and the tile elimination tree
+void tile_fill(int T, std::vector<uint8_t> &pattern, std::vector<int> &parent);
+// Subtree-to-rank split of the tile elimination tree (multi-GPU): the top of
+// the tree (the upper nested-dissection separators, the camera and the rhs)
+// is replicated, the subtrees below it are dealt to the ranks, and every
+// capture goes to the rank owning the lowest tile column of its tags (its
+// columns lie on one root path: they are pairwise coupled), or, if its tags
+// are all in the top, to the rank with the fewest observations so far.
+struct RankSplit {
+  std::vector<int> col_owner;   // [T] owning rank, -1 = top (replicated)
+  std::vector<int> cap_owner;   // [nc]
+  int n_top_cols = 0;
+  double top_work = 0.0, max_rank_work = 0.0, total_work = 0.0;   // tile-task counts
+  std::vector<int> col_class(int rank) const {   // llt_plan_symbolic's classes
+    std::vector<int> c(col_owner.size());
+    for (size_t k = 0; k < c.size(); ++k) c[k] = col_owner[k] < 0 ? 1 : (col_owner[k] == rank ? 0 : 2);
+    return c;
+  }
+};
+RankSplit rank_split(const HostProblem &h, const ReducedLayout &L, int nranks);
 // Ticket-order check of the task graph: executing the tasks one at a time in
 // ticket order, is every wait already satisfied when its task runs?
 bool dag_check(const LltPlan &plan);
@@ -166,7 +204,8 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed);
 // Upload the host lists and allocate the plan's device buffers.
 void llt_plan_upload(LltPlan &plan, hipStream_t s);
 // llt_plan_symbolic + llt_plan_upload
-void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern, hipStream_t s);
+void llt_plan_build(LltPlan &plan, int T, long lda, std::vector<uint8_t> &pattern, hipStream_t s,
+                    const std::vector<int> *col_class = nullptr);
 void llt_plan_free(LltPlan &plan);                 // device arrays and the arena
 void llt_plan_reset(LltPlan &plan);                // host side only; the arena is kept for the next plan
 
@@ -186,8 +225,12 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
 // k_schur blocks before the gather writes S)
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
                   double radius, double *S, hipStream_t s, bool prep = false, long zero_tiles = 0);
+// (which: -1 every row; 0 / 1 only the rows of tile columns of that class)
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
-                         hipStream_t s);
+                         hipStream_t s, int which = -1);
+// multi-rank: the backward solve's y before its all-reduce: this rank's
+// subtree rows kept, the top rows kept on rank 0 only, every other row 0
+void launch_mask_y(const DevProblem &P, double *yF, int rank, hipStream_t s);
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
                     double radius, const double *yF, double *xc, double *parts, hipStream_t s,
                     bool reuse_ui = false, bool with_cost = false);
@@ -227,8 +270,10 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
 // The same factorization as one persistent launch over the plan's task graph
 // (tickets in a topological order, dependency counters in global memory).
 // (reset = false: the counters were zeroed by launch_exec_reset)
+// (phase: -1 every task; 0 / 1 one phase of a multi-rank plan, LltPlan)
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups,
-                          int *progress = nullptr, unsigned long long *trace = nullptr, bool reset = true);
+                          int *progress = nullptr, unsigned long long *trace = nullptr, bool reset = true,
+                          int phase = -1);
 // the LM diagonal clamp(s^2 colnorm, dmin, dmax) over n slots (k_lm_diag)
 struct LmDiagArgs {
   long n;

@@ -691,9 +691,10 @@ __global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__r
 // the rows past the rhs become identity rows; the rhs row gets a pivot large
 // enough to stay positive (its factor row is L^{-1} b, its pivot unused).
 __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, double radius,
-                               double *__restrict__ S) {
+                               double *__restrict__ S, int which) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.N) return;
+  if (which >= 0 && P.tile_class[i >> 6] != which) return;
   double *d = reduced_elem(S, P, i, i);
   if (i < P.nR) {
     const int slot = P.row_slot[i];
@@ -704,6 +705,14 @@ __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, do
   } else {
     *d = 1.0;
   }
+}
+
+// multi-rank y before its all-reduce (launch_mask_y)
+__global__ void k_mask_y(DevProblem P, double *__restrict__ yF, int rank) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.nR) return;
+  const int c = P.tile_class[i >> 6];
+  if (!(c == 0 || (c == 1 && rank == 0))) yF[i] = 0.0;
 }
 
 // Cost at x (candidate evaluation) of capture c: active / fixed cost,
@@ -1135,9 +1144,14 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
 }
 
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
-                         hipStream_t s) {
+                         hipStream_t s, int which) {
   hipLaunchKernelGGL(k_prep_reduced, dim3((unsigned)((P.N + 255) / 256)), dim3(256), 0, s, P, diag,
-                     radius, S);
+                     radius, S, which);
+}
+
+void launch_mask_y(const DevProblem &P, double *yF, int rank, hipStream_t s) {
+  if (P.nR == 0) return;
+  hipLaunchKernelGGL(k_mask_y, dim3((unsigned)((P.nR + 255) / 256)), dim3(256), 0, s, P, yF, rank);
 }
 
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,

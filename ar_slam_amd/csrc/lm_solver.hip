@@ -289,6 +289,14 @@ struct arslam_lm {
   int ceres_e_cap = 0, ceres_e_tag = 0;   // Ceres 2.0's e-block set of the loaded problem, by kind
   void reload_values(const arslam_soa_problem *p);
   bool pk_loaded = false;   // the resident problem came from the pointer-keyed API
+  // several ranks: the whole problem's capture count, this rank's captures
+  // (ascending; the loaded problem's capture c is own_caps[c]) and its local arrays
+  int nc_full = 0;
+  std::vector<int> own_caps;
+  std::vector<double> loc_cap, loc_corners;
+  std::vector<int> loc_obs_cap, loc_obs_tag;
+  std::vector<unsigned char> loc_cap_const;
+  double split_top_work = 0.0, split_max_rank_work = 0.0, split_total_work = 0.0;
   bool reuse_order = false;  // load(): keep the previous tag order when the free tags are unchanged
   std::vector<int> prev_tag_row;
   int prev_ordering = -1, prev_skip = -1;
@@ -345,42 +353,82 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
     side = (nranks == 1 && cs.e_tag > cs.e_cap && cs.max_tag_obs <= arslam::kMaxObsPerCapture) ? ARSLAM_ELIM_TAGS
                                                                                               : ARSLAM_ELIM_CAPTURES;
   fail_if(side == ARSLAM_ELIM_TAGS && nranks > 1, ARSLAM_E_UNSUPPORTED,
-          "tag elimination is single-rank only (the shards are capture ranges)");
+          "tag elimination is single-rank only (the ranks own captures)");
+  fail_if(nranks > 1 && opt.factor_executor != 1, ARSLAM_E_UNSUPPORTED,
+          "several ranks need the persistent executor (factor_executor = 1)");
   fail_if(side == ARSLAM_ELIM_TAGS && cs.max_tag_obs > arslam::kMaxObsPerCapture, ARSLAM_E_UNSUPPORTED,
           "tag elimination: more than 64 observations of one tag");
   if (side != elim_used) prev_tag_row.clear();   // the f-side changed: no order to reuse
   elim_used = side;
   const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
   const arslam_soa_problem *p = side == ARSLAM_ELIM_TAGS ? &swapped : p_in;
-  if (nranks > 1) ensure_stream();   // the structure exchange below runs on the device
-  // host structure; with several ranks the tag use, the co-visibility and the
-  // tile pattern are made global by max/sum all-reduces (same on every rank)
-  arslam::ReduceSumF64 deg_sum;
-  arslam::ReduceMaxU8 u8_max;
-  if (nranks > 1) {
-    deg_sum = [&](std::vector<double> &v) {
-      DevBuf<double> tmp;
-      tmp.alloc(v.size());
-      tmp.upload(v.data(), v.size(), stream);
-      allreduce(tmp.p, v.size(), ARSLAM_OP_SUM);
-      HIP_CHECK(hipMemcpyAsync(v.data(), tmp.p, v.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
-      HIP_CHECK(hipStreamSynchronize(stream));
-    };
-    u8_max = [&](std::vector<uint8_t> &v) {
-      DevBuf<uint8_t> tmp;
-      tmp.alloc(v.size());
-      tmp.upload(v.data(), v.size(), stream);
-      allreduce_any(tmp.p, v.size(), ARSLAM_DT_U8, ARSLAM_OP_MAX);
-      HIP_CHECK(hipMemcpyAsync(v.data(), tmp.p, v.size(), hipMemcpyDeviceToHost, stream));
-      HIP_CHECK(hipStreamSynchronize(stream));
-    };
-  }
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
   double tp[6] = {now_s(), 0, 0, 0, 0, 0};
-  arslam::HostProblem h = arslam::host_problem(p, deg_sum);   // validates p
+  // an incremental re-load (pointer-keyed path, same options) whose free tags
+  // are unchanged keeps the previous elimination order: the ordering (nested
+  // dissection) is the largest part of the host setup
+  const bool can_reuse = reuse_order && !prev_tag_row.empty() && prev_ordering == opt.reduced_ordering &&
+                         prev_skip == opt.cholesky_skip_zero_tiles;
+  arslam::HostProblem h;
+  arslam::ReducedLayout L;
+  std::vector<int> col_class;
+  own_caps.clear();
+  nc_full = p->n_cap;
+  if (nranks > 1) {
+    // Several ranks: every rank holds the whole problem and computes the same
+    // structure (deterministic host code, no exchange): the reduced layout,
+    // then the subtree-to-rank split of the tile elimination tree, which
+    // gives this rank its captures and tile columns (arslam::rank_split).
+    const arslam::HostProblem hf = arslam::host_problem(p, nullptr);   // validates p
+    L = arslam::reduced_layout(hf, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
+                               can_reuse ? &prev_tag_row : nullptr, prev_order_edges);
+    const arslam::RankSplit split = arslam::rank_split(hf, L, nranks);
+    col_class = split.col_class(rank);
+    split_top_work = split.top_work;
+    split_max_rank_work = split.max_rank_work;
+    split_total_work = split.total_work;
+    for (int c = 0; c < p->n_cap; ++c)
+      if (split.cap_owner[c] == rank) own_caps.push_back(c);
+    // this rank's problem: its captures (ascending), their observations, every tag
+    std::vector<int> loc_of(p->n_cap, -1);
+    loc_cap.resize(6 * own_caps.size());
+    loc_cap_const.assign(own_caps.size(), 0);
+    for (size_t c = 0; c < own_caps.size(); ++c) {
+      loc_of[own_caps[c]] = (int)c;
+      std::memcpy(&loc_cap[6 * c], p->cap + 6L * own_caps[c], 6 * sizeof(double));
+      if (p->cap_const) loc_cap_const[c] = p->cap_const[own_caps[c]];
+    }
+    loc_obs_cap.clear(); loc_obs_tag.clear(); loc_corners.clear();
+    for (int b = 0; b < p->n_obs; ++b) {
+      const int lc = loc_of[p->obs_cap[b]];
+      if (lc < 0) continue;
+      loc_obs_cap.push_back(lc);
+      loc_obs_tag.push_back(p->obs_tag[b]);
+      loc_corners.insert(loc_corners.end(), p->corners + 8L * b, p->corners + 8L * b + 8);
+    }
+    arslam_soa_problem pl = *p;
+    pl.n_cap = (int)own_caps.size();
+    pl.n_obs = (int)loc_obs_cap.size();
+    pl.cap = loc_cap.data();
+    pl.obs_cap = loc_obs_cap.data();
+    pl.obs_tag = loc_obs_tag.data();
+    pl.corners = loc_corners.data();
+    pl.cap_const = p->cap_const ? loc_cap_const.data() : nullptr;
+    // the tags' use (freedom) and the observation count are the whole problem's
+    const arslam::ReduceSumF64 global_deg = [&](std::vector<double> &deg) {
+      std::fill(deg.begin(), deg.end(), 0.0);
+      for (int b = 0; b < p->n_obs; ++b) deg[p->obs_tag[b]] += 1.0;
+      deg[p->n_tag] = p->n_obs;
+    };
+    h = arslam::host_problem(&pl, global_deg);
+  } else {
+    h = arslam::host_problem(p, nullptr);   // validates p
+    L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
+                               can_reuse ? &prev_tag_row : nullptr, prev_order_edges);
+  }
   tp[1] = now_s();
   ensure_stream();
-  soa = *p;
+  soa = *p;   // (several ranks: the whole problem; write_back maps this rank's captures)
   nc = h.nc;
   nt = h.nt;
   nb = h.nb;
@@ -389,14 +437,6 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   slot_free = h.slot_free;
   x0 = h.x0;
   const int maxk = h.maxk;
-  // an incremental re-load (pointer-keyed path, same options) whose free tags
-  // are unchanged keeps the previous elimination order: the ordering (nested
-  // dissection) is the largest part of the host setup
-  const bool can_reuse = reuse_order && !prev_tag_row.empty() && prev_ordering == opt.reduced_ordering &&
-                         prev_skip == opt.cholesky_skip_zero_tiles;
-  arslam::ReducedLayout L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0,
-                                                   u8_max, u8_max, can_reuse ? &prev_tag_row : nullptr,
-                                                   prev_order_edges);
   prev_tag_row = L.tag_row;
   prev_order_edges = L.order_edges;
   prev_ordering = opt.reduced_ordering;
@@ -413,7 +453,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   has_f = nR > 0;
   if (has_f) {
     N = L.N;
-    arslam::llt_plan_build(plan, L.T, N, L.pattern, stream);
+    arslam::llt_plan_build(plan, L.T, N, L.pattern, stream, nranks > 1 ? &col_class : nullptr);
   } else {
     N = 0;
     arslam::llt_plan_free(plan);
@@ -502,6 +542,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   P.tag_start = d_tag_start.p; P.tag_obs = d_tag_obs.p; P.corners = d_corners.p;
   P.tag_row = d_tag_row.p; P.row_slot = d_row_slot.p;
   P.tile_id = plan.tile_id; P.T = plan.T;
+  P.tile_class = nranks > 1 && has_f ? plan.tile_class : nullptr;
   P.cap_off = d_cap_off.p; P.slab = d_slab.p; P.dest_row = d_dest_row.p; P.dest_start = d_dest_start.p;
   P.contrib = d_contrib.p; P.n_dest = n_dest; P.jrows = d_jrows.p; P.cap_ui = d_cap_ui.p;
   P.gather_items = d_gather_items.p; P.gather_splits = d_gather_splits.p; P.gather_part = d_gather_part.p;
@@ -522,10 +563,14 @@ void arslam_lm::reload_values(const arslam_soa_problem *p_in) {
   const double t0 = now_s();
   const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
   const arslam_soa_problem *p = elim_used == ARSLAM_ELIM_TAGS ? &swapped : p_in;
-  fail_if(!loaded || p->n_cap != nc || p->n_tag != nt || p->n_obs != nb, ARSLAM_E_STATE,
+  fail_if(!loaded || p->n_cap != nc_full || p->n_tag != nt || (nranks == 1 && p->n_obs != nb), ARSLAM_E_STATE,
           "reload_values: structure differs from the loaded problem");
   std::memcpy(x0.data(), p->camera, 3 * sizeof(double));
-  if (nc) std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
+  if (nranks > 1) {
+    for (int c = 0; c < nc; ++c) std::memcpy(x0.data() + 3 + 6L * c, p->cap + 6L * own_caps[c], 6 * sizeof(double));
+  } else if (nc) {
+    std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
+  }
   if (nt) std::memcpy(x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
   d_x0.upload(x0.data(), n, stream);
   HIP_CHECK(hipStreamSynchronize(stream));
@@ -586,7 +631,11 @@ void arslam_lm::write_back(const double *d_src) {
   spin_sync();
   const double *h = h_x.p;
   std::memcpy(soa.camera, h, 3 * sizeof(double));
-  if (nc) std::memcpy(soa.cap, h + 3, 6L * nc * sizeof(double));
+  if (nranks > 1) {   // this rank's captures into the whole problem's array
+    for (int c = 0; c < nc; ++c) std::memcpy(soa.cap + 6L * own_caps[c], h + 3 + 6L * c, 6 * sizeof(double));
+  } else if (nc) {
+    std::memcpy(soa.cap, h + 3, 6L * nc * sizeof(double));
+  }
   if (nt) std::memcpy(soa.tag, h + 3 + 6L * nc, 6L * nt * sizeof(double));
   if (pk_stage) scatter_to_blocks();
 }
@@ -790,15 +839,14 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     if (has_f) {
       timers[PH_SCHUR].start(stream);
       // one rank: the gather writes the final S (D_f^2 and the padding rows
-      // included); several: S is summed over the ranks first.  k_schur's extra
-      // blocks clear S's tiles first.
+      // included).  Several: this rank's captures' share; the D_f^2 of the
+      // rank's own subtree rows now, of the top rows after their exchange
+      // (below).  k_schur's extra blocks clear S's tiles first.
       arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1, plan.n_tiles);
-      if (nranks > 1) {
-        allreduce(d_S.p, (size_t)plan.n_assembled * 4096, ARSLAM_OP_SUM);
-        arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream);
-      }
-      if (dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull)   // test hook
-        arslam::debug_set_reduced_diag(P, d_S.p, P.cam_row >= 0 ? P.cam_row : nR - 1, -1.0, stream);
+      const bool force_indefinite = dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull;
+      const long hook_row = P.cam_row >= 0 ? P.cam_row : nR - 1;   // (a top row with several ranks)
+      if (nranks > 1) arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream, 0);
+      else if (force_indefinite) arslam::debug_set_reduced_diag(P, d_S.p, hook_row, -1.0, stream);   // test hook
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
       timing_begin();
@@ -828,6 +876,16 @@ void arslam_lm::solve(arslam_lm_summary *s) {
             std::fclose(f);
           }
           dag_traced = true;
+        } else if (nranks > 1) {
+          // phase 0: this rank's subtree columns, and their updates of the top
+          // tiles (its share of the top's Schur complement); then the top tiles
+          // are summed over the ranks -- the step's one bulk exchange -- and
+          // every rank factors the top columns (phase 1) on identical inputs
+          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 0);
+          allreduce(d_S.p, (size_t)plan.n_top_tiles * 4096, ARSLAM_OP_SUM);
+          arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream, 1);
+          if (force_indefinite) arslam::debug_set_reduced_diag(P, d_S.p, hook_row, -1.0, stream);   // test hook
+          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 1);
         } else {
           arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false);
         }
@@ -866,6 +924,13 @@ void arslam_lm::solve(arslam_lm_summary *s) {
         arslam::launch_dense_back_solve_dag(plan, d_S.p, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false);
       else
         arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
+      if (nranks > 1) {
+        // y of the top columns (identical on every rank) and of each rank's
+        // own subtrees: summed with every other row zero -- exact, so every
+        // rank holds the same full y and the f-side update stays replicated
+        arslam::launch_mask_y(P, d_yF.p, rank, stream);
+        allreduce(d_yF.p, nR, ARSLAM_OP_SUM);
+      }
       timers[PH_SOLVE].stop(stream);
     }
     timers[PH_BACK].start(stream);
@@ -982,6 +1047,12 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->elimination_used = elim_used;
   s->ceres_e_captures = ceres_e_cap;
   s->ceres_e_tags = ceres_e_tag;
+  s->n_ranks = nranks;
+  s->n_owned_captures = nc;
+  s->n_top_tiles = nranks > 1 ? plan.n_top_tiles : 0;
+  s->split_top_work = split_top_work;
+  s->split_max_rank_work = split_max_rank_work;
+  s->split_total_work = split_total_work;
 }
 
 // ===========================================================================
@@ -1276,6 +1347,15 @@ int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks, const unsigned char i
       NCCL_CHECK(ncclCommInitRank(&h->comm, nranks, u, rank));
     }
   });
+}
+
+int arslam_lm_owned_captures(const arslam_lm *h, int *out, int cap, int *n) {
+  if (!h || !n || (cap > 0 && !out)) return ARSLAM_E_INVALID_ARG;
+  if (!h->loaded) return ARSLAM_E_STATE;
+  const int k = h->nranks > 1 ? (int)h->own_caps.size() : h->nc;
+  for (int i = 0; i < k && i < cap; ++i) out[i] = h->nranks > 1 ? h->own_caps[i] : i;
+  *n = k;
+  return ARSLAM_OK;
 }
 
 int arslam_device_count(void) {

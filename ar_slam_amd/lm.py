@@ -43,11 +43,12 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_num_residual_blocks", "arslam_lm_load_soa", "arslam_lm_solve_loaded",
            "arslam_lm_solve_soa", "arslam_comm_unique_id", "arslam_lm_set_comm", "arslam_lm_set_comm_callback",
            "arslam_device_count", "arslam_lm_last_error", "arslam_lm_version",
-           "arslam_lm_set_iteration_callback",
+           "arslam_lm_set_iteration_callback", "arslam_lm_owned_captures",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_break_dependency",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
+           "arslam_debug_rank_split",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
            "arslam_slam_create", "arslam_slam_destroy", "arslam_slam_set_verbose", "arslam_slam_load_yaml",
@@ -122,6 +123,9 @@ class Summary(C.Structure):
                 ("factor_update_flops", C.c_double), ("factor_scalar_flops", C.c_double),
                 ("comm_bytes", C.c_double),
                 ("elimination_used", C.c_int), ("ceres_e_captures", C.c_int), ("ceres_e_tags", C.c_int),
+                ("n_ranks", C.c_int), ("n_owned_captures", C.c_int), ("n_top_tiles", C.c_long),
+                ("split_top_work", C.c_double), ("split_max_rank_work", C.c_double),
+                ("split_total_work", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 
     def to_dict(self):
@@ -161,6 +165,8 @@ def lib():
     L.arslam_lm_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Options)]
     L.arslam_lm_set_comm_callback.argtypes = [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, C.c_void_p]
     L.arslam_lm_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
+    L.arslam_debug_rank_split.argtypes = [C.POINTER(SoaProblem), C.c_int, C.c_int, C.POINTER(SplitInfo), _ip]
+    L.arslam_lm_owned_captures.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int)]
     for fn in ("arslam_slam_destroy", "arslam_slam_set_verbose", "arslam_slam_load_yaml",
                "arslam_slam_load_yaml_string", "arslam_slam_save_yaml", "arslam_slam_add_detections",
                "arslam_slam_solve", "arslam_slam_solve_incremental", "arslam_slam_localize_many",
@@ -354,6 +360,14 @@ class ResidentProblem(_Handle):
         _check(lib().arslam_lm_solve_loaded(self._h, C.byref(s)))
         return s.to_dict()
 
+    def owned_captures(self):
+        """Indices of the captures this rank owns (every capture on one rank)."""
+        n = C.c_int(0)
+        _check(lib().arslam_lm_owned_captures(self._h, None, C.c_int(0), C.byref(n)))
+        out = (C.c_int * max(n.value, 1))()
+        _check(lib().arslam_lm_owned_captures(self._h, out, C.c_int(n.value), C.byref(n)))
+        return np.array(out[:n.value], np.int64)
+
     def debug_break_dependency(self, ticket):
         """Test hook: make one dependency wait of the factorization task graph unreachable."""
         out = C.c_long(-1)
@@ -472,6 +486,23 @@ def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const
     _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
                                            tag_row.ctypes.data_as(_ip)))
     return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]
+
+
+class SplitInfo(C.Structure):
+    _fields_ = [("tiles_per_side", C.c_int), ("n_top_cols", C.c_int), ("n_own_cols", C.c_int),
+                ("n_top_tiles", C.c_long), ("n_tiles", C.c_long), ("n_dag_tasks", C.c_long),
+                ("phase_split", C.c_long), ("dag_valid", C.c_int), ("n_owned_captures", C.c_int),
+                ("top_work", C.c_double), ("max_rank_work", C.c_double), ("total_work", C.c_double)]
+
+
+def debug_rank_split(camera, cap, tag, obs_cap, obs_tag, corners, nranks, rank):
+    """Host-only: the multi-rank split the solver makes for `rank` of `nranks` (two-phase tile
+    plan of that rank, its validity) and every capture's owner.  Returns (info dict, cap_owner)."""
+    A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners)
+    info = SplitInfo()
+    owner = np.zeros(max(A.cap.shape[0], 1), np.int32)
+    _check(lib().arslam_debug_rank_split(C.byref(A.s), nranks, rank, C.byref(info), owner.ctypes.data_as(_ip)))
+    return {f: getattr(info, f) for f, _ in SplitInfo._fields_}, owner[:A.cap.shape[0]]
 
 
 def debug_ceres_e_blocks(camera, cap, tag, obs_cap, obs_tag, corners=None, camera_const=False, cap_const=None,

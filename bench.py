@@ -13,10 +13,11 @@ resident initial state.
                  timed solves / wall time of the K solves (max over ranks)
   ms_per_step  = ms-to-converged of one solve
 
-Multi-GPU (torchrun, one process per GPU): captures are sharded in
-contiguous ranges; every step all-reduces the reduced tag+camera system over
-RCCL (the path has a real exchange step, so total work is fixed: strong
-scaling).
+Multi-GPU (torchrun, one process per GPU): every rank loads the whole
+problem and the solver splits the reduced system's elimination tree below its
+top separators; each rank factors its own subtrees (and owns their captures),
+then the top columns' tiles are summed over RCCL and factored on every rank
+(the path has a real exchange step, and total work is fixed: strong scaling).
 
 The JSON line also carries the dominant kernel's roofline (the MFMA fp64
 trailing update of the reduced-system Cholesky, timed with HIP events around
@@ -43,7 +44,8 @@ HBM_PEAK_GBS = 8000.0
 
 
 def shard_graph(g, rank, world):
-    """Contiguous capture range of this rank; all tags replicated."""
+    """Contiguous capture range of this rank; all tags replicated (the CPU oracle's sharded
+    restatement, tests/test_distributed.py; the GPU path splits the whole problem itself)."""
     lo = (g.n_cap * rank) // world
     hi = (g.n_cap * (rank + 1)) // world
     sel = (g.obs_cap >= lo) & (g.obs_cap < hi)
@@ -244,8 +246,9 @@ def main():
         return
     from ar_slam_amd import lm, synth
     g = synth.config_graph(args.config)
-    part = shard_graph(g, rank, world) if world > 1 else dict(
-        camera=g.camera, cap=g.cap, tag=g.tag, obs_cap=g.obs_cap, obs_tag=g.obs_tag, corners=g.corners)
+    # every rank loads the whole problem; the solver splits it (subtree-to-rank split of the
+    # reduced system's elimination tree: each rank owns the captures of its subtrees)
+    part = dict(camera=g.camera, cap=g.cap, tag=g.tag, obs_cap=g.obs_cap, obs_tag=g.obs_tag, corners=g.corners)
     comm = None
     if world > 1:
         obj = [lm.comm_unique_id() if rank == 0 else None]
@@ -333,7 +336,8 @@ def main():
             "config": {"workload": f"{args.config}: {g.n_cap} captures / {g.n_tag} tags / "
                                    f"{g.n_obs} observations (k=8), one full LM solve per step",
                        "n_obs": int(g.n_obs), "n_reduced": int(last["n_reduced"]),
-                       "parallelism": f"capture-shard x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"subtree split x{world} (RCCL all-reduce of the top tiles)"
+                                      if world > 1 else "single GPU"},
             "ms_to_converged": 1e3 * elapsed / args.steps,
             # the cold setup of the problem (first load: ordering, plan, upload), outside the timed
             # region, and the ms-to-converged a first Solve of a new problem would see
@@ -348,6 +352,9 @@ def main():
                                "ordering": ["natural", "RCM", "nested dissection"][args.ordering],
                                "executor": ["level launches", "persistent task graph"][args.executor],
                                "skip_zero_tiles": bool(args.skip_zero_tiles)},
+            "comm_mb_per_lm_iteration": last["comm_bytes"] / max(last["num_linear_solves"], 1) / 1e6,
+            "split": {k: last[k] for k in ("n_ranks", "n_owned_captures", "n_top_tiles", "split_top_work",
+                                           "split_max_rank_work", "split_total_work")},
             "phase_ms_per_solve": {k: phased[f"t_{k}_ms"] for k in
                                    ("linearize", "schur", "cholesky", "solve", "backsub", "cost")},
             "roofline": roofline,

@@ -140,6 +140,13 @@ typedef struct {
   int elimination_used;         /* ARSLAM_ELIM_CAPTURES or ARSLAM_ELIM_TAGS */
   int ceres_e_captures;         /* Ceres 2.0's e-block set for this problem (ComputeStableSchurOrdering): */
   int ceres_e_tags;             /*   captures and tags in it (the camera joins it only in degenerate graphs) */
+  /* several ranks (subtree-to-rank split of the reduced system's elimination tree) */
+  int n_ranks;
+  int n_owned_captures;         /* captures this rank owns (every capture on one rank) */
+  long n_top_tiles;             /* tiles of the replicated top columns: the per-step exchange is these */
+  double split_top_work;        /* tile tasks of the top columns (replicated on every rank) */
+  double split_max_rank_work;   /* tile tasks of the busiest rank's subtrees */
+  double split_total_work;      /* tile tasks of the whole factorization */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
 } arslam_lm_summary;
@@ -202,9 +209,14 @@ int arslam_lm_solve_loaded(arslam_lm *h, arslam_lm_summary *summary);
 int arslam_lm_solve_soa(arslam_soa_problem *p, const arslam_lm_options *opt,
                         arslam_lm_summary *summary);
 
-/* Multi-GPU (capture-sharded, one process per GPU): each rank loads the
- * observations of its capture shard plus every tag; the reduced tag+camera
- * system is all-reduced over RCCL every step. */
+/* Multi-GPU (one process per GPU): every rank loads the WHOLE problem (the
+ * same arslam_soa_problem / the same residual blocks) and the solver splits
+ * it: the elimination tree of the reduced tag+camera system is cut below its
+ * top separators, each rank owns some of the subtrees below the cut and the
+ * captures whose tags lie in them, factors those columns, and the ranks then
+ * sum only the top columns' tiles over RCCL before factoring the top
+ * (replicated).  Results are written back for the rank's own captures
+ * (arslam_lm_owned_captures) and for the camera and every tag. */
 int arslam_comm_unique_id(unsigned char id[ARSLAM_COMM_ID_BYTES]);
 int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks,
                        const unsigned char id[ARSLAM_COMM_ID_BYTES]);
@@ -219,6 +231,10 @@ enum { ARSLAM_DT_F64 = 0, ARSLAM_DT_U8 = 1 };
 enum { ARSLAM_OP_SUM = 0, ARSLAM_OP_MAX = 1 };
 typedef int (*arslam_allreduce_fn)(void *ctx, void *buf, size_t count, int dtype, int op);
 int arslam_lm_set_comm_callback(arslam_lm *h, int rank, int nranks, arslam_allreduce_fn fn, void *ctx);
+
+/* The captures (indices into the loaded problem) this rank owns, ascending;
+ * *n = their count (writes <= cap).  One rank owns every capture. */
+int arslam_lm_owned_captures(const arslam_lm *h, int *out, int cap, int *n);
 
 /* ceres::IterationCallback (Solver::Options::callbacks; the reference installs
  * one for its debug display, ar_slam_util.cpp:982-998, 1006-1009): called

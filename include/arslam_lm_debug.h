@@ -85,6 +85,23 @@ int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[4]);
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);
 
+/* Host only: the multi-rank split arslam_lm_load_soa makes for rank `rank` of
+ * `nranks` (nested dissection, sparse tiles) -- its two-phase tile plan, and
+ * every capture's owning rank (cap_owner[n_cap], may be NULL). */
+typedef struct {
+  int tiles_per_side;
+  int n_top_cols;           /* tile columns replicated on every rank */
+  int n_own_cols;           /* tile columns of this rank's subtrees */
+  long n_top_tiles;         /* tiles of the top columns (the per-step exchange) */
+  long n_tiles;             /* tiles stored on this rank (top + own) */
+  long n_dag_tasks, phase_split;   /* tasks of the plan; [0, phase_split) run before the exchange */
+  int dag_valid;            /* 1: ticket order valid and the randomised interleavings finish */
+  int n_owned_captures;
+  double top_work, max_rank_work, total_work;   /* tile-task counts (RankSplit) */
+} arslam_split_info;
+int arslam_debug_rank_split(const arslam_soa_problem *p, int nranks, int rank, arslam_split_info *info,
+                            int *cap_owner);
+
 #ifdef __cplusplus
 }
 #endif

@@ -143,3 +143,35 @@ def test_scalar_flops_match_symbolic_factorization(L, name):
     g = synth.config_graph(name)
     info, tag_row = _plan(L, g)
     assert info["scalar_flops"] == pytest.approx(_brute_force_scalar_flops(g, tag_row), rel=1e-12)
+
+
+@pytest.mark.parametrize("name,worlds", [("medium", [2, 3]), ("cfg2", [2, 3, 4, 8]), ("cfg3", [2, 4, 8])])
+def test_rank_split_partitions_the_factorization(L, name, worlds):
+    """The multi-GPU split (arslam::rank_split, llt_plan_symbolic with column classes): every rank
+    derives the same capture owners from the whole problem; the ranks' subtree columns and the
+    replicated top columns partition the tile columns; each rank's two-phase task graph (its
+    subtrees before the exchange, the top after it) is deadlock-free; and the exchange -- the
+    top columns' tiles -- is a small part of the factor (cfg3 at 2 ranks: 55 of 2,461 tiles,
+    where the replicated path all-reduced the 1,535 assembled ones)."""
+    g = synth.config_graph(name)
+    single, _ = _plan(L, g)
+    for world in worlds:
+        infos, owners = [], None
+        for r in range(world):
+            info, own = L.debug_rank_split(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, world, r)
+            infos.append(info)
+            if owners is None:
+                owners = own
+            np.testing.assert_array_equal(own, owners)
+            assert info["dag_valid"] == 1, (world, r, info)
+            assert 0 < info["phase_split"] <= info["n_dag_tasks"] or info["n_own_cols"] == 0
+        assert owners.min() >= 0 and owners.max() < world
+        assert [int((owners == r).sum()) for r in range(world)] == [i["n_owned_captures"] for i in infos]
+        T = single["tiles_per_side"]
+        assert infos[0]["n_top_cols"] + sum(i["n_own_cols"] for i in infos) == T
+        assert all(i["n_top_tiles"] == infos[0]["n_top_tiles"] for i in infos)
+        if name != "medium":   # (a 36-tile graph split 3 ways is mostly top)
+            assert infos[0]["n_top_tiles"] < 0.5 * single["n_factor_tiles"]
+    if name == "cfg3":
+        info, _ = L.debug_rank_split(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, 2, 0)
+        assert info["n_top_tiles"] <= 100 and info["n_top_tiles"] * 32768 < 4e6
