@@ -421,6 +421,11 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
       deg[p->n_tag] = p->n_obs;
     };
     h = arslam::host_problem(&pl, global_deg);
+    // the layout's tag slots are the whole problem's (3 + 6 nc_full + 6 t + a):
+    // renumber them for this rank's parameter vector (3 + 6 nc_own + 6 t + a)
+    const long shift = 6L * (p->n_cap - (long)own_caps.size());
+    for (int &sl : L.row_slot)
+      if (sl >= 3) sl -= (int)shift;
   } else {
     h = arslam::host_problem(p, nullptr);   // validates p
     L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
