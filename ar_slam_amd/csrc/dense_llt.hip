@@ -341,9 +341,14 @@ __device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *L
 // idle(p, w, lane) runs on waves 1-3 beside wave 0's diagonal block p (after
 // their share of the trailing update): the persistent executor fetches its
 // fused TRSM's tile there.
+// F (optional): a 64x64 tile in LDS (pitch LQ) whose product F F^T is first
+// subtracted from D -- the last update of the diagonal tile, folded into the
+// factorization: wave 0 folds block (0,0) and goes straight on to its
+// diag16 while waves 1-3 fold the other nine lower blocks beside it (the
+// same MFMA products in the same order as a separate fold: bit-identical).
 template <class Idle>
 __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *bad, int tid, double *colx,
-                                     Idle &&idle) {
+                                     Idle &&idle, const double *F = nullptr) {
   const int w = tid >> 6, lane = tid & 63;
   if (tid == 0) *bad = 0;
   __syncthreads();
@@ -351,9 +356,19 @@ __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *b
     const int b0 = 16 * p;
     STAMP(10 + 4 * p);
     if (w == 0) {
+      if (p == 0 && F) wave_gemm16_sub(D, F, F, 64, lane);
       if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
       diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane, colx);
     } else if (p == 0) {
+      if (F) {
+        // lower blocks 1..9 in row order (I, C), I >= C: (1,0) (1,1) (2,0) (2,1) (2,2) (3,0) ...
+        for (int t = w; t < 10; t += 3) {
+          int I = 0;
+          while ((I + 1) * (I + 2) / 2 <= t) ++I;
+          const int C = t - I * (I + 1) / 2;
+          wave_gemm16_sub(D + 16 * I * LQ + 16 * C, F + 16 * I * LQ, F + 16 * C * LQ, 64, lane);
+        }
+      }
       idle(0, w, lane);
     } else {
       // panel p-1's update of blocks (I, C), I >= C >= p, except (p, p)
@@ -377,6 +392,88 @@ __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *b
     STAMP(12 + 4 * p);
     STAMP(13 + 4 * p);
   }
+  return *bad == 0;
+}
+
+// LDS flags of the asynchronous panel pipeline below (one workgroup)
+__device__ __forceinline__ void lds_set(int *f, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  *reinterpret_cast<volatile int *>(f) = v;
+}
+__device__ __forceinline__ void lds_add(int *f, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait(const int *f, int v) {
+  while (*reinterpret_cast<const volatile int *>(f) < v) __builtin_amdgcn_s_sleep(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// The same factorization (same products in the same order: bit-identical) as
+// blocked_potrf64_idle, without workgroup barriers on wave 0's chain.  Wave 0
+// runs diag16(p) -> the next block's apply (p+1, p) -> the lookahead update of
+// (p+1, p+1) -> diag16(p+1) ...; waves 1-3 apply the blocks further down and
+// do the trailing updates of each panel (and the optional fold F F^T) beside
+// it, synchronised through LDS counters: fl[0] = panels whose diagonal block is
+// factored and next block applied (wave 0), fl[1] = applies done by waves 1-3,
+// fl[2] = update rounds done by waves 1-3 (round 0 the fold, round p+1 panel
+// p's trailing updates; three increments per round).  idle(p, w, lane) runs
+// on waves 1-3 after round p (as beside panel p in the barrier version).
+template <class Idle>
+__device__ bool blocked_potrf64_async(double *D, double *inv, double *LTd, int *bad, int *fl, int tid,
+                                      double *colx, Idle &&idle, const double *F = nullptr) {
+  const int w = tid >> 6, lane = tid & 63;
+  if (tid == 0) {
+    *bad = 0;
+    fl[0] = fl[1] = fl[2] = 0;
+  }
+  __syncthreads();
+  if (w == 0) {
+    for (int p = 0; p < 4; ++p) {
+      const int b0 = 16 * p;
+      if (p == 0 && F) wave_gemm16_sub(D, F, F, 64, lane);
+      if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
+      if (p > 0) lds_wait(fl + 2, 3 * p);   // rounds 0 .. p-1: the fold and panels 0 .. p-2
+      diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane, colx);
+      if (p < 3) {
+        lds_wait(fl + 2, 3 * (p + 1));      // round p: block (p+1, p) has panel p-1's update
+        wave_apply_inv16(D + (b0 + 16) * LQ + b0, LTd + p * 16 * LI, lane);
+        lds_set(fl, p + 1);
+      }
+    }
+  } else {
+    if (F) {
+      // the fold's lower blocks 1..9 in row order (I, C), I >= C: (1,0) (1,1) (2,0) (2,1) ...
+      for (int t = w; t < 10; t += 3) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int C = t - I * (I + 1) / 2;
+        wave_gemm16_sub(D + 16 * I * LQ + 16 * C, F + 16 * I * LQ, F + 16 * C * LQ, 64, lane);
+      }
+    }
+    idle(0, w, lane);
+    lds_add(fl + 2, lane);
+    for (int p = 0; p < 3; ++p) {
+      const int b0 = 16 * p;
+      lds_wait(fl, p + 1);                  // L_pp's block inverse, block (p+1, p) applied
+      if (w < 3 - p - 1 + 1 && p + 1 + w <= 3)   // blocks (p+2 .. 3, p): wave w takes p + 1 + w
+        wave_apply_inv16(D + (b0 + 16 * (1 + w)) * LQ + b0, LTd + p * 16 * LI, lane);
+      lds_add(fl + 1, lane);
+      lds_wait(fl + 1, 3 * (p + 1));        // every block of panel p applied
+      // panel p's update of blocks (I, C), I >= C >= p + 1, except (p + 1, p + 1)
+      const int m = 3 - p, ntl = m * (m + 1) / 2;
+      for (int t = w; t < ntl; t += 3) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int C = t - I * (I + 1) / 2;
+        const int bi = 16 * (p + 1 + I), bc = 16 * (p + 1 + C);
+        wave_gemm16_sub(D + bi * LQ + bc, D + bi * LQ + b0, D + bc * LQ + b0, 16, lane);
+      }
+      idle(p + 1, w, lane);
+      lds_add(fl + 2, lane);
+    }
+  }
+  __syncthreads();
   return *bad == 0;
 }
 
@@ -714,6 +811,33 @@ __device__ __forceinline__ void ld_wt16x8(const double *const p[8], dbl2 v[8]) {
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
       : "memory");
 }
+// sixteen 16-byte sc1 loads p[k] -> v[k], waited
+__device__ __forceinline__ void ld_wt16x16(const double *const p[16], dbl2 v[16]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %16, off sc1\n\t"
+      "global_load_dwordx4 %1, %17, off sc1\n\t"
+      "global_load_dwordx4 %2, %18, off sc1\n\t"
+      "global_load_dwordx4 %3, %19, off sc1\n\t"
+      "global_load_dwordx4 %4, %20, off sc1\n\t"
+      "global_load_dwordx4 %5, %21, off sc1\n\t"
+      "global_load_dwordx4 %6, %22, off sc1\n\t"
+      "global_load_dwordx4 %7, %23, off sc1\n\t"
+      "global_load_dwordx4 %8, %24, off sc1\n\t"
+      "global_load_dwordx4 %9, %25, off sc1\n\t"
+      "global_load_dwordx4 %10, %26, off sc1\n\t"
+      "global_load_dwordx4 %11, %27, off sc1\n\t"
+      "global_load_dwordx4 %12, %28, off sc1\n\t"
+      "global_load_dwordx4 %13, %29, off sc1\n\t"
+      "global_load_dwordx4 %14, %30, off sc1\n\t"
+      "global_load_dwordx4 %15, %31, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
+        "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]),
+        "=&v"(v[15])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]), "v"(p[8]),
+        "v"(p[9]), "v"(p[10]), "v"(p[11]), "v"(p[12]), "v"(p[13]), "v"(p[14]), "v"(p[15])
+      : "memory");
+}
 // eight 8-byte sc1 loads, waited
 __device__ __forceinline__ void ld_wt8x8(const double *const p[8], double v[8]) {
   asm volatile(
@@ -742,6 +866,25 @@ __device__ __forceinline__ void load_tile_wt(const double *__restrict__ g, doubl
   for (int q = 0; q < 8; ++q) {
     const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
     *reinterpret_cast<dbl2 *>(lds + r * LQ + c2) = v[q];
+  }
+}
+
+// two tiles at once (both sets of sc1 loads in flight before either is stored)
+__device__ __forceinline__ void load_two_tiles_wt(const double *__restrict__ g1, double *lds1,
+                                                  const double *__restrict__ g2, double *lds2, int tid) {
+  const double *p[16];
+  dbl2 v[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    p[q] = g1 + 2 * (q * 256 + tid);
+    p[8 + q] = g2 + 2 * (q * 256 + tid);
+  }
+  ld_wt16x16(p, v);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
+    *reinterpret_cast<dbl2 *>(lds1 + r * LQ + c2) = v[q];
+    *reinterpret_cast<dbl2 *>(lds2 + r * LQ + c2) = v[8 + q];
   }
 }
 
@@ -855,11 +998,12 @@ __device__ __forceinline__ unsigned long long realtime() {
 
 __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
-  __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 4 + T64];
+  __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 8 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
-  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [5] fused TRSM tile prefetched
+  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [5] fused TRSM tile prefetched,
+  // [6] its fetch requested, [8..10] the POTRF pipeline's flags
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
-  double *colx = LTd + 4 * 16 * LI + 4;   // POTRF pivot scratch (X stays free for the prefetch)
+  double *colx = LTd + 4 * 16 * LI + 8;   // POTRF pivot scratch (X stays free for the prefetch)
   int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.ticket;
   // claimed continuation targets in flight.  A target is claimed once its
   // EARLY waits are all drawn; its late waits may name undrawn tickets, so at
@@ -943,9 +1087,18 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // needs; the early waits are met here, the late ones come after)
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (task.z >= 0) {
+      const int4 fit = task.z >= 0 ? a.items[task.z] : make_int4(0, 0, 0, 0);
+      // a one-column folded update runs inside the factorization (fold_f: its
+      // L_kj tile in X -- the predecessor's solved tile for a continuation,
+      // else loaded beside A_kk); several columns fold first, as one GEMM pass
+      const bool fold_in = task.z >= 0 && fit.z - fit.y == 1;
+      if (fold_in) {
+        const double *Akk = tile_ptr(a.S, a.tid_map, a.T, k, k);
+        if (cont && a.ks[fit.y] == pk) load_tile_wt(Akk, D, tid);
+        else load_two_tiles_wt(Akk, D, tile_ptr(a.S, a.tid_map, a.T, k, a.ks[fit.y]), X, tid);
+      } else if (task.z >= 0) {
         // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
-        const int4 it = a.items[task.z];
+        const int4 it = fit;
         dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
         // A_kk (final: the task's waits are met) straight into the MFMA
         // accumulator layout, sc1 loads in flight during the fold's GEMMs
@@ -995,7 +1148,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // the tile's last update lands a few microseconds into the POTRF
       // (cfg3 k_factor_dag 758 -> 736 us).
       if (tid == 0) sh[6] = 0;
-      const bool ok = blocked_potrf64_idle(D, inv, LTd, sh + 1, tid, colx, [&](int p, int wv, int ln) {
+      const bool ok = blocked_potrf64_async(D, inv, LTd, sh + 1, sh + 8, tid, colx, [&](int p, int wv, int ln) {
         auto poll = [&]() {
           if (!pf_src || pw1 - pw0 > 64) return false;
           const int q = pw0 + ln;
@@ -1008,6 +1161,13 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         if (p == 0) {
           if (wv != 1) return;
           const bool met = poll();
+          if (fold_in) {   // X still holds the fold's operand: fetch beside panel 1 instead
+            if (ln == 0) {
+              sh[5] = 0;
+              if (met) sh[6] = -1;
+            }
+            return;
+          }
           if (met) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
@@ -1045,7 +1205,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           }
           if (wv == 1 && ln == 0) sh[5] = 1;
         }
-      });
+      }, fold_in ? X : nullptr);
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();

@@ -142,7 +142,7 @@ struct Timer {
   }
 };
 
-enum { PH_LIN, PH_SCHUR, PH_CHOL, PH_SOLVE, PH_BACK, PH_COST, PH_N };
+enum { PH_LIN, PH_SCHUR, PH_CHOL, PH_SOLVE, PH_BACK, PH_COST, PH_FAC0, PH_FAC1, PH_N };
 
 }  // namespace
 
@@ -886,11 +886,15 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           // tiles (its share of the top's Schur complement); then the top tiles
           // are summed over the ranks -- the step's one bulk exchange -- and
           // every rank factors the top columns (phase 1) on identical inputs
+          timers[PH_FAC0].start(stream);
           arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 0);
+          timers[PH_FAC0].stop(stream);
           allreduce(d_S.p, (size_t)plan.n_top_tiles * 4096, ARSLAM_OP_SUM);
           arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream, 1);
           if (force_indefinite) arslam::debug_set_reduced_diag(P, d_S.p, hook_row, -1.0, stream);   // test hook
+          timers[PH_FAC1].start(stream);
           arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 1);
+          timers[PH_FAC1].stop(stream);
         } else {
           arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false);
         }
@@ -1040,6 +1044,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->t_solve_ms = timers[PH_SOLVE].acc_ms;
   s->t_backsub_ms = timers[PH_BACK].acc_ms;
   s->t_cost_ms = timers[PH_COST].acc_ms;
+  s->t_factor_own_ms = timers[PH_FAC0].acc_ms;
+  s->t_factor_top_ms = timers[PH_FAC1].acc_ms;
   s->t_dominant_ms = dom_ms;
   s->dominant_flops = dom_flops;
   s->n_dominant_launches = dom_launches;
