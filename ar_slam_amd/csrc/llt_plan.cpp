@@ -98,7 +98,9 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   // chain needs, and a schedule that budgets for that draws the chain tasks
   // ahead of them (cfg3 k_factor_dag 720 -> ~688 us with 16 + 16 per column;
   // flat from 12 + 12 to 20 + 12, worse at 24 + 24; round-2 sweeps).
-  const double cc[7] = {16.0, 4.0, 5.0, 6.0, 16.0, 16.0, 5.0};
+  double cc[7] = {16.0, 4.0, 5.0, 6.0, 16.0, 16.0, 5.0};
+  if (const char *e = std::getenv("ARSLAM_SIM_COST"))   // debug: list-schedule cost sweeps (tools/sim_sweep.sh)
+    std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf,%lf", &cc[0], &cc[1], &cc[2], &cc[3], &cc[4], &cc[5], &cc[6]);
   for (int v = 0; v < n; ++v) {
     const DagNode &nd = nodes[v];
     pr.clear();

@@ -109,6 +109,52 @@ struct PinnedBuf {
   }
 };
 
+// The problem's uploaded arrays: one grow-only device allocation, one
+// page-locked host image, one host->device copy per load (instead of a
+// pageable copy and a driver staging pass per array).
+struct UploadArena {
+  char *dev = nullptr, *host = nullptr;
+  size_t dev_cap = 0, host_cap = 0;
+  struct Piece { void **dst; const void *src; size_t bytes, off; };
+  std::vector<Piece> pieces;
+  template <class T>
+  void add(T **dst, const T *src, size_t count) { pieces.push_back({reinterpret_cast<void **>(dst), src, count * sizeof(T), 0}); }
+  // lay the pieces out, copy them into the host image and enqueue the one
+  // transfer; the sources may go out of scope once this returns, the image
+  // stays untouched until the caller's next stream sync
+  void commit(hipStream_t s) {
+    size_t used = 0;
+    for (Piece &p : pieces) {
+      p.off = used;
+      used += (std::max<size_t>(p.bytes, 1) + 255) & ~size_t(255);
+    }
+    if (used > host_cap) {
+      if (host) (void)hipHostFree(host);
+      host = nullptr;
+      host_cap = 0;
+      HIP_CHECK(hipHostMalloc(&host, used + used / 2, hipHostMallocDefault));
+      host_cap = used + used / 2;
+    }
+    if (used > dev_cap) {
+      if (dev) (void)hipFree(dev);
+      dev = nullptr;
+      dev_cap = 0;
+      HIP_CHECK(hipMalloc(&dev, used + used / 2));
+      dev_cap = used + used / 2;
+    }
+    for (Piece &p : pieces) {
+      if (p.bytes) std::memcpy(host + p.off, p.src, p.bytes);
+      *p.dst = dev + p.off;
+    }
+    if (used) HIP_CHECK(hipMemcpyAsync(dev, host, used, hipMemcpyHostToDevice, s));
+    pieces.clear();
+  }
+  ~UploadArena() {
+    if (dev) (void)hipFree(dev);
+    if (host) (void)hipHostFree(host);
+  }
+};
+
 struct Timer {
   hipEvent_t a = nullptr, b = nullptr;
   double acc_ms = 0.0;
@@ -176,19 +222,23 @@ struct arslam_lm {
   hipStream_t stream = nullptr;
   int device = 0;
 
-  DevBuf<int> d_cap_start, d_obs_tag, d_obs_lblk, d_cap_blk_start, d_blk_tag, d_tag_start, d_tag_obs;
-  DevBuf<unsigned char> d_obs_active, d_slot_free;
-  DevBuf<double> d_corners, d_x0, d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
+  // uploaded arrays (pointers into `upload`, re-laid out by every load)
+  UploadArena upload;
+  int *u_cap_start = nullptr, *u_obs_tag = nullptr, *u_obs_lblk = nullptr, *u_cap_blk_start = nullptr,
+      *u_blk_tag = nullptr, *u_tag_start = nullptr, *u_tag_obs = nullptr, *u_tag_row = nullptr,
+      *u_row_slot = nullptr, *u_fslot_row = nullptr, *u_dest_start = nullptr;
+  unsigned char *u_obs_active = nullptr, *u_slot_free = nullptr;
+  double *u_corners = nullptr, *u_x0 = nullptr;
+  long *u_cap_off = nullptr;
+  int2 *u_dest_row = nullptr;
+  int4 *u_gather_items = nullptr, *u_gather_splits = nullptr;
+  arslam::SchurContrib *u_contrib = nullptr;
+  DevBuf<double> d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_S, d_z, d_yF;
   double *d_norms_p = nullptr;   // inside d_red
-  DevBuf<int> d_flag, d_tag_row, d_row_slot, d_fslot_row;
-  DevBuf<long> d_cap_off;
+  DevBuf<int> d_flag;
   DevBuf<double> d_slab, d_jrows, d_cap_ui;
-  DevBuf<int2> d_dest_row;
-  DevBuf<int4> d_gather_items, d_gather_splits;
   DevBuf<double> d_gather_part;
-  DevBuf<int> d_dest_start;
-  DevBuf<arslam::SchurContrib> d_contrib;
   arslam::LltPlan plan;
   double *x = nullptr, *xc = nullptr;
   unsigned long long dbg_indefinite_mask = 0;   // arslam_lm_debug_force_indefinite
@@ -285,6 +335,11 @@ struct arslam_lm {
   }
 
   void load(const arslam_soa_problem *p);
+  void upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L);
+  bool try_extend(const arslam_soa_problem *p);
+  arslam::ReducedLayout lay;      // the loaded layout (one rank), kept for try_extend
+  bool pk_appended_only = false;  // since the last load only residual blocks of known tags were added
+  int setup_kind = ARSLAM_SETUP_LOAD;
   int elim_used = ARSLAM_ELIM_CAPTURES;   // the side load() eliminates (the device problem is role-swapped for TAGS)
   int ceres_e_cap = 0, ceres_e_tag = 0;   // Ceres 2.0's e-block set of the loaded problem, by kind
   void reload_values(const arslam_soa_problem *p);
@@ -441,17 +496,10 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   nb_global = h.nb_global;
   slot_free = h.slot_free;
   x0 = h.x0;
-  const int maxk = h.maxk;
   prev_tag_row = L.tag_row;
   prev_order_edges = L.order_edges;
   prev_ordering = opt.reduced_ordering;
   prev_skip = opt.cholesky_skip_zero_tiles;
-  const std::vector<int> &cap_start = h.cap_start, &obs_tag = h.obs_tag, &obs_lblk = h.obs_lblk,
-                         &cap_blk_start = h.cap_blk_start, &blk_tag = h.blk_tag, &tag_start = h.tag_start,
-                         &tag_obs = h.tag_obs, &tag_row = L.tag_row, &row_slot = L.row_slot;
-  const std::vector<double> &corners = h.corners;
-  const std::vector<unsigned char> &obs_active = h.obs_active;
-  const int cam_row = L.cam_row;
   tp[2] = now_s();
   scalar_flops = L.scalar_flops;
   nR = L.nR;
@@ -464,19 +512,61 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
     arslam::llt_plan_free(plan);
   }
   tp[3] = now_s();
+  tp[4] = now_s();
+  upload_problem(h, L);
+  tp[5] = now_s();
+  if (nranks == 1) lay = std::move(L);   // (try_extend: an appended problem keeps this layout and plan)
+  setup_kind = ARSLAM_SETUP_LOAD;
+  soa = *p;
+  loaded = true;
+  pk_appended_only = true;
+  setup_s = now_s() - t_load;
+  if (prof)
+    std::fprintf(stderr, "arslam setup: nc %d nt %d host+layout %.3f plan %.3f gather+upload %.3f ms\n",
+                 nc, nt, 1e3 * (tp[1] - tp[0]), 1e3 * (tp[3] - tp[2]), 1e3 * (tp[5] - tp[4]));
+}
 
-  // ---- device upload ----
-  d_cap_start.alloc(nc + 1); d_cap_start.upload(cap_start.data(), nc + 1, stream);
-  d_obs_tag.alloc(nb); d_obs_tag.upload(obs_tag.data(), nb, stream);
-  d_obs_lblk.alloc(nb); d_obs_lblk.upload(obs_lblk.data(), nb, stream);
-  d_cap_blk_start.alloc(nc + 1); d_cap_blk_start.upload(cap_blk_start.data(), nc + 1, stream);
-  d_blk_tag.alloc(std::max<size_t>(blk_tag.size(), 1)); d_blk_tag.upload(blk_tag.data(), blk_tag.size(), stream);
-  d_tag_start.alloc(nt + 1); d_tag_start.upload(tag_start.data(), nt + 1, stream);
-  d_tag_obs.alloc(std::max(nb, 1)); d_tag_obs.upload(tag_obs.data(), nb, stream);
-  d_obs_active.alloc(std::max(nb, 1)); d_obs_active.upload(obs_active.data(), nb, stream);
-  d_slot_free.alloc(n); d_slot_free.upload(slot_free.data(), n, stream);
-  d_corners.alloc(std::max(8L * nb, 1L)); d_corners.upload(corners.data(), 8L * nb, stream);
-  d_x0.alloc(n); d_x0.upload(x0.data(), n, stream);
+// Everything the device needs from the host structure, the layout and the
+// Schur gather plan, in one upload (UploadArena), plus the scratch buffers
+// sized for the problem.  Ends with the load's one stream sync.
+void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L) {
+  const int maxk = h.maxk;
+  const std::vector<int> &row_slot = L.row_slot;
+  // f-side slot -> reduced row (camera slots 0..2, then the tag slots)
+  std::vector<int> fslot_row(3 + 6L * nt, -1);
+  for (size_t r = 0; r < row_slot.size(); ++r) {
+    const long sl = row_slot[r];
+    if (sl < 0) continue;
+    if (sl < 3) fslot_row[sl] = (int)r;
+    else if (sl >= 3 + 6L * nc) fslot_row[sl - 6L * nc] = (int)r;
+  }
+  arslam::SchurGather sg;
+  if (has_f) sg = arslam::schur_gather_plan(h, L);
+  const int n_dest = has_f ? (int)sg.dest_start.size() - 1 : 0;
+  const int n_items = (int)sg.items.size() / 4, n_splits = (int)sg.splits.size() / 4;
+  upload.add(&u_cap_start, h.cap_start.data(), nc + 1);
+  upload.add(&u_obs_tag, h.obs_tag.data(), nb);
+  upload.add(&u_obs_lblk, h.obs_lblk.data(), nb);
+  upload.add(&u_cap_blk_start, h.cap_blk_start.data(), nc + 1);
+  upload.add(&u_blk_tag, h.blk_tag.data(), h.blk_tag.size());
+  upload.add(&u_tag_start, h.tag_start.data(), nt + 1);
+  upload.add(&u_tag_obs, h.tag_obs.data(), nb);
+  upload.add(&u_obs_active, h.obs_active.data(), nb);
+  upload.add(&u_slot_free, h.slot_free.data(), n);
+  upload.add(&u_corners, h.corners.data(), 8L * nb);
+  upload.add(&u_x0, x0.data(), n);
+  upload.add(&u_tag_row, L.tag_row.data(), L.tag_row.size());
+  upload.add(&u_row_slot, row_slot.data(), row_slot.size());
+  upload.add(&u_fslot_row, fslot_row.data(), fslot_row.size());
+  if (has_f) {
+    upload.add(&u_cap_off, sg.cap_off.data(), nc + 1);
+    upload.add(&u_dest_row, reinterpret_cast<const int2 *>(sg.dest_row.data()), n_dest);
+    upload.add(&u_dest_start, sg.dest_start.data(), n_dest + 1);
+    upload.add(&u_contrib, sg.contrib.data(), sg.contrib.size());
+    upload.add(&u_gather_items, reinterpret_cast<const int4 *>(sg.items.data()), n_items);
+    upload.add(&u_gather_splits, reinterpret_cast<const int4 *>(sg.splits.data()), n_splits);
+  }
+  upload.commit(stream);
   d_xa.alloc(n); d_xb.alloc(n); d_xbest.alloc(n);
   d_g.alloc(n); d_colnorm.alloc(n); d_scale.alloc(n); d_diag.alloc(n);
   d_obs_tg.alloc(std::max(12L * nb, 1L));
@@ -486,47 +576,14 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   n_fparts = (int)((std::max(nR, 1L) + 255) / 256);
   d_fparts.alloc(2L * std::max(n_fparts, 1));
   // stays zero when there are no reduced rows (k_update_f is then not launched)
-  HIP_CHECK(hipMemsetAsync(d_fparts.p, 0, d_fparts.n * sizeof(double), stream));
+  if (!has_f) HIP_CHECK(hipMemsetAsync(d_fparts.p, 0, d_fparts.n * sizeof(double), stream));
   d_red.alloc(16 + 8 + 6 * 64);   // LM scalars | slot norms: results + k_slot_norms block partials
   d_norms_p = d_red.p + 16;       // (one D2H carries both after a linearization)
   d_flag.alloc(1);
-  d_tag_row.alloc(tag_row.size()); d_tag_row.upload(tag_row.data(), tag_row.size(), stream);
-  d_row_slot.alloc(std::max<size_t>(row_slot.size(), 1)); d_row_slot.upload(row_slot.data(), row_slot.size(), stream);
-  {
-    // f-side slot -> reduced row (camera slots 0..2, then the tag slots)
-    std::vector<int> fslot_row(3 + 6L * nt, -1);
-    for (size_t r = 0; r < row_slot.size(); ++r) {
-      const long sl = row_slot[r];
-      if (sl < 0) continue;
-      if (sl < 3) fslot_row[sl] = (int)r;
-      else if (sl >= 3 + 6L * nc) fslot_row[sl - 6L * nc] = (int)r;
-    }
-    d_fslot_row.alloc(fslot_row.size());
-    d_fslot_row.upload(fslot_row.data(), fslot_row.size(), stream);
-    HIP_CHECK(hipStreamSynchronize(stream));   // (the host vector goes out of scope)
-  }
-  int n_dest = 0, n_items = 0, n_splits = 0;
   if (has_f) {
-    tp[4] = now_s();
-    const arslam::SchurGather sg = arslam::schur_gather_plan(h, L);
-    tp[5] = now_s();
-    n_dest = (int)sg.dest_start.size() - 1;
-    d_cap_off.alloc(nc + 1); d_cap_off.upload(sg.cap_off.data(), nc + 1, stream);
     d_slab.alloc(std::max(sg.cap_off[nc], 1L));
-    d_dest_row.alloc(std::max(n_dest, 1));
-    d_dest_row.upload(reinterpret_cast<const int2 *>(sg.dest_row.data()), n_dest, stream);
-    d_dest_start.alloc(n_dest + 1); d_dest_start.upload(sg.dest_start.data(), n_dest + 1, stream);
-    d_contrib.alloc(std::max<size_t>(sg.contrib.size(), 1)); d_contrib.upload(sg.contrib.data(), sg.contrib.size(), stream);
-    n_items = (int)sg.items.size() / 4;
-    n_splits = (int)sg.splits.size() / 4;
-    d_gather_items.alloc(std::max(n_items, 1));
-    d_gather_items.upload(reinterpret_cast<const int4 *>(sg.items.data()), n_items, stream);
-    d_gather_splits.alloc(std::max(n_splits, 1));
-    d_gather_splits.upload(reinterpret_cast<const int4 *>(sg.splits.data()), n_splits, stream);
     d_gather_part.alloc(36L * std::max(sg.n_pslots, 1));
-    HIP_CHECK(hipStreamSynchronize(stream));   // sg's host buffers go out of scope
-    d_S.alloc((size_t)plan.n_tiles * 4096);
-    HIP_CHECK(hipMemsetAsync(d_S.p, 0, d_S.n * sizeof(double), stream));
+    d_S.alloc((size_t)plan.n_tiles * 4096);   // (cleared by k_schur's extra blocks every step)
     d_z.alloc(N);
     d_yF.alloc(N);
   } else {
@@ -536,30 +593,80 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   }
   HIP_CHECK(hipMemsetAsync(d_parts.p, 0, d_parts.n * sizeof(double), stream));
 
-  P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nR = nR; P.N = N; P.lda = N; P.cam_row = cam_row;
+  P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nR = nR; P.N = N; P.lda = N; P.cam_row = L.cam_row;
   P.max_obs_per_cap = std::max(maxk, 1);
   P.swap_roles = elim_used == ARSLAM_ELIM_TAGS ? 1 : 0;
   P.nf = 3 + 6 * nt;
-  P.fslot_row = d_fslot_row.p;
-  P.cap_start = d_cap_start.p; P.obs_tag = d_obs_tag.p; P.obs_lblk = d_obs_lblk.p;
-  P.cap_blk_start = d_cap_blk_start.p; P.blk_tag = d_blk_tag.p;
-  P.obs_active = d_obs_active.p; P.slot_free = d_slot_free.p;
-  P.tag_start = d_tag_start.p; P.tag_obs = d_tag_obs.p; P.corners = d_corners.p;
-  P.tag_row = d_tag_row.p; P.row_slot = d_row_slot.p;
+  P.fslot_row = u_fslot_row;
+  P.cap_start = u_cap_start; P.obs_tag = u_obs_tag; P.obs_lblk = u_obs_lblk;
+  P.cap_blk_start = u_cap_blk_start; P.blk_tag = u_blk_tag;
+  P.obs_active = u_obs_active; P.slot_free = u_slot_free;
+  P.tag_start = u_tag_start; P.tag_obs = u_tag_obs; P.corners = u_corners;
+  P.tag_row = u_tag_row; P.row_slot = u_row_slot;
   P.tile_id = plan.tile_id; P.T = plan.T;
   P.tile_class = nranks > 1 && has_f ? plan.tile_class : nullptr;
-  P.cap_off = d_cap_off.p; P.slab = d_slab.p; P.dest_row = d_dest_row.p; P.dest_start = d_dest_start.p;
-  P.contrib = d_contrib.p; P.n_dest = n_dest; P.jrows = d_jrows.p; P.cap_ui = d_cap_ui.p;
-  P.gather_items = d_gather_items.p; P.gather_splits = d_gather_splits.p; P.gather_part = d_gather_part.p;
+  P.cap_off = u_cap_off; P.slab = d_slab.p; P.dest_row = u_dest_row; P.dest_start = u_dest_start;
+  P.contrib = u_contrib; P.n_dest = n_dest; P.jrows = d_jrows.p; P.cap_ui = d_cap_ui.p;
+  P.gather_items = u_gather_items; P.gather_splits = u_gather_splits; P.gather_part = d_gather_part.p;
   P.n_items = n_items; P.n_splits = n_splits;
-  HIP_CHECK(hipStreamSynchronize(stream));
+  HIP_CHECK(hipStreamSynchronize(stream));   // the upload's sources go out of scope
+}
+
+// An appended problem (arslam_lm_solve after AddResidualBlock only, no new
+// tag, no constant changed): if every capture's tile pairs are already in the
+// loaded tile pattern, the reduced layout, the elimination order and the whole
+// factorization plan stay as they are -- only the capture side, the gather
+// plan and the values are rebuilt and uploaded.  false: load() instead.
+bool arslam_lm::try_extend(const arslam_soa_problem *p) {
+  if (!loaded || nranks > 1 || elim_used != ARSLAM_ELIM_CAPTURES || !has_f || opt.elimination == ARSLAM_ELIM_TAGS)
+    return false;
+  const double t0 = now_s();
+  if (opt.elimination == ARSLAM_ELIM_AUTO) {   // the side Ceres would eliminate may change as the graph grows
+    const arslam::SchurSide cs = arslam::ceres_schur_side(p);
+    if (cs.e_tag > cs.e_cap && cs.max_tag_obs <= arslam::kMaxObsPerCapture) return false;
+    ceres_e_cap = cs.e_cap;
+    ceres_e_tag = cs.e_tag;
+  }
+  if (p->n_tag != nt) return false;
+  arslam::HostProblem h = arslam::host_problem(p, nullptr);
+  // the same free tags and camera (the same reduced rows)
+  if ((lay.cam_row >= 0) != (h.slot_free[0] != 0)) return false;
+  for (int t = 0; t < nt; ++t)
+    if ((lay.tag_row[t] >= 0) != (h.slot_free[3 + 6L * h.nc + 6L * t] != 0)) return false;
+  // every capture's tiles pairwise in the loaded (assembled) pattern
+  const int T = lay.T;
+  std::vector<int> ts;
+  for (int c = 0; c < h.nc; ++c) {
+    ts.clear();
+    if (lay.cam_row >= 0) {
+      ts.push_back(lay.cam_row / 64);
+      ts.push_back((lay.cam_row + 2) / 64);
+    }
+    for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a) {
+      const int r0 = lay.tag_row[h.blk_tag[a]];
+      if (r0 < 0) continue;
+      ts.push_back(r0 / 64);
+      ts.push_back((r0 + 5) / 64);
+    }
+    for (size_t a = 0; a < ts.size(); ++a)
+      for (size_t b = 0; b < ts.size(); ++b)
+        if (ts[a] >= ts[b] && !lay.pattern[(size_t)ts[a] * T + ts[b]]) return false;
+  }
+  // the tag slots move with the capture count
+  for (int &sl : lay.row_slot)
+    if (sl >= 3) sl += 6 * (h.nc - nc);
+  nc = h.nc;
+  nb = h.nb;
+  n = h.n;
+  nb_global = h.nb_global;
+  slot_free = h.slot_free;
+  x0 = h.x0;
+  upload_problem(h, lay);
   soa = *p;
-  loaded = true;
-  setup_s = now_s() - t_load;
-  if (prof)
-    std::fprintf(stderr, "arslam setup: nc %d nt %d host %.3f layout %.3f plan %.3f upload %.3f gather %.3f rest %.3f ms\n",
-                 nc, nt, 1e3 * (tp[1] - tp[0]), 1e3 * (tp[2] - tp[1]), 1e3 * (tp[3] - tp[2]),
-                 1e3 * (tp[4] - tp[3]), 1e3 * (tp[5] - tp[4]), 1e3 * (now_s() - tp[5]));
+  pk_appended_only = true;
+  setup_kind = ARSLAM_SETUP_APPEND;
+  setup_s = now_s() - t0;
+  return true;
 }
 
 // Same structure as the loaded problem, new parameter values (the pointer-keyed
@@ -577,9 +684,10 @@ void arslam_lm::reload_values(const arslam_soa_problem *p_in) {
     std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
   }
   if (nt) std::memcpy(x0.data() + 3 + 6L * nc, p->tag, 6L * nt * sizeof(double));
-  d_x0.upload(x0.data(), n, stream);
+  HIP_CHECK(hipMemcpyAsync(u_x0, x0.data(), n * sizeof(double), hipMemcpyHostToDevice, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
   soa = *p;
+  setup_kind = ARSLAM_SETUP_VALUES;
   setup_s = now_s() - t0;
 }
 
@@ -707,10 +815,11 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->n_obs = nb;
   s->n_reduced = has_f ? (int)nR : 0;
   s->setup_time_s = setup_s;
+  s->setup_kind = setup_kind;
   x = d_xa.p;
   xc = d_xb.p;
-  HIP_CHECK(hipMemcpyAsync(x, d_x0.p, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
-  HIP_CHECK(hipMemcpyAsync(d_xbest.p, d_x0.p, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(x, u_x0, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(d_xbest.p, u_x0, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
   const bool root = rank == 0;
   if (o.minimizer_progress_to_stdout && root) print_header();
   // the patched dependency of arslam_lm_debug_break_dependency lasts one solve
@@ -1197,6 +1306,7 @@ int arslam_lm_add_residual_block(arslam_lm *h, const double corners[8], double *
     } else {
       t = ti->second;
     }
+    if (ti == h->tag_of.end()) h->pk_appended_only = false;   // a new tag: new reduced rows
     h->pk_dirty = true;
     h->pk_obs_cap.push_back(c);
     h->pk_obs_tag.push_back(t);
@@ -1209,14 +1319,14 @@ int arslam_lm_set_parameter_block_constant(arslam_lm *h, double *block) {
   return guarded([&] {
     fail_if(block != h->camera_ptr && !h->cap_of.count(block) && !h->tag_of.count(block),
             ARSLAM_E_INVALID_ARG, "parameter block is not part of the problem");
-    if (h->constant.insert(block).second) h->pk_dirty = true;
+    if (h->constant.insert(block).second) h->pk_dirty = true, h->pk_appended_only = false;
   });
 }
 
 int arslam_lm_set_parameter_block_variable(arslam_lm *h, double *block) {
   if (!h || !block) return ARSLAM_E_INVALID_ARG;
   return guarded([&] {
-    if (h->constant.erase(block)) h->pk_dirty = true;
+    if (h->constant.erase(block)) h->pk_dirty = true, h->pk_appended_only = false;
   });
 }
 
@@ -1256,6 +1366,8 @@ int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
     } stage_guard{h};
     if (h->loaded && h->pk_loaded && !h->pk_dirty) {
       h->reload_values(&p);   // same problem, new values: no host rebuild, no re-upload of observations
+    } else if (h->loaded && h->pk_loaded && h->pk_appended_only && h->try_extend(&p)) {
+      h->pk_dirty = false;    // appended residual blocks within the loaded tile pattern: layout and plan kept
     } else {
       h->reuse_order = h->pk_loaded;   // a grown pointer-keyed problem (not the first load)
       h->load(&p);

@@ -64,6 +64,7 @@ _dp = C.POINTER(C.c_double)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
 SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = 0, 1, 2
 ELIM_AUTO, ELIM_CAPTURES, ELIM_TAGS = 0, 1, 2   # arslam_lm_options.elimination
+SETUP_LOAD, SETUP_VALUES, SETUP_APPEND = 0, 1, 2   # arslam_lm_summary.setup_kind
 _ip = C.POINTER(C.c_int)
 _up = C.POINTER(C.c_ubyte)
 
@@ -112,7 +113,7 @@ class Summary(C.Structure):
                 ("initial_cost", C.c_double), ("final_cost", C.c_double),
                 ("fixed_cost", C.c_double), ("final_rms_px", C.c_double),
                 ("n_obs", C.c_int), ("n_reduced", C.c_int),
-                ("setup_time_s", C.c_double), ("minimizer_time_s", C.c_double),
+                ("setup_time_s", C.c_double), ("setup_kind", C.c_int), ("minimizer_time_s", C.c_double),
                 ("total_time_s", C.c_double),
                 ("t_linearize_ms", C.c_double), ("t_schur_ms", C.c_double),
                 ("t_cholesky_ms", C.c_double), ("t_solve_ms", C.c_double),
@@ -125,7 +126,8 @@ class Summary(C.Structure):
                 ("elimination_used", C.c_int), ("ceres_e_captures", C.c_int), ("ceres_e_tags", C.c_int),
                 ("n_ranks", C.c_int), ("n_owned_captures", C.c_int), ("n_top_tiles", C.c_long),
                 ("split_top_work", C.c_double), ("split_max_rank_work", C.c_double),
-                ("split_total_work", C.c_double),
+                ("split_total_work", C.c_double), ("t_factor_own_ms", C.c_double),
+                ("t_factor_top_ms", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
 
     def to_dict(self):

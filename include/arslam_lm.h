@@ -63,6 +63,11 @@ enum { ARSLAM_ELIM_AUTO = 0, ARSLAM_ELIM_CAPTURES = 1, ARSLAM_ELIM_TAGS = 2 };
 enum { ARSLAM_CONVERGENCE = 0, ARSLAM_NO_CONVERGENCE = 1, ARSLAM_FAILURE = 2, ARSLAM_USER_SUCCESS = 3,
        ARSLAM_USER_FAILURE = 4 };
 
+/* summary.setup_kind: a full load (structure, elimination order, plan), the
+ * loaded problem with new values only, or an appended problem whose new
+ * residual blocks fit the loaded tile pattern (order and plan kept) */
+enum { ARSLAM_SETUP_LOAD = 0, ARSLAM_SETUP_VALUES = 1, ARSLAM_SETUP_APPEND = 2 };
+
 /* which termination test fired */
 enum {
   ARSLAM_RULE_NONE = 0, ARSLAM_RULE_GRADIENT = 1, ARSLAM_RULE_PARAMETER = 2,
@@ -121,6 +126,7 @@ typedef struct {
   double final_rms_px;          /* sqrt(2 final_cost / (4 n_obs)) */
   int n_obs, n_reduced;         /* residual blocks; size of the reduced (tag+camera) system */
   double setup_time_s;          /* host assembly + upload */
+  int setup_kind;               /* ARSLAM_SETUP_*: how the problem reached the device for this solve */
   double minimizer_time_s;      /* first evaluation to termination */
   double total_time_s;
   /* accumulated device time per phase (ms), from HIP events */
@@ -147,6 +153,8 @@ typedef struct {
   double split_top_work;        /* tile tasks of the top columns (replicated on every rank) */
   double split_max_rank_work;   /* tile tasks of the busiest rank's subtrees */
   double split_total_work;      /* tile tasks of the whole factorization */
+  double t_factor_own_ms;       /* device time of the factorization's phase 0 (own subtrees) and */
+  double t_factor_top_ms;       /*   phase 1 (the top), summed over the solve (phase_timing = 1) */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
 } arslam_lm_summary;

@@ -152,6 +152,62 @@ def test_pointer_api_resolve_reuses_the_resident_problem(lm):
     assert s4["setup_time_s"] > s2["setup_time_s"]
 
 
+def test_appended_problem_keeps_plan_and_matches_a_fresh_load(lm, oracle):
+    """solveIncremental's growth (ar_slam_util.cpp:720-736): residual blocks of new captures that
+    see only known tags are appended to the resident problem.  When their tile pairs are in the
+    loaded pattern the layout, elimination order and factorization plan are kept
+    (setup_kind APPEND: only the capture side, the gather plan and the values are uploaded), and
+    the solve gives the trace a fresh load of the grown problem gives, and the oracle's."""
+    g = synth.config_graph("cfg2")
+    camera = g.camera.copy()
+    caps = [g.cap[c].copy() for c in range(g.n_cap)]
+    tags = [g.tag[t].copy() for t in range(g.n_tag)]
+    prob = lm.Problem(elimination=lm.ELIM_CAPTURES)
+    first = 700
+    seen = set()
+    for b in range(g.n_obs):
+        if g.obs_cap[b] < first:
+            prob.add_residual_block(g.corners[b], camera, caps[g.obs_cap[b]], tags[g.obs_tag[b]])
+            seen.add(int(g.obs_tag[b]))
+    s1 = prob.solve()
+    assert s1["setup_kind"] == lm.SETUP_LOAD
+    # append the later captures whose tags are all known
+    added = [c for c in range(first, g.n_cap) if set(g.obs_tag[g.obs_cap == c].tolist()) <= seen][:20]
+    assert len(added) >= 5
+    for c in added:
+        for b in np.nonzero(g.obs_cap == c)[0]:
+            prob.add_residual_block(g.corners[b], camera, caps[c], tags[g.obs_tag[b]])
+    start = (camera.copy(), [c.copy() for c in caps], [t.copy() for t in tags])
+    s2 = prob.solve()
+    assert s2["setup_kind"] == lm.SETUP_APPEND, s2["setup_kind"]
+    assert s2["setup_time_s"] < s1["setup_time_s"]
+    # a fresh problem of the same blocks, from the same values
+    fresh = lm.Problem(elimination=lm.ELIM_CAPTURES)
+    cam_f, caps_f, tags_f = start[0].copy(), [c.copy() for c in start[1]], [t.copy() for t in start[2]]
+    order = [b for b in range(g.n_obs) if g.obs_cap[b] < first] + \
+        [b for c in added for b in np.nonzero(g.obs_cap == c)[0]]
+    for b in order:
+        fresh.add_residual_block(g.corners[b], cam_f, caps_f[g.obs_cap[b]], tags_f[g.obs_tag[b]])
+    s3 = fresh.solve()
+    assert s3["setup_kind"] == lm.SETUP_LOAD
+    assert [i["step_is_successful"] for i in s2["iterations"]] == [i["step_is_successful"] for i in s3["iterations"]]
+    for a, b in zip(s2["iterations"], s3["iterations"]):
+        assert abs(a["cost"] - b["cost"]) <= 1e-9 * b["cost"]
+    assert abs(camera[0] - cam_f[0]) <= 1e-8 * cam_f[0]
+    # and the oracle on the grown problem from the same start
+    cap_ids = sorted({int(g.obs_cap[b]) for b in order})
+    cpos = {c: i for i, c in enumerate(cap_ids)}
+    tag_ids = sorted({int(g.obs_tag[b]) for b in order})
+    tpos = {t: i for i, t in enumerate(tag_ids)}
+    _, _, _, so = oracle.solve(start[0].copy(), np.array([start[1][c] for c in cap_ids]),
+                               np.array([start[2][t] for t in tag_ids]),
+                               np.array([cpos[int(g.obs_cap[b])] for b in order], np.int32),
+                               np.array([tpos[int(g.obs_tag[b])] for b in order], np.int32),
+                               g.corners[order])
+    assert so["termination"] == s2["termination"]
+    assert abs(so["final_cost"] - s2["final_cost"]) <= 1e-8 * so["final_cost"]
+
+
 def test_localize_constant_map(lm, oracle):
     """localizeOne: tags and camera constant (ar_slam_util.cpp:965,972), one free capture each."""
     g = synth.config_graph("medium")
