@@ -1035,6 +1035,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // and runs it at once, the folded tile still in LDS.  Otherwise the
   // workgroup that drew the target claims and runs it once its waits are met.
   int next = -1, prev_k = -1;
+  bool next_met = false;   // a claimed continuation whose early waits were already seen met
   for (;;) {
     // thread coordinates re-derived per task from a laundered threadIdx: the
     // per-lane LDS/tile addresses of every task type are then computed where
@@ -1053,8 +1054,10 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     }
     const int t = next;
     const int pk = prev_k;   // a claimed continuation: the predecessor's column (its L_{k,pk} is in X)
+    const bool premet = next_met;
     next = -1;
     prev_k = -1;
+    next_met = false;
     DAG_PROGRESS(0, t);
     DAG_PROGRESS(1, 1);
     if (t >= a.t_end) break;
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     if (w == 0) {
       // (sub.y: the end of the early waits; the late ones are a fused TRSM's,
       // or a folded TRSM's L_kk)
-      const bool ok = dag_wait(a.counters, a.waits, a.wait_off[t], sub.y, a.flag, lane, task.x != 2);
+      const bool ok = premet || dag_wait(a.counters, a.waits, a.wait_off[t], sub.y, a.flag, lane, task.x != 2);
       if (lane == 0) {
         if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
         // a drawn continuation target: run it only if its predecessor did not claim it
@@ -1233,25 +1236,52 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         }
         const int c = a.cont[t];
         double *Ct = a.S + (long)sub.x * (T64 * T64);
+        // The continuation claim's round trips ride along the solve instead of
+        // following it: the ticket count and the in-flight reservation go out
+        // now; the claim itself (after the solve) answers during the tile's
+        // store; wave 0's other lanes poll the target's early waits, so a
+        // claimed target whose waits were already met skips its own poll.
+        int tk_seen = 0, infl_old = 0;
+        bool c_met = false;
+        if (c >= 0 && w == 0) {
+          if (lane == 0) {
+            tk_seen = ld_acquire_relaxed(ticket);
+            infl_old = atomicAdd(inflight, 1);
+          }
+          const int cw0 = a.wait_off[c], cw1 = a.sub[c].y;
+          if (cw1 - cw0 <= 63) {
+            const int q = cw0 + lane - 1;
+            bool open = false;
+            if (lane >= 1 && q < cw1) {
+              const int2 cv = a.waits[q];   // (the tile this task publishes below counts as met)
+              open = cv.x != sub.x && ld_acquire_relaxed(a.counters + cv.x) < cv.y;
+            }
+            c_met = __builtin_amdgcn_ballot_w64(open) == 0;
+          }
+        }
         if (!pref) load_tile_wt(Ct, X, tid);
         __syncthreads();
         blocked_trsm64(X, D, inv, LTd, tid);
+        // claim the continuation target before the tile is published: its
+        // drawer waits for this tile, so it cannot have claimed it yet
+        int claim = -1;
+        if (c >= 0 && tid == 0) {
+          if (a.t_begin + tk_seen > a.maxdep[c] && infl_old < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0)
+            claim = c;
+          else
+            atomicSub(inflight, 1);
+        }
         store_tile_wt(Ct, X, tid, false);
         dag_release(tid);
         if (tid == 0) {
-          // claim the continuation target first: its drawer waits for this
-          // tile, so it cannot have claimed it yet
-          int claim = -1;
-          if (c >= 0 && a.t_begin + ld_acquire_relaxed(ticket) > a.maxdep[c]) {
-            if (atomicAdd(inflight, 1) < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0) claim = c;
-            else atomicSub(inflight, 1);
-          }
           sh[4] = claim;
+          sh[7] = c_met ? 1 : 0;
           __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
         __syncthreads();
         next = sh[4];
+        next_met = sh[7] != 0;
         if (next >= 0) prev_k = k;
       }
     } else if (task.x == 3) {

@@ -88,10 +88,12 @@ def bench_incremental(name="cfg2"):
     n = s.num_solves
     sums = [s.solve_summary(i) for i in range(n)]
     setup = sum(d["setup_time_s"] for d in sums)
+    kinds = [sum(d["setup_kind"] == k for d in sums) for k in range(3)]
     mini = sum(d["minimizer_time_s"] for d in sums)
     return {"flow": f"solveIncremental on {name} ({g.n_cap} captures / {g.n_tag} tags), one message per capture",
             "wall_s": wall, "solves": n, "lm_iterations": sum(d["num_linear_solves"] for d in sums),
             "setup_ms_per_solve": 1e3 * setup / n, "minimizer_ms_per_solve": 1e3 * mini / n,
+            "setup_kinds": {"full load": kinds[0], "values only": kinds[1], "appended (plan kept)": kinds[2]},
             "final_rms_px": sums[-1]["final_rms_px"]}
 
 

@@ -27,8 +27,10 @@ wall = time.perf_counter() - t0
 n = s.num_solves
 setup = mini = 0.0
 iters = 0
+kinds = [0, 0, 0]
 for i in range(n):
     d = s.solve_summary(i)
+    kinds[d["setup_kind"]] += 1
     setup += d["setup_time_s"]
     mini += d["minimizer_time_s"]
     iters += d["num_linear_solves"]
@@ -37,4 +39,5 @@ print(json.dumps({"flow": f"solveIncremental, {name}: {g.n_cap} captures / {g.n_
                   "wall_s": wall, "solves": n, "lm_iterations": iters,
                   "setup_ms_per_solve": 1e3 * setup / n, "minimizer_ms_per_solve": 1e3 * mini / n,
                   "other_ms_per_solve": 1e3 * (wall - setup - mini) / n,
+                  "setup_kinds": {"load": kinds[0], "values": kinds[1], "append": kinds[2]},
                   "final_rms_px": last["final_rms_px"], "final_termination": last["termination"]}))
