@@ -838,6 +838,95 @@ __device__ __forceinline__ void ld_wt16x16(const double *const p[16], dbl2 v[16]
         "v"(p[9]), "v"(p[10]), "v"(p[11]), "v"(p[12]), "v"(p[13]), "v"(p[14]), "v"(p[15])
       : "memory");
 }
+// 11 16-byte sc1 loads p[k] -> v[k] in one batch, waited
+__device__ __forceinline__ void ld_wt16x11(const double *const p[11], dbl2 v[11]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %11, off sc1\n\t"
+      "global_load_dwordx4 %1, %12, off sc1\n\t"
+      "global_load_dwordx4 %2, %13, off sc1\n\t"
+      "global_load_dwordx4 %3, %14, off sc1\n\t"
+      "global_load_dwordx4 %4, %15, off sc1\n\t"
+      "global_load_dwordx4 %5, %16, off sc1\n\t"
+      "global_load_dwordx4 %6, %17, off sc1\n\t"
+      "global_load_dwordx4 %7, %18, off sc1\n\t"
+      "global_load_dwordx4 %8, %19, off sc1\n\t"
+      "global_load_dwordx4 %9, %20, off sc1\n\t"
+      "global_load_dwordx4 %10, %21, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]), "v"(p[8]), "v"(p[9]), "v"(p[10])
+      : "memory");
+}
+// 19 16-byte sc1 loads p[k] -> v[k] in one batch, waited
+__device__ __forceinline__ void ld_wt16x19(const double *const p[19], dbl2 v[19]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %19, off sc1\n\t"
+      "global_load_dwordx4 %1, %20, off sc1\n\t"
+      "global_load_dwordx4 %2, %21, off sc1\n\t"
+      "global_load_dwordx4 %3, %22, off sc1\n\t"
+      "global_load_dwordx4 %4, %23, off sc1\n\t"
+      "global_load_dwordx4 %5, %24, off sc1\n\t"
+      "global_load_dwordx4 %6, %25, off sc1\n\t"
+      "global_load_dwordx4 %7, %26, off sc1\n\t"
+      "global_load_dwordx4 %8, %27, off sc1\n\t"
+      "global_load_dwordx4 %9, %28, off sc1\n\t"
+      "global_load_dwordx4 %10, %29, off sc1\n\t"
+      "global_load_dwordx4 %11, %30, off sc1\n\t"
+      "global_load_dwordx4 %12, %31, off sc1\n\t"
+      "global_load_dwordx4 %13, %32, off sc1\n\t"
+      "global_load_dwordx4 %14, %33, off sc1\n\t"
+      "global_load_dwordx4 %15, %34, off sc1\n\t"
+      "global_load_dwordx4 %16, %35, off sc1\n\t"
+      "global_load_dwordx4 %17, %36, off sc1\n\t"
+      "global_load_dwordx4 %18, %37, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15]), "=&v"(v[16]), "=&v"(v[17]), "=&v"(v[18])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]), "v"(p[8]), "v"(p[9]), "v"(p[10]), "v"(p[11]), "v"(p[12]), "v"(p[13]), "v"(p[14]), "v"(p[15]), "v"(p[16]), "v"(p[17]), "v"(p[18])
+      : "memory");
+}
+// A 64x64 tile g1 -> lds1 (and g2 -> lds2 if given) and a column's 16x16
+// block inverses ltd_g -> LTd (1152 doubles): every sc1 load in flight at
+// once, one round trip instead of one per array
+__device__ __forceinline__ void load_tiles_ltd_wt(const double *__restrict__ g1, double *lds1,
+                                                  const double *__restrict__ g2, double *lds2,
+                                                  const double *__restrict__ ltd_g, double *LTd, int tid) {
+  constexpr int kL = kLtdSize / 2;   // 16-byte elements of the block inverses (576)
+  const double *p[19];
+  dbl2 v[19];
+  const int nt = g2 ? 16 : 8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    p[q] = g1 + 2 * (q * 256 + tid);
+    p[8 + q] = (g2 ? g2 : g1) + 2 * (q * 256 + tid);
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int e = tid + 256 * u;
+    p[16 + u] = ltd_g + 2 * (e < kL ? e : 0);
+  }
+  if (g2) {
+    ld_wt16x19(p, v);
+  } else {
+    const double *p11[11] = {p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[16], p[17], p[18]};
+    dbl2 v11[11];
+    ld_wt16x11(p11, v11);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = v11[q];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) v[16 + u] = v11[8 + u];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
+    *reinterpret_cast<dbl2 *>(lds1 + r * LQ + c2) = v[q];
+    if (nt == 16) *reinterpret_cast<dbl2 *>(lds2 + r * LQ + c2) = v[8 + q];
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int e = tid + 256 * u;
+    if (e < kL) *reinterpret_cast<dbl2 *>(LTd + 2 * e) = v[16 + u];
+  }
+}
 // eight 8-byte sc1 loads, waited
 __device__ __forceinline__ void ld_wt8x8(const double *const p[8], double v[8]) {
   asm volatile(
@@ -1054,7 +1143,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     }
     const int t = next;
     const int pk = prev_k;   // a claimed continuation: the predecessor's column (its L_{k,pk} is in X)
-    const bool premet = next_met;
+    const bool premet = cont && next_met;   // (only for the claimed target it was polled for)
     next = -1;
     prev_k = -1;
     next_met = false;
@@ -1281,29 +1370,13 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
         __syncthreads();
         next = sh[4];
-        next_met = sh[7] != 0;
+        next_met = next >= 0 && sh[7] != 0;
         if (next >= 0) prev_k = k;
       }
     } else if (task.x == 3) {
       // ---- INV k: L_kk^{-1} for the backward solve (off the critical chain) ----
       const int k = task.y;
-      load_tile_wt(a.Ld + (long)k * T64 * T64, D, tid);
-      {
-        const double *ltd_g = a.ltd + (long)k * kLtdSize;
-        const double *p8[8];
-        dbl2 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = tid + 256 * u;
-          p8[u] = ltd_g + 2 * (e < kLtdSize / 2 ? e : 0);
-        }
-        ld_wt16x8(p8, v);
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const int e = tid + 256 * u;
-          if (e < kLtdSize / 2) *reinterpret_cast<dbl2 *>(LTd + 2 * e) = v[u];
-        }
-      }
+      load_tiles_ltd_wt(a.Ld + (long)k * T64 * T64, D, nullptr, nullptr, a.ltd + (long)k * kLtdSize, LTd, tid);
       __syncthreads();
       blocked_trinv64(D, LTd, X, tid);
       __syncthreads();
@@ -1317,24 +1390,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // ---- TRSM i,k: L_ik L_kk^T = A_ik, blocked with the 16x16 inverses ----
       const int i = task.y, k = task.z;
       double *Ct = tile_ptr(a.S, a.tid_map, a.T, i, k);
-      load_tile_wt(Ct, X, tid);
-      load_tile_wt(a.Ld + (long)k * T64 * T64, D, tid);
-      {
-        const double *ltd_g = a.ltd + (long)k * kLtdSize;
-        const double *p8[8];
-        dbl2 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = tid + 256 * u;
-          p8[u] = ltd_g + 2 * (e < kLtdSize / 2 ? e : 0);
-        }
-        ld_wt16x8(p8, v);
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const int e = tid + 256 * u;
-          if (e < kLtdSize / 2) *reinterpret_cast<dbl2 *>(LTd + 2 * e) = v[u];
-        }
-      }
+      // the tile, L_kk and its block inverses in one round trip
+      load_tiles_ltd_wt(Ct, X, a.Ld + (long)k * T64 * T64, D, a.ltd + (long)k * kLtdSize, LTd, tid);
       __syncthreads();
       if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
       blocked_trsm64(X, D, inv, LTd, tid);
@@ -1360,8 +1417,10 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           }
           __syncthreads();
         }
-        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tid);
-        if (ti != tj) load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, tj, k), X, tid);
+        if (ti != tj)   // both operands in one round trip
+          load_two_tiles_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tile_ptr(a.S, a.tid_map, a.T, tj, k), X, tid);
+        else
+          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tid);
         __syncthreads();
         gemm64_nt(D, ti != tj ? X : D, tid, acc);   // a diagonal target: one operand tile, fetched once
       }

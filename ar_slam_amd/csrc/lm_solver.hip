@@ -613,10 +613,13 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
 }
 
 // An appended problem (arslam_lm_solve after AddResidualBlock only, no new
-// tag, no constant changed): if every capture's tile pairs are already in the
-// loaded tile pattern, the reduced layout, the elimination order and the whole
-// factorization plan stay as they are -- only the capture side, the gather
-// plan and the values are rebuilt and uploaded.  false: load() instead.
+// tag, no constant changed): if every capture's tile pairs are tiles of the
+// loaded factor (assembled or fill: k_schur clears every tile of S each step
+// and the gather addresses any of them), the reduced layout, the elimination
+// order and the whole factorization plan stay as they are -- only the capture
+// side, the gather plan and the values are rebuilt and uploaded.  false:
+// load() instead.  (summary.factor_scalar_flops keeps the loaded problem's
+// count: a new coupling inside a fill tile changes the scalar structure.)
 bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   if (!loaded || nranks > 1 || elim_used != ARSLAM_ELIM_CAPTURES || !has_f || opt.elimination == ARSLAM_ELIM_TAGS)
     return false;
@@ -633,8 +636,9 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   if ((lay.cam_row >= 0) != (h.slot_free[0] != 0)) return false;
   for (int t = 0; t < nt; ++t)
     if ((lay.tag_row[t] >= 0) != (h.slot_free[3 + 6L * h.nc + 6L * t] != 0)) return false;
-  // every capture's tiles pairwise in the loaded (assembled) pattern
+  // every capture's tiles pairwise in the loaded factor's tiles
   const int T = lay.T;
+  std::vector<std::pair<int, int>> grown;   // fill tiles that become assembled
   std::vector<int> ts;
   for (int c = 0; c < h.nc; ++c) {
     ts.clear();
@@ -650,8 +654,12 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
     }
     for (size_t a = 0; a < ts.size(); ++a)
       for (size_t b = 0; b < ts.size(); ++b)
-        if (ts[a] >= ts[b] && !lay.pattern[(size_t)ts[a] * T + ts[b]]) return false;
+        if (ts[a] >= ts[b] && !lay.pattern[(size_t)ts[a] * T + ts[b]]) {
+          if (plan.h_tile_id[(size_t)ts[a] * T + ts[b]] < 0) return false;
+          grown.emplace_back(ts[a], ts[b]);
+        }
   }
+  for (const auto &g : grown) lay.pattern[(size_t)g.first * T + g.second] = 1;
   // the tag slots move with the capture count
   for (int &sl : lay.row_slot)
     if (sl >= 3) sl += 6 * (h.nc - nc);

@@ -171,8 +171,18 @@ def test_appended_problem_keeps_plan_and_matches_a_fresh_load(lm, oracle):
             seen.add(int(g.obs_tag[b]))
     s1 = prob.solve()
     assert s1["setup_kind"] == lm.SETUP_LOAD
-    # append the later captures whose tags are all known
-    added = [c for c in range(first, g.n_cap) if set(g.obs_tag[g.obs_cap == c].tolist()) <= seen][:20]
+    # append later captures whose tags are all known and were seen together before (their
+    # blocks of the reduced system are then tiles of the loaded factor)
+    pairs = set()
+    for c in range(first):
+        ts = sorted(set(g.obs_tag[g.obs_cap == c].tolist()))
+        pairs.update((a, b) for a in ts for b in ts if a < b)
+    added = []
+    for c in range(first, g.n_cap):
+        ts = sorted(set(g.obs_tag[g.obs_cap == c].tolist()))
+        if set(ts) <= seen and all((a, b) in pairs for a in ts for b in ts if a < b):
+            added.append(c)
+    added = added[:20]
     assert len(added) >= 5
     for c in added:
         for b in np.nonzero(g.obs_cap == c)[0]:
