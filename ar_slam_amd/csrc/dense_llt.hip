@@ -341,7 +341,7 @@ __device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *L
 // idle(p, w, lane) runs on waves 1-3 beside wave 0's diagonal block p (after
 // their share of the trailing update): the persistent executor fetches its
 // fused TRSM's tile there.
-// F (optional): a 64x64 tile in LDS (pitch LQ) whose product F F^T is first
+// F (with fold / non-null): a 64x64 tile in LDS (pitch LQ) whose product F F^T is first
 // subtracted from D -- the last update of the diagonal tile, folded into the
 // factorization: wave 0 folds block (0,0) and goes straight on to its
 // diag16 while waves 1-3 fold the other nine lower blocks beside it (the
@@ -395,17 +395,23 @@ __device__ bool blocked_potrf64_idle(double *D, double *inv, double *LTd, int *b
   return *bad == 0;
 }
 
-// LDS flags of the asynchronous panel pipeline below (one workgroup)
+// LDS flags of the asynchronous panel pipeline below (one workgroup).  The
+// volatile accesses go through LDS-typed pointers: a volatile access through a
+// generic pointer stays a flat access (the address space is not inferred),
+// and hipcc mis-selects the aperture compare of some of those.
+typedef __attribute__((address_space(3))) volatile int lds_vint;
+__device__ __forceinline__ lds_vint *as_lds(const int *f) { return (lds_vint *)(f); }
 __device__ __forceinline__ void lds_set(int *f, int v) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  *reinterpret_cast<volatile int *>(f) = v;
+  *as_lds(f) = v;
 }
 __device__ __forceinline__ void lds_add(int *f, int lane) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (lane == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+__device__ __forceinline__ int lds_get(const int *f) { return *as_lds(f); }
 __device__ __forceinline__ void lds_wait(const int *f, int v) {
-  while (*reinterpret_cast<const volatile int *>(f) < v) __builtin_amdgcn_s_sleep(0);
+  while (*as_lds(f) < v) __builtin_amdgcn_s_sleep(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -421,17 +427,17 @@ __device__ __forceinline__ void lds_wait(const int *f, int v) {
 // on waves 1-3 after round p (as beside panel p in the barrier version).
 template <class Idle>
 __device__ bool blocked_potrf64_async(double *D, double *inv, double *LTd, int *bad, int *fl, int tid,
-                                      double *colx, Idle &&idle, const double *F = nullptr) {
+                                      double *colx, Idle &&idle, const double *F = nullptr, bool fold = false) {
   const int w = tid >> 6, lane = tid & 63;
   if (tid == 0) {
     *bad = 0;
-    fl[0] = fl[1] = fl[2] = 0;
+    fl[0] = fl[1] = fl[2] = fl[3] = 0;   // (fl[3]: the caller's prefetch count)
   }
   __syncthreads();
   if (w == 0) {
     for (int p = 0; p < 4; ++p) {
       const int b0 = 16 * p;
-      if (p == 0 && F) wave_gemm16_sub(D, F, F, 64, lane);
+      if (p == 0 && fold) wave_gemm16_sub(D, F, F, 64, lane);
       if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
       if (p > 0) lds_wait(fl + 2, 3 * p);   // rounds 0 .. p-1: the fold and panels 0 .. p-2
       diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane, colx);
@@ -442,7 +448,7 @@ __device__ bool blocked_potrf64_async(double *D, double *inv, double *LTd, int *
       }
     }
   } else {
-    if (F) {
+    if (fold) {
       // the fold's lower blocks 1..9 in row order (I, C), I >= C: (1,0) (1,1) (2,0) (2,1) ...
       for (int t = w; t < 10; t += 3) {
         int I = 0;
@@ -481,6 +487,20 @@ __device__ bool blocked_potrf64(double *D, double *inv, double *LTd, int *bad, i
   return blocked_potrf64_idle(D, inv, LTd, bad, tid, colx, [](int, int, int) {});
 }
 
+// Column step p of the blocked solve X L^T = A for row block rb of X (one
+// wave): X[rb, p] -= X[rb, 0:p] L[p, 0:p]^T, then X[rb, p] <- X[rb, p] L_pp^{-T}.
+__device__ __forceinline__ void trsm_step(double *X, const double *D, const double *LTd, int rb, int p, int lane) {
+  const int b0 = 16 * p;
+  if (p > 0) wave_gemm16_sub(X + 16 * rb * LQ + b0, X + 16 * rb * LQ, D + b0 * LQ, b0, lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_apply_inv16(X + 16 * rb * LQ + b0, LTd + p * 16 * LI, lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // In-LDS blocked solve X L^T = A for a 64x64 tile X (256 threads), L from
 // blocked_potrf64 (lower part of D, inv = 1 / diag).
 __device__ void blocked_trsm64(double *X, const double *D, const double *inv, const double *LTd,
@@ -488,18 +508,7 @@ __device__ void blocked_trsm64(double *X, const double *D, const double *inv, co
   // row block w of X depends only on itself (and on D, LTd): the four
   // column steps need wave-local ordering only; one barrier at the end
   const int w = tid >> 6, lane = tid & 63;
-  for (int p = 0; p < 4; ++p) {
-    const int b0 = 16 * p;
-    if (p > 0)   // X[:, b0:b0+16] -= X[:, 0:b0] L[b0:b0+16, 0:b0]^T  (wave w: rows 16w..)
-      wave_gemm16_sub(X + 16 * w * LQ + b0, X + 16 * w * LQ, D + b0 * LQ, b0, lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    wave_apply_inv16(X + 16 * w * LQ + b0, LTd + p * 16 * LI, lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
+  for (int p = 0; p < 4; ++p) trsm_step(X, D, LTd, w, p, lane);
   __syncthreads();
 }
 
@@ -1070,6 +1079,7 @@ struct DagArgs {
   int *ticket;                // its ticket counter
   int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
   unsigned long long *trace;  // debug: [n_tasks][8] s_memrealtime at draw / waits met / end, workgroup, sub-phases
+  const int *gate;            // device LM loop: the launch returns at once while *gate != 0
 };
 
 __device__ __forceinline__ unsigned long long realtime() {
@@ -1086,11 +1096,12 @@ __device__ __forceinline__ unsigned long long realtime() {
   } while (0)
 
 __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
+  if (gated(a.gate)) return;
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
   __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 8 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
-  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [5] fused TRSM tile prefetched,
-  // [6] its fetch requested, [8..10] the POTRF pipeline's flags
+  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation,
+  // [6] its fetch requested, [8..10] the POTRF pipeline's flags, [11] thirds of that tile loaded
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
   double *colx = LTd + 4 * 16 * LI + 8;   // POTRF pivot scratch (X stays free for the prefetch)
   int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.ticket;
@@ -1230,7 +1241,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       __syncthreads();
       if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
       // The fused TRSM's tile: wave 1 fetches it into X while wave 0 factors
-      // the first diagonal block, if its late waits are already met (sh[5]);
+      // the first diagonal block, if its late waits are already met;
       // otherwise it is waited for and loaded after L_kk is published.
       const double *pf_src = sub.x >= 0 ? a.S + (long)sub.x * (T64 * T64) : nullptr;
       const int pw0 = sub.y, pw1 = a.wait_off[t + 1];
@@ -1240,6 +1251,11 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // the tile's last update lands a few microseconds into the POTRF
       // (cfg3 k_factor_dag 758 -> 736 us).
       if (tid == 0) sh[6] = 0;
+      // sh[11]: thirds of the tile loaded into X (3: all; set to 0 by the
+      // pipeline's start).  Each wave decides for its own third: a wave that
+      // reaches a panel late must not take another wave's completed third for
+      // the whole tile.
+      bool third_done = false;
       const bool ok = blocked_potrf64_async(D, inv, LTd, sh + 1, sh + 8, tid, colx, [&](int p, int wv, int ln) {
         auto poll = [&]() {
           if (!pf_src || pw1 - pw0 > 64) return false;
@@ -1254,10 +1270,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           if (wv != 1) return;
           const bool met = poll();
           if (fold_in) {   // X still holds the fold's operand: fetch beside panel 1 instead
-            if (ln == 0) {
-              sh[5] = 0;
-              if (met) sh[6] = -1;
-            }
+            if (ln == 0 && met) *as_lds(sh + 6) = -1;
             return;
           }
           if (met) {
@@ -1274,13 +1287,15 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
                 *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
               }
             }
+            lds_set(sh + 11, 3);
           }
-          if (ln == 0) sh[5] = met ? 1 : 0;
-        } else if (sh[5]) {
           return;
-        } else if (!sh[6]) {   // not requested yet: poll beside panels 1 and 2
-          if (wv == 1 && p < 3 && poll() && ln == 0) sh[6] = p;
-        } else if (sh[6] < p) {   // requested beside an earlier panel: the three thirds
+        }
+        if (third_done || lds_get(sh + 11) >= 3) return;
+        const int req = lds_get(sh + 6);
+        if (req == 0) {   // not requested yet: poll beside panels 1 and 2
+          if (wv == 1 && p < 3 && poll() && ln == 0) *as_lds(sh + 6) = p;
+        } else if (req < p) {   // requested beside an earlier panel: the three thirds
           // 2048 16-byte elements of the 64x64 tile: wave w takes e in [(w-1)*683, min(w*683, 2048))
           const int e0 = (wv - 1) * 683, e1 = min(wv * 683, 2048);
           for (int base = e0; base < e1; base += 8 * 64) {
@@ -1295,9 +1310,10 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
               if (e < e1) *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
             }
           }
-          if (wv == 1 && ln == 0) sh[5] = 1;
+          third_done = true;
+          lds_add(sh + 11, ln);
         }
-      }, fold_in ? X : nullptr);
+      }, X, fold_in);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
@@ -1315,7 +1331,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       if (a.trace && tid == 0) a.trace[8L * t + 6] = realtime();
       if (sub.x >= 0) {
         // fused TRSM of the parent's tile against the L_kk still in LDS
-        const bool pref = sh[5] != 0;   // (written inside the POTRF, barriers since)
+        const bool pref = sh[11] >= 3;   // (written inside the POTRF, barriers since)
         if (!pref) {
           if (w == 0) {
             const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane, true);
@@ -1330,27 +1346,41 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // now; the claim itself (after the solve) answers during the tile's
         // store; wave 0's other lanes poll the target's early waits, so a
         // claimed target whose waits were already met skips its own poll.
+        // Every wave polls the target's early waits (lanes 1..63) and reads
+        // the answer after its first two solve steps: a claimed continuation
+        // whose waits all four waves saw met skips its own poll.  (Its A_kk
+        // prefetched into registers here was measured neutral: the release
+        // before the counter bump, s_waitcnt vmcnt(0), then waits for it.)
         int tk_seen = 0, infl_old = 0;
-        bool c_met = false;
-        if (c >= 0 && w == 0) {
-          if (lane == 0) {
+        bool c_poll = false, c_mine = false;
+        int c_got = 0, c_need = 0;
+        if (c >= 0) {
+          if (tid == 0) {
             tk_seen = ld_acquire_relaxed(ticket);
             infl_old = atomicAdd(inflight, 1);
           }
           const int cw0 = a.wait_off[c], cw1 = a.sub[c].y;
-          if (cw1 - cw0 <= 63) {
-            const int q = cw0 + lane - 1;
-            bool open = false;
-            if (lane >= 1 && q < cw1) {
-              const int2 cv = a.waits[q];   // (the tile this task publishes below counts as met)
-              open = cv.x != sub.x && ld_acquire_relaxed(a.counters + cv.x) < cv.y;
+          c_poll = cw1 - cw0 <= 63;
+          const int q = cw0 + lane - 1;
+          if (c_poll && lane >= 1 && q < cw1) {
+            const int2 cv = a.waits[q];
+            if (cv.x != sub.x) {   // (the tile this task publishes below counts as met)
+              c_mine = true;
+              c_need = cv.y;
+              c_got = ld_acquire_relaxed(a.counters + cv.x);
             }
-            c_met = __builtin_amdgcn_ballot_w64(open) == 0;
           }
         }
         if (!pref) load_tile_wt(Ct, X, tid);
         __syncthreads();
-        blocked_trsm64(X, D, inv, LTd, tid);
+        // blocked_trsm64, its steps inline (row block w per wave)
+        trsm_step(X, D, LTd, w, 0, lane);
+        trsm_step(X, D, LTd, w, 1, lane);
+        const bool c_met = c_poll && __builtin_amdgcn_ballot_w64(c_mine && c_got < c_need) == 0;
+        trsm_step(X, D, LTd, w, 2, lane);
+        trsm_step(X, D, LTd, w, 3, lane);
+        if (lane == 0) sh[12 + w] = c_met ? 1 : 0;
+        __syncthreads();
         // claim the continuation target before the tile is published: its
         // drawer waits for this tile, so it cannot have claimed it yet
         int claim = -1;
@@ -1364,13 +1394,12 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         dag_release(tid);
         if (tid == 0) {
           sh[4] = claim;
-          sh[7] = c_met ? 1 : 0;
           __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
         __syncthreads();
         next = sh[4];
-        next_met = next >= 0 && sh[7] != 0;
+        next_met = next >= 0 && sh[12] && sh[13] && sh[14] && sh[15];
         if (next >= 0) prev_k = k;
       }
     } else if (task.x == 3) {
@@ -1614,11 +1643,11 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
                                                     int T, const double *__restrict__ Ld, long nR,
                                                     const int *__restrict__ cols, const int2 *__restrict__ gather,
                                                     const int *__restrict__ gbeg, int ncols, double *yF,
-                                                    int *counters, int *flag) {
+                                                    int *counters, int *flag, const int *gate) {
   __shared__ double red[4][T64];
   __shared__ double ys[T64];
   __shared__ int sh[2];
-  if (*flag) return;
+  if (gated(gate) || *flag) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   int *ticket = counters + T;   // (counters[0..T) are unused: y entries are their own flags)
   const double *Xinv = Ld + (long)T * T64 * T64;
@@ -1716,6 +1745,8 @@ namespace {
 // (with ld.n > 0 also the step's LM diagonal: k_lm_diag's work, one launch less)
 __global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c, long nc, int *d, long nd,
                              LmDiagArgs ld) {
+  if (gated(ld.gate)) return;
+  if (gated(ld.keep_diag)) ld.n = 0;
   const long n = na + nb + nc + nd;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < ld.nys; e += (long)gridDim.x * blockDim.x)
     ld.ysent[e] = __longlong_as_double((long long)kYSentinel);
@@ -1771,7 +1802,7 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
 }
 
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
-                          unsigned long long *trace, bool reset, int phase) {
+                          unsigned long long *trace, bool reset, int phase, const int *gate) {
   const int t_begin = phase == 1 ? (int)P.phase_split : 0;
   const int t_end = phase == 0 ? (int)P.phase_split : (int)P.n_dag_tasks;
   if (t_end <= t_begin) return;
@@ -1784,13 +1815,13 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
             P.dag_maxdep, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
             P.upd_part, P.upd_cnt, flag, t_begin, t_end,
-            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagCounterExtra - 1 : 0), progress, trace};
+            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagCounterExtra - 1 : 0), progress, trace, gate};
   const int grid = (int)std::min<long>(n_workgroups, t_end - t_begin);
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
 
 void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, double *yF, int *flag,
-                                 hipStream_t s, int n_workgroups, bool reset) {
+                                 hipStream_t s, int n_workgroups, bool reset, const int *gate) {
   const int ncols = (int)P.h_bcols.size();
   if (ncols == 0) return;
   if (reset) {
@@ -1802,7 +1833,7 @@ void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, dou
   }
   const int grid = std::min(n_workgroups, ncols);
   hipLaunchKernelGGL(k_bsolve_dag, dim3((unsigned)grid), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag, nR, P.bs_cols,
-                     P.bs_gather, P.bs_gbeg, ncols, yF, P.bs_counters, flag);
+                     P.bs_gather, P.bs_gbeg, ncols, yF, P.bs_counters, flag, gate);
 }
 
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,

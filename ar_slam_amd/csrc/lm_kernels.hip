@@ -192,6 +192,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
                                                      double *__restrict__ colnorm,
                                                      double *__restrict__ obs_tg,
                                                      double *__restrict__ parts) {
+  if (gated(P.gate_lin)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int c = blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
@@ -259,6 +260,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
 
 __global__ void k_tag_reduce(DevProblem P, const double *__restrict__ obs_tg,
                              double *__restrict__ g, double *__restrict__ colnorm) {
+  if (gated(P.gate_lin)) return;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= 12L * P.nt) return;
   const int t = (int)(e / 12), j = (int)(e % 12);
@@ -301,6 +303,8 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
 __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ scale,
                                                  const double *__restrict__ diag, double radius,
                                                  double *__restrict__ zero_tiles) {
+  if (gated(P.gate_step)) return;
+  radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   SCHUR_STAMP_INIT;
   const int c = blockIdx.x, lane = threadIdx.x;
@@ -618,6 +622,8 @@ __device__ __forceinline__ void prep_pad_row(const DevProblem &P, const double *
 
 __global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__restrict__ S,
                                                       const double *__restrict__ diag, double radius) {
+  if (gated(P.gate_step)) return;
+  radius = step_radius(P, radius);
   __shared__ double part[4][kWave];
   __shared__ SchurContrib cts[4][kWave];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -663,6 +669,8 @@ __global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__re
 // Split destinations: the pieces' partial sums, in piece order.
 __global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__restrict__ S,
                                                        const double *__restrict__ diag, double radius) {
+  if (gated(P.gate_step)) return;
+  radius = step_radius(P, radius);
   __shared__ double part[4][kWave];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int sp = blockIdx.x * 4 + w;
@@ -692,6 +700,8 @@ __global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__r
 // enough to stay positive (its factor row is L^{-1} b, its pivot unused).
 __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, double radius,
                                double *__restrict__ S, int which) {
+  if (gated(P.gate_step)) return;
+  radius = step_radius(P, radius);
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.N) return;
   if (which >= 0 && P.tile_class[i >> 6] != which) return;
@@ -779,6 +789,8 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
                                                    const double *__restrict__ yF,
                                                    double *__restrict__ xc,
                                                    double *__restrict__ parts, int reuse_ui, int with_cost) {
+  if (gated(P.gate_step)) return;
+  radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int c = blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
@@ -915,6 +927,7 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
                                                   const double *__restrict__ yF,
                                                   double *__restrict__ xc,
                                                   double *__restrict__ fparts) {
+  if (gated(P.gate_step)) return;
   __shared__ double red[2][256];
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0;
@@ -956,7 +969,8 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
 __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
                                                        const double *__restrict__ fparts,
                                                        int nfparts, double *__restrict__ out,
-                                                       const int *__restrict__ flag) {
+                                                       const int *__restrict__ flag, const int *gate) {
+  if (gated(gate)) return;
   __shared__ double red[1024];
   const int t = threadIdx.x;
   const int p = blockIdx.x;
@@ -999,7 +1013,8 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
                                                     const unsigned char *__restrict__ free_,
                                                     const double *__restrict__ g,
                                                     const double *__restrict__ x,
-                                                    double *__restrict__ part) {
+                                                    double *__restrict__ part, const int *gate) {
+  if (gated(gate)) return;
   __shared__ double red[6][256];
   const int t = threadIdx.x;
   double v[6] = {0, 0, 0, 0, 0, 0};
@@ -1029,7 +1044,8 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
 
 // second stage: out[q] = reduction over the kNormBlocks partials (fixed tree)
 __global__ __launch_bounds__(64) void k_slot_norms_final(const double *__restrict__ part,
-                                                         double *__restrict__ out) {
+                                                         double *__restrict__ out, const int *gate) {
+  if (gated(gate)) return;
   __shared__ double red[6][kNormBlocks];
   const int t = threadIdx.x;
   for (int q = 0; q < 6; ++q) red[q][t] = part[6L * t + q];
@@ -1045,8 +1061,8 @@ __global__ __launch_bounds__(64) void k_slot_norms_final(const double *__restric
 
 // camera slots from the reduced per-capture partials (masked by freedom)
 __global__ void k_camera_slots(const unsigned char *__restrict__ free_, const double *__restrict__ red,
-                               double *__restrict__ g, double *__restrict__ colnorm) {
-  if (threadIdx.x == 0) {
+                               double *__restrict__ g, double *__restrict__ colnorm, const int *gate) {
+  if (threadIdx.x == 0 && !gated(gate)) {
     g[0] = free_[0] ? red[P_GF] : 0.0;
     colnorm[0] = free_[0] ? red[P_CF] : 0.0;
     g[1] = g[2] = 0.0;
@@ -1177,20 +1193,20 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 }
 
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
-                         hipStream_t s, const int *flag) {
-  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag);
+                         hipStream_t s, const int *flag, const int *gate) {
+  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, gate);
 }
 
 void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out, hipStream_t s) {
   // out[0..7] results, out[8..] the per-block partials (see d_norms)
   hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g, x,
-                     out + 8);
-  hipLaunchKernelGGL(k_slot_norms_final, dim3(1), dim3(kNormBlocks), 0, s, out + 8, out);
+                     out + 8, P.gate_lin);
+  hipLaunchKernelGGL(k_slot_norms_final, dim3(1), dim3(kNormBlocks), 0, s, out + 8, out, P.gate_lin);
 }
 
 void launch_camera_slots(const DevProblem &P, const double *red, double *g, double *colnorm,
                          hipStream_t s) {
-  hipLaunchKernelGGL(k_camera_slots, dim3(1), dim3(64), 0, s, P.slot_free, red, g, colnorm);
+  hipLaunchKernelGGL(k_camera_slots, dim3(1), dim3(64), 0, s, P.slot_free, red, g, colnorm, P.gate_lin);
 }
 
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,

@@ -65,6 +65,7 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int,
 SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = 0, 1, 2
 ELIM_AUTO, ELIM_CAPTURES, ELIM_TAGS = 0, 1, 2   # arslam_lm_options.elimination
 SETUP_LOAD, SETUP_VALUES, SETUP_APPEND = 0, 1, 2   # arslam_lm_summary.setup_kind
+LOOP_HOST, LOOP_DEVICE, LOOP_GRAPH = 0, 1, 2         # arslam_lm_summary.lm_loop
 _ip = C.POINTER(C.c_int)
 _up = C.POINTER(C.c_ubyte)
 
@@ -90,7 +91,7 @@ class Options(C.Structure):
                 ("update_state_every_iteration", C.c_int),
                 ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int),
                 ("reduced_ordering", C.c_int), ("kernel_timing", C.c_int), ("factor_executor", C.c_int),
-                ("phase_timing", C.c_int)]
+                ("phase_timing", C.c_int), ("device_loop", C.c_int)]
 
 
 class Iteration(C.Structure):
@@ -128,7 +129,7 @@ class Summary(C.Structure):
                 ("split_top_work", C.c_double), ("split_max_rank_work", C.c_double),
                 ("split_total_work", C.c_double), ("t_factor_own_ms", C.c_double),
                 ("t_factor_top_ms", C.c_double),
-                ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1))]
+                ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1)), ("lm_loop", C.c_int)]
 
     def to_dict(self):
         its = [{f: getattr(self.iters[i], f) for f, _ in Iteration._fields_}

@@ -224,6 +224,8 @@ def main():
     ap.add_argument("--no-localize", action="store_true", help="skip the cfg5 batched-localize side key")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--device-loop", action="store_true",
+                    help="LM decisions on the device, iterations enqueued ahead as hipGraphs (measured slower)")
     ap.add_argument("--skip-zero-tiles", type=int, default=1)
     ap.add_argument("--ordering", type=int, default=2, help="0 natural, 1 RCM, 2 nested dissection")
     ap.add_argument("--executor", type=int, default=1, help="0 level launches, 1 persistent task graph")
@@ -258,7 +260,7 @@ def main():
         comm = (rank, world, obj[0])
     opts = dict(device=local_rank, kernel_timing=0 if args.no_kernel_timing else 1,
                 cholesky_skip_zero_tiles=args.skip_zero_tiles, reduced_ordering=args.ordering,
-                factor_executor=args.executor)
+                factor_executor=args.executor, device_loop=1 if args.device_loop else 0)
     # the timed solves record no per-phase events (each costs GPU time between
     # kernels); the dominant kernel's own events stay on for the roofline.
     # Construction = the cold per-problem setup a Ceres Solve's preprocessor
@@ -349,6 +351,7 @@ def main():
             "final_rms_px": last["final_rms_px"],
             "termination": f"{last['termination']} ({last['rule']})",
             "lm_iterations_per_solve": last["num_linear_solves"],
+            "lm_loop": {0: "host", 1: "device", 2: "device, one hipGraph per iteration"}.get(last.get("lm_loop"), "?"),
             "reduced_system": {"rows": int(last["n_reduced"]), "factor_tiles": int(last["n_factor_tiles"]),
                                "etree_levels": int(last["n_levels"]),
                                "ordering": ["natural", "RCM", "nested dissection"][args.ordering],

@@ -103,8 +103,15 @@ typedef struct {
   int factor_executor;               /* reduced-system Cholesky: 0 two launches per elimination-tree
                                         level, 1 one persistent task-graph launch (default) */
   int phase_timing;                  /* 1 (default): HIP events around each phase of the step
-                                        (summary t_*_ms); 0: none (each event record costs a few
-                                        microseconds of GPU time between kernels) */
+                                        (summary t_*_ms; host loop only); 0: none (each event
+                                        record costs a few microseconds of GPU time) */
+  int device_loop;                   /* 1: the LM decisions (step acceptance, radius, termination)
+                                        run on the device and the host enqueues iterations ahead,
+                                        one hipGraph launch each, whenever nothing needs the host
+                                        between iterations (one rank, no iteration callback, no
+                                        per-iteration write-back or progress table, phase_timing
+                                        = 0); 0 (default): the host decides each step, one round
+                                        trip per step -- measured faster on MI355X */
 } arslam_lm_options;
 
 /* ceres::IterationSummary subset */
@@ -157,7 +164,12 @@ typedef struct {
   double t_factor_top_ms;       /*   phase 1 (the top), summed over the solve (phase_timing = 1) */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
+  int lm_loop;                  /* ARSLAM_LOOP_*: which loop drove the minimizer */
 } arslam_lm_summary;
+
+/* summary.lm_loop: the host decided every step; the device decided, kernels
+ * enqueued per iteration; the device decided, one hipGraph launch per iteration */
+enum { ARSLAM_LOOP_HOST = 0, ARSLAM_LOOP_DEVICE = 1, ARSLAM_LOOP_GRAPH = 2 };
 
 /* Whole problem in struct-of-arrays form (bulk / benchmark path). */
 typedef struct {

@@ -28,8 +28,12 @@ n = s.num_solves
 setup = mini = 0.0
 iters = 0
 kinds = [0, 0, 0]
+PH = ("t_linearize_ms", "t_schur_ms", "t_cholesky_ms", "t_solve_ms", "t_backsub_ms", "t_cost_ms")
+ph = dict.fromkeys(PH, 0.0)
 for i in range(n):
     d = s.solve_summary(i)
+    for k in PH:
+        ph[k] += d.get(k, 0.0)
     kinds[d["setup_kind"]] += 1
     setup += d["setup_time_s"]
     mini += d["minimizer_time_s"]
@@ -39,5 +43,6 @@ print(json.dumps({"flow": f"solveIncremental, {name}: {g.n_cap} captures / {g.n_
                   "wall_s": wall, "solves": n, "lm_iterations": iters,
                   "setup_ms_per_solve": 1e3 * setup / n, "minimizer_ms_per_solve": 1e3 * mini / n,
                   "other_ms_per_solve": 1e3 * (wall - setup - mini) / n,
+                  "device_phase_ms_per_solve": {k[2:-3]: round(v / n, 4) for k, v in ph.items()},
                   "setup_kinds": {"load": kinds[0], "values": kinds[1], "append": kinds[2]},
                   "final_rms_px": last["final_rms_px"], "final_termination": last["termination"]}))
