@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void k_bench(const double *A, const double *Fg
   __shared__ __attribute__((aligned(16))) double LTd[4 * 16 * LI];
   __shared__ double colx[64];
   __shared__ int bad;
-  __shared__ int fl[4];
+  __shared__ int fl[8];
   const int tid = threadIdx.x;
   __builtin_amdgcn_s_setprio(3);
   unsigned long long tot = 0, best = ~0ull;
@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void k_bench(const double *A, const double *Fg
     if (variant == 0) blocked_potrf64(D, inv, LTd, &bad, tid, colx);
     else if (variant == 1) blocked_potrf64_async(D, inv, LTd, &bad, fl, tid, colx, none);
     else if (variant == 2) blocked_potrf64_idle(D, inv, LTd, &bad, tid, colx, none, F);
-    else if (variant == 3) blocked_potrf64_async(D, inv, LTd, &bad, fl, tid, colx, none, F);
+    else if (variant == 3) blocked_potrf64_async(D, inv, LTd, &bad, fl, tid, colx, none, F, true);
     else if (tid < 64) {
       for (int p = 0; p < 4; ++p) diag16(D, 16 * p, inv, LTd + p * 16 * LI, &bad, tid, colx);
     }
