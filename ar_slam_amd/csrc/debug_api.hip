@@ -291,3 +291,42 @@ extern "C" int arslam_debug_schur_stamps(unsigned long long out[16]) {
   arslam::debug_read_schur_stamps(out);
   return ARSLAM_OK;
 }
+
+extern "C" int arslam_debug_gather_extend(const arslam_soa_problem *p, int c0, int *identical, int *n_dest) {
+  if (!p || !identical || !n_dest || c0 < 0 || c0 > p->n_cap) return ARSLAM_E_INVALID_ARG;
+  try {
+    // the first c0 captures' residual blocks, in p's order
+    std::vector<int> oc, ot;
+    std::vector<double> cr;
+    for (int b = 0; b < p->n_obs; ++b)
+      if (p->obs_cap[b] < c0) {
+        oc.push_back(p->obs_cap[b]);
+        ot.push_back(p->obs_tag[b]);
+        cr.insert(cr.end(), p->corners + 8L * b, p->corners + 8L * b + 8);
+      }
+    arslam_soa_problem q = *p;
+    q.n_cap = c0;
+    q.n_obs = (int)oc.size();
+    q.obs_cap = oc.data();
+    q.obs_tag = ot.data();
+    q.corners = cr.data();
+    const arslam::HostProblem hs = arslam::host_problem(&q, nullptr);
+    const arslam::ReducedLayout L = arslam::reduced_layout(hs, 2, true, nullptr, nullptr);
+    arslam::SchurGather G = arslam::schur_gather_plan(hs, L);
+    const arslam::HostProblem hf = arslam::host_problem(p, nullptr);
+    arslam::schur_gather_extend(G, hf, L, c0);
+    const arslam::SchurGather F = arslam::schur_gather_plan(hf, L);
+    bool same = G.cap_off == F.cap_off && G.dest_row == F.dest_row && G.dest_start == F.dest_start &&
+                G.items == F.items && G.splits == F.splits && G.n_pslots == F.n_pslots &&
+                G.max_contrib == F.max_contrib && G.contrib.size() == F.contrib.size();
+    for (size_t i = 0; same && i < G.contrib.size(); ++i)
+      same = !std::memcmp(&G.contrib[i], &F.contrib[i], sizeof(arslam::SchurContrib));
+    *identical = same ? 1 : 0;
+    *n_dest = (int)F.dest_start.size() - 1;
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}

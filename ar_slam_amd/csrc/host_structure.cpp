@@ -6,6 +6,7 @@
 #include "host_structure.h"
 
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <iterator>
 #include <cstdio>
@@ -751,73 +752,53 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   return L;
 }
 
-SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
-  SchurGather G;
-  G.cap_off.assign(h.nc + 1, 0);
-  struct Item {
-    long key;   // rX << 32 | rY
-    int c;
-    int px, py, nblk;
-  };
-  std::vector<Item> items;
-  std::vector<std::pair<int, int>> blk;   // (global first row, local first column) of the capture's blocks
-  for (int c = 0; c < h.nc; ++c) {
-    const int nblk = h.cap_blk_start[c + 1] - h.cap_blk_start[c];
-    const long m = 1 + 6L * nblk;
-    G.cap_off[c + 1] = G.cap_off[c] + schur_slab_size(nblk);
-    if (h.cap_start[c + 1] == h.cap_start[c]) continue;   // no residuals: k_schur stores nothing
-    blk.clear();
-    if (L.cam_row >= 0) blk.emplace_back(L.cam_row, 0);
-    for (int u = 0; u < nblk; ++u) {
-      const int tr = L.tag_row[h.blk_tag[h.cap_blk_start[c] + u]];
-      if (tr >= 0) blk.emplace_back(tr, 1 + 6 * u);
-    }
-    if (blk.empty()) continue;
-    blk.emplace_back((int)L.nR, (int)m);   // rhs row
-    for (size_t a = 0; a < blk.size(); ++a)
-      for (size_t b = 0; b < blk.size(); ++b) {
-        const int rx = blk[a].first, ry = blk[b].first;
-        if (rx < ry || ry == L.nR) continue;   // lower blocks; the rhs only as a row
-        items.push_back({((long)rx << 32) | ry, c, blk[a].second, blk[b].second, nblk});
-      }
+namespace {
+
+struct GatherItem {
+  long key;   // rX << 32 | rY
+  int c;
+  int px, py, nblk;
+};
+
+// capture c's lower blocks of the reduced system (and its rhs row) as gather items
+void capture_gather_items(const HostProblem &h, const ReducedLayout &L, int c, std::vector<GatherItem> &items,
+                          std::vector<std::pair<int, int>> &blk) {
+  const int nblk = h.cap_blk_start[c + 1] - h.cap_blk_start[c];
+  const long m = 1 + 6L * nblk;
+  if (h.cap_start[c + 1] == h.cap_start[c]) return;   // no residuals: k_schur stores nothing
+  blk.clear();
+  if (L.cam_row >= 0) blk.emplace_back(L.cam_row, 0);
+  for (int u = 0; u < nblk; ++u) {
+    const int tr = L.tag_row[h.blk_tag[h.cap_blk_start[c] + u]];
+    if (tr >= 0) blk.emplace_back(tr, 1 + 6 * u);
   }
-  // stable sort by (rX, rY): two stable counting passes (rY, then rX; rows
-  // are < nR + 1), so each destination's contributions stay in capture
-  // order -- the gather's fixed summation order.  (A comparison sort of the
-  // ~45 items per capture was half of the per-Solve setup of an incremental
-  // flow.)
-  {
-    const long nrow = L.nR + 2;
-    std::vector<int> cnt(nrow + 1);
-    std::vector<Item> tmp(items.size());
-    for (int pass = 0; pass < 2; ++pass) {
-      auto row = [&](const Item &t) { return pass == 0 ? (long)(t.key & 0xffffffffL) : (long)(t.key >> 32); };
-      std::fill(cnt.begin(), cnt.end(), 0);
-      for (const Item &t : items) cnt[row(t) + 1]++;
-      for (long r = 0; r < nrow; ++r) cnt[r + 1] += cnt[r];
-      for (const Item &t : items) tmp[cnt[row(t)]++] = t;
-      items.swap(tmp);
+  if (blk.empty()) return;
+  blk.emplace_back((int)L.nR, (int)m);   // rhs row
+  for (size_t a = 0; a < blk.size(); ++a)
+    for (size_t b = 0; b < blk.size(); ++b) {
+      const int rx = blk[a].first, ry = blk[b].first;
+      if (rx < ry || ry == L.nR) continue;   // lower blocks; the rhs only as a row
+      items.push_back({((long)rx << 32) | ry, c, blk[a].second, blk[b].second, nblk});
     }
-  }
-  G.contrib.reserve(items.size());
-  for (size_t i = 0; i < items.size(); ++i) {
-    if (i == 0 || items[i].key != items[i - 1].key) {
-      if (i) G.max_contrib = std::max(G.max_contrib, (int)(G.contrib.size() - G.dest_start.back()));
-      G.dest_row.push_back((int)(items[i].key >> 32));
-      G.dest_row.push_back((int)(items[i].key & 0xffffffffL));
-      G.dest_start.push_back((int)G.contrib.size());
-    }
-    const Item &t = items[i];
-    const int m = 1 + 6 * t.nblk, U = schur_blk(t.px, m), V = schur_blk(t.py, m);
-    if (U >= V) G.contrib.push_back({G.cap_off[t.c] + schur_block_off(U, V, t.nblk), 0, schur_blk_size(V, t.nblk)});
-    else G.contrib.push_back({G.cap_off[t.c] + schur_block_off(V, U, t.nblk), 1, schur_blk_size(U, t.nblk)});
-  }
-  if (!G.dest_start.empty())
-    G.max_contrib = std::max(G.max_contrib, (int)(G.contrib.size() - G.dest_start.back()));
-  G.dest_start.push_back((int)G.contrib.size());
+}
+
+SchurContrib gather_contrib(const SchurGather &G, const GatherItem &t) {
+  const int m = 1 + 6 * t.nblk, U = schur_blk(t.px, m), V = schur_blk(t.py, m);
+  if (U >= V) return {G.cap_off[t.c] + schur_block_off(U, V, t.nblk), 0, schur_blk_size(V, t.nblk)};
+  return {G.cap_off[t.c] + schur_block_off(V, U, t.nblk), 1, schur_blk_size(U, t.nblk)};
+}
+
+// the gather launch's work items: a destination per item, or its contributions
+// in chunks summed through partial slots (k_schur_combine)
+void gather_partition(SchurGather &G) {
+  G.items.clear();
+  G.splits.clear();
+  G.n_pslots = 0;
+  G.max_contrib = 0;
   const int nd = (int)G.dest_start.size() - 1;
   for (int d = 0; d < nd; ++d) {
     const int k0 = G.dest_start[d], k1 = G.dest_start[d + 1];
+    G.max_contrib = std::max(G.max_contrib, k1 - k0);
     if (k1 - k0 <= kSchurChunk) {
       G.items.insert(G.items.end(), {d, k0, k1, -1});
       continue;
@@ -828,7 +809,96 @@ SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
       G.items.insert(G.items.end(), {d, k0 + q * kSchurChunk, std::min(k1, k0 + (q + 1) * kSchurChunk), G.n_pslots + q});
     G.n_pslots += pieces;
   }
+}
+
+}  // namespace
+
+SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
+  SchurGather G;
+  G.cap_off.assign(h.nc + 1, 0);
+  std::vector<GatherItem> items;
+  std::vector<std::pair<int, int>> blk;   // (global first row, local first column) of the capture's blocks
+  for (int c = 0; c < h.nc; ++c) {
+    const int nblk = h.cap_blk_start[c + 1] - h.cap_blk_start[c];
+    G.cap_off[c + 1] = G.cap_off[c] + schur_slab_size(nblk);
+    capture_gather_items(h, L, c, items, blk);
+  }
+  // stable sort by (rX, rY): two stable counting passes (rY, then rX; rows
+  // are < nR + 1), so each destination's contributions stay in capture
+  // order -- the gather's fixed summation order.  (A comparison sort of the
+  // ~45 items per capture was half of the per-Solve setup of an incremental
+  // flow.)
+  {
+    const long nrow = L.nR + 2;
+    std::vector<int> cnt(nrow + 1);
+    std::vector<GatherItem> tmp(items.size());
+    for (int pass = 0; pass < 2; ++pass) {
+      auto row = [&](const GatherItem &t) { return pass == 0 ? (long)(t.key & 0xffffffffL) : (long)(t.key >> 32); };
+      std::fill(cnt.begin(), cnt.end(), 0);
+      for (const GatherItem &t : items) cnt[row(t) + 1]++;
+      for (long r = 0; r < nrow; ++r) cnt[r + 1] += cnt[r];
+      for (const GatherItem &t : items) tmp[cnt[row(t)]++] = t;
+      items.swap(tmp);
+    }
+  }
+  G.contrib.reserve(items.size());
+  for (size_t i = 0; i < items.size(); ++i) {
+    if (i == 0 || items[i].key != items[i - 1].key) {
+      G.dest_row.push_back((int)(items[i].key >> 32));
+      G.dest_row.push_back((int)(items[i].key & 0xffffffffL));
+      G.dest_start.push_back((int)G.contrib.size());
+    }
+    G.contrib.push_back(gather_contrib(G, items[i]));
+  }
+  G.dest_start.push_back((int)G.contrib.size());
+  gather_partition(G);
   return G;
+}
+
+// The plan of a problem grown by the captures [c0, nc) whose captures below c0
+// are unchanged (the same layout L): each destination keeps its contributions
+// and gains the new captures' after them -- capture order, the summation order
+// of a fresh plan -- and a block no capture had touched becomes a destination
+// in (rX, rY) order.  Equal to schur_gather_plan of the grown problem.
+void schur_gather_extend(SchurGather &G, const HostProblem &h, const ReducedLayout &L, int c0) {
+  const int nc0 = (int)G.cap_off.size() - 1;
+  if (c0 != nc0) throw std::logic_error("schur_gather_extend: not an append of captures");
+  G.cap_off.resize(h.nc + 1);
+  std::vector<GatherItem> items;
+  std::vector<std::pair<int, int>> blk;
+  for (int c = c0; c < h.nc; ++c) {
+    const int nblk = h.cap_blk_start[c + 1] - h.cap_blk_start[c];
+    G.cap_off[c + 1] = G.cap_off[c] + schur_slab_size(nblk);
+    capture_gather_items(h, L, c, items, blk);
+  }
+  std::stable_sort(items.begin(), items.end(), [](const GatherItem &a, const GatherItem &b) { return a.key < b.key; });
+  const int nd = (int)G.dest_start.size() - 1;
+  std::vector<int> dest_row, dest_start;
+  std::vector<SchurContrib> contrib;
+  dest_row.reserve(G.dest_row.size() + 2 * items.size());
+  dest_start.reserve(G.dest_start.size() + items.size());
+  contrib.reserve(G.contrib.size() + items.size());
+  const long kEnd = LONG_MAX;
+  size_t i = 0;
+  int d = 0;
+  while (d < nd || i < items.size()) {
+    const long ko = d < nd ? ((long)G.dest_row[2 * d] << 32) | G.dest_row[2 * d + 1] : kEnd;
+    const long kn = i < items.size() ? items[i].key : kEnd;
+    const long k = std::min(ko, kn);
+    dest_row.push_back((int)(k >> 32));
+    dest_row.push_back((int)(k & 0xffffffffL));
+    dest_start.push_back((int)contrib.size());
+    if (ko == k) {
+      contrib.insert(contrib.end(), G.contrib.begin() + G.dest_start[d], G.contrib.begin() + G.dest_start[d + 1]);
+      ++d;
+    }
+    for (; i < items.size() && items[i].key == k; ++i) contrib.push_back(gather_contrib(G, items[i]));
+  }
+  dest_start.push_back((int)contrib.size());
+  G.dest_row.swap(dest_row);
+  G.dest_start.swap(dest_start);
+  G.contrib.swap(contrib);
+  gather_partition(G);
 }
 
 }  // namespace arslam

@@ -154,5 +154,7 @@ struct SchurGather {
   int max_contrib = 0;
 };
 SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L);
+// the same plan, updated for a problem grown by captures [c0, nc) (the captures below c0 unchanged)
+void schur_gather_extend(SchurGather &G, const HostProblem &h, const ReducedLayout &L, int c0);
 
 }  // namespace arslam

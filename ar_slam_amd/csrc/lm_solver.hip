@@ -76,14 +76,15 @@ template <class T>
 struct DevBuf {
   T *p = nullptr;
   size_t n = 0, cap = 0;
-  void alloc(size_t count) {
+  void alloc(size_t count) {   // grows by half again (a growing incremental problem reallocates rarely)
     n = count;
     if (count <= cap) return;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
-    cap = count;
+    const size_t want = cap == 0 && count <= 16 ? count : count + count / 2;
+    HIP_CHECK(hipMalloc(&p, want * sizeof(T)));
+    cap = want;
   }
   void upload(const T *h, size_t count, hipStream_t s) {
     if (count) HIP_CHECK(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
@@ -370,7 +371,10 @@ struct arslam_lm {
   }
 
   void load(const arslam_soa_problem *p);
-  void upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L);
+  // (extend_from >= 0: captures [extend_from, nc) were appended to the loaded
+  // problem, the others unchanged: the gather plan is extended, not rebuilt)
+  void upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L, int extend_from = -1);
+  arslam::SchurGather sg;   // the loaded problem's Schur gather plan
   bool try_extend(const arslam_soa_problem *p);
   arslam::ReducedLayout lay;      // the loaded layout (one rank), kept for try_extend
   bool pk_appended_only = false;  // since the last load only residual blocks of known tags were added
@@ -564,7 +568,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
 // Everything the device needs from the host structure, the layout and the
 // Schur gather plan, in one upload (UploadArena), plus the scratch buffers
 // sized for the problem.  Ends with the load's one stream sync.
-void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L) {
+void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L, int extend_from) {
   const int maxk = h.maxk;
   const std::vector<int> &row_slot = L.row_slot;
   // f-side slot -> reduced row (camera slots 0..2, then the tag slots)
@@ -575,8 +579,12 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
     if (sl < 3) fslot_row[sl] = (int)r;
     else if (sl >= 3 + 6L * nc) fslot_row[sl - 6L * nc] = (int)r;
   }
-  arslam::SchurGather sg;
-  if (has_f) sg = arslam::schur_gather_plan(h, L);
+  static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
+  const double tu0 = prof ? now_s() : 0.0;
+  if (!has_f) sg = arslam::SchurGather{};
+  else if (extend_from >= 0 && (int)sg.cap_off.size() == extend_from + 1) arslam::schur_gather_extend(sg, h, L, extend_from);
+  else sg = arslam::schur_gather_plan(h, L);
+  const double tu1 = prof ? now_s() : 0.0;
   const int n_dest = has_f ? (int)sg.dest_start.size() - 1 : 0;
   const int n_items = (int)sg.items.size() / 4, n_splits = (int)sg.splits.size() / 4;
   upload.add(&u_cap_start, h.cap_start.data(), nc + 1);
@@ -645,7 +653,11 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.gather_items = u_gather_items; P.gather_splits = u_gather_splits; P.gather_part = d_gather_part.p;
   P.n_items = n_items; P.n_splits = n_splits;
   ++problem_epoch;   // (captured LM iterations hold the old arrays)
+  const double tu2 = prof ? now_s() : 0.0;
   HIP_CHECK(hipStreamSynchronize(stream));   // the upload's sources go out of scope
+  if (prof)
+    std::fprintf(stderr, "arslam upload: gather plan %.3f arena+allocs %.3f sync %.3f ms\n", 1e3 * (tu1 - tu0),
+                 1e3 * (tu2 - tu1), 1e3 * (now_s() - tu2));
 }
 
 // An appended problem (arslam_lm_solve after AddResidualBlock only, no new
@@ -667,7 +679,9 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
     ceres_e_tag = cs.e_tag;
   }
   if (p->n_tag != nt) return false;
+  const double t1 = now_s();
   arslam::HostProblem h = arslam::host_problem(p, nullptr);
+  const double t2 = now_s();
   // the same free tags and camera (the same reduced rows)
   if ((lay.cam_row >= 0) != (h.slot_free[0] != 0)) return false;
   for (int t = 0; t < nt; ++t)
@@ -676,7 +690,16 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   const int T = lay.T;
   std::vector<std::pair<int, int>> grown;   // fill tiles that become assembled
   std::vector<int> ts;
+  // (only the captures of the appended residual blocks: the others' tile
+  // pairs were in the pattern already)
+  std::vector<char> touched(h.nc, 0);
+  int first_touched = h.nc;
+  for (long b = nb; b < p->n_obs; ++b) {
+    touched[p->obs_cap[b]] = 1;
+    first_touched = std::min(first_touched, p->obs_cap[b]);
+  }
   for (int c = 0; c < h.nc; ++c) {
+    if (!touched[c]) continue;
     ts.clear();
     if (lay.cam_row >= 0) {
       ts.push_back(lay.cam_row / 64);
@@ -696,6 +719,8 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
         }
   }
   for (const auto &g : grown) lay.pattern[(size_t)g.first * T + g.second] = 1;
+  // only new captures got residual blocks: their contributions extend the gather plan
+  const int extend_from = first_touched >= nc ? nc : -1;
   // the tag slots move with the capture count
   for (int &sl : lay.row_slot)
     if (sl >= 3) sl += 6 * (h.nc - nc);
@@ -705,11 +730,16 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   nb_global = h.nb_global;
   slot_free = h.slot_free;
   x0 = h.x0;
-  upload_problem(h, lay);
+  const double t3 = now_s();
+  upload_problem(h, lay, extend_from);
   soa = *p;
   pk_appended_only = true;
   setup_kind = ARSLAM_SETUP_APPEND;
   setup_s = now_s() - t0;
+  static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
+  if (prof)
+    std::fprintf(stderr, "arslam append: nc %d side %.3f host %.3f check %.3f upload %.3f ms\n", nc,
+                 1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2), 1e3 * (now_s() - t3));
   return true;
 }
 

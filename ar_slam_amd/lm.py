@@ -48,7 +48,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_break_dependency",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
-           "arslam_debug_rank_split",
+           "arslam_debug_rank_split", "arslam_debug_gather_extend",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
            "arslam_slam_create", "arslam_slam_destroy", "arslam_slam_set_verbose", "arslam_slam_load_yaml",
@@ -489,6 +489,15 @@ def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const
     _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
                                            tag_row.ctypes.data_as(_ip)))
     return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]
+
+
+def debug_gather_extend(camera, cap, tag, obs_cap, obs_tag, corners, c0):
+    """Host-only: the appended-problem Schur gather plan (the first c0 captures' plan extended by the
+    rest) against a fresh plan of the whole problem.  Returns (identical, n_destinations)."""
+    A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners)
+    same, nd = C.c_int(0), C.c_int(0)
+    _check(lib().arslam_debug_gather_extend(C.byref(A.s), c0, C.byref(same), C.byref(nd)))
+    return bool(same.value), nd.value
 
 
 class SplitInfo(C.Structure):

@@ -101,6 +101,12 @@ typedef struct {
 } arslam_split_info;
 int arslam_debug_rank_split(const arslam_soa_problem *p, int nranks, int rank, arslam_split_info *info,
                             int *cap_owner);
+/* Host-only: the Schur gather plan of p's first c0 captures (their residual
+ * blocks, p's order), extended by captures c0.. (schur_gather_extend, the
+ * appended-problem path), against the plan built afresh for all of p with the
+ * same layout.  *identical = 1 when every array agrees; *n_dest the
+ * destinations of the full plan. */
+int arslam_debug_gather_extend(const arslam_soa_problem *p, int c0, int *identical, int *n_dest);
 
 #ifdef __cplusplus
 }

@@ -175,3 +175,16 @@ def test_rank_split_partitions_the_factorization(L, name, worlds):
     if name == "cfg3":
         info, _ = L.debug_rank_split(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, 2, 0)
         assert info["n_top_tiles"] <= 100 and info["n_top_tiles"] * 32768 < 4e6
+
+
+@pytest.mark.parametrize("name,cuts", [("small", [1, 17, 40]), ("cfg2", [300, 700, 999])])
+def test_gather_plan_extension_equals_a_fresh_plan(L, name, cuts):
+    """The appended-problem path (try_extend) extends the loaded Schur gather plan by the new
+    captures' contributions instead of rebuilding it: every destination keeps its contributions in
+    capture order (the gather's fixed summation order) and gains the new ones after them.  The
+    result must be the fresh plan of the grown problem, array for array."""
+    g = synth.config_graph(name)
+    for c0 in cuts:
+        same, nd = L.debug_gather_extend(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, c0)
+        assert same, (name, c0)
+        assert nd > 0
