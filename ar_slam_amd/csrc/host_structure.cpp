@@ -72,6 +72,7 @@ struct Dissector {
   const std::vector<std::vector<int>> &adj;
   const std::vector<double> &xyz;   // optional 3-D embedding (tag positions), 3 per node
   int leaf;
+  bool fast = false;
   std::vector<int> mark, lev;
   int next_tag = 1;
   std::vector<std::vector<int>> parts;   // elimination order
@@ -227,7 +228,12 @@ struct Dissector {
     std::vector<std::pair<double, int>> pr(m);
     double best_score = -1;
     std::vector<int> best_side;
-    constexpr int n_dir = 6, n_q = 20;
+    // (fast, components of up to 512 tags: half the directions and every
+    // other quantile, a quarter of the König covers -- the order was most of
+    // an incremental reload; a slightly larger fill, e.g. cfg2 213 tiles
+    // against 205)
+    const bool big = !fast || m > 512;
+    const int n_dir = big ? 6 : 3, n_q = 20, q_step = big ? 1 : 2;
     for (int k = 0; k < n_dir; ++k) {
       // cut directions in the plane of the two principal axes
       const double ang = M_PI * k / n_dir, ca = std::cos(ang), sa = std::sin(ang);
@@ -238,7 +244,7 @@ struct Dissector {
         pr[i] = {dir[0] * xyz[3L * u] + dir[1] * xyz[3L * u + 1] + dir[2] * xyz[3L * u + 2], u};
       }
       std::sort(pr.begin(), pr.end());
-      for (int qi = 3 * n_q / 10; qi <= 7 * n_q / 10; ++qi) {   // cut at quantiles 0.30 .. 0.70
+      for (int qi = 3 * n_q / 10; qi <= 7 * n_q / 10; qi += q_step) {   // cut at quantiles 0.30 .. 0.70
         const int cut = m * qi / n_q;
         if (cut < 1 || cut >= m) continue;
         for (int i = 0; i < m; ++i) side[pr[i].second] = i < cut ? 1 : 2;
@@ -365,8 +371,9 @@ std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj) {
 }
 
 std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf,
-                                       const std::vector<double> &xyz) {
+                                       const std::vector<double> &xyz, bool fast) {
   Dissector d(adj, xyz, leaf);
+  d.fast = fast;
   std::vector<int> all(n);
   for (int i = 0; i < n; ++i) all[i] = i;
   d.run(all, 0);
@@ -607,7 +614,7 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
 
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
                              const ReduceMaxU8 &pattern_max,
-                             const std::vector<int> *reuse_tag_row, long reuse_edges) {
+                             const std::vector<int> *reuse_tag_row, long reuse_edges, bool fast_order) {
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: layout phases
   auto clk = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   double tl[5] = {prof ? clk() : 0.0, 0, 0, 0, 0};
@@ -661,8 +668,9 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   for (auto &v : adj) L.n_edges += (long)v.size();
   if (prof) tl[1] = clk();
   bool reuse = reuse_tag_row && (int)reuse_tag_row->size() == std::max(nt, 1) && 10 * L.n_edges <= 11 * reuse_edges;
-  L.order_edges = reuse ? reuse_edges : L.n_edges;
   for (int t = 0; reuse && t < nt; ++t) reuse = ((*reuse_tag_row)[t] >= 0) == (tfree[t] != 0);
+  L.order_edges = reuse ? reuse_edges : L.n_edges;
+  L.order_reused = reuse;
   std::vector<std::vector<int>> parts;
   if (reuse) {
     // (the earlier order; rows below)
@@ -673,7 +681,7 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
       for (int a = 0; a < 3; ++a) xyz[3L * t + a] = h.x0[3 + 6L * nc + 6L * t + a];
     // leaves of up to 32 tags (192 rows = 3 whole tiles): a smaller dissection
     // would not shorten the elimination tree, only add padding and parts
-    parts = nd_parts(nt, adj, 32, xyz);
+    parts = nd_parts(nt, adj, 32, xyz, fast_order);
   } else {
     std::vector<int> order;
     if (ordering == 1 && nt > 1) order = rcm_order(nt, adj);

@@ -60,8 +60,10 @@ std::vector<int> rcm_order(int n, const std::vector<std::vector<int>> &adj);
 // Nested-dissection parts (leaves and separators) in elimination order.
 // xyz (optional, 3 per node): an embedding for geometric separators; the
 // smaller of the geometric and the BFS-level separator is used.
+// (fast: components of up to 512 tags try a quarter of the geometric cuts --
+// for the reorders of a growing incremental problem)
 std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>> &adj, int leaf,
-                                       const std::vector<double> &xyz = {});
+                                       const std::vector<double> &xyz = {}, bool fast = false);
 
 HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum);
 
@@ -92,6 +94,7 @@ struct ReducedLayout {
   double scalar_flops = 0.0;        // flops of the scalar Cholesky of the real rows in this order
   long n_edges = 0;                 // co-visibility edges (directed) among the free tags
   long order_edges = 0;             // edges when the tag order was computed (n_edges unless reused)
+  bool order_reused = false;        // the tag order is the caller's earlier one
 };
 
 // Flops of the scalar (row-level) Cholesky of the reduced system in the row
@@ -108,7 +111,8 @@ double scalar_cholesky_flops(const std::vector<std::vector<int>> &adj, const std
 // keeps its elimination order until the fill it was made for is outdated.
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
                              const ReduceMaxU8 &pattern_max,
-                             const std::vector<int> *reuse_tag_row = nullptr, long reuse_edges = 0);
+                             const std::vector<int> *reuse_tag_row = nullptr, long reuse_edges = 0,
+                             bool fast_order = false);
 
 // Deterministic Schur assembly.  k_schur stores capture c's local reduced
 // system at slab + cap_off[c] block-packed: local blocks U = 0 (f, 1 row),

@@ -391,10 +391,56 @@ struct arslam_lm {
   std::vector<int> loc_obs_cap, loc_obs_tag;
   std::vector<unsigned char> loc_cap_const;
   double split_top_work = 0.0, split_max_rank_work = 0.0, split_total_work = 0.0;
+  // co-visibility of the free tags (a bit matrix, directed edge count as
+  // ReducedLayout::n_edges), kept up to date through appends: an appended
+  // problem whose graph outgrew the one its elimination order was computed
+  // for by more than a tenth reloads with a fresh order (a stale order on the
+  // incremental cfg2 flow: 18 elimination-tree levels and 358 us per
+  // factorization against 10 and 217 us fresh)
+  std::vector<uint64_t> covis;
+  long covis_nt = 0, covis_edges = 0;
+  void covis_build(const arslam::HostProblem &h, const arslam::ReducedLayout &L) {
+    covis_nt = h.nt <= 16384 ? h.nt : 0;
+    covis_edges = 0;
+    covis.assign(((size_t)covis_nt * covis_nt + 63) / 64, 0);
+    for (int c = 0; c < h.nc && covis_nt; ++c) covis_add(h, L, c);
+  }
+  void covis_add(const arslam::HostProblem &h, const arslam::ReducedLayout &L, int c) {
+    if (!covis_nt) return;
+    for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a)
+      for (int b = h.cap_blk_start[c]; b < h.cap_blk_start[c + 1]; ++b) {
+        const int ta = h.blk_tag[a], tb = h.blk_tag[b];
+        if (ta == tb || L.tag_row[ta] < 0 || L.tag_row[tb] < 0) continue;
+        const size_t bit = (size_t)ta * covis_nt + tb;
+        if (!(covis[bit >> 6] >> (bit & 63) & 1)) {
+          covis[bit >> 6] |= 1ull << (bit & 63);
+          ++covis_edges;
+        }
+      }
+  }
   bool reuse_order = false;  // load(): keep the previous tag order when the free tags are unchanged
   std::vector<int> prev_tag_row;
   int prev_ordering = -1, prev_skip = -1;
   long prev_order_edges = 0;
+  // the capture count the order was computed at: nested dissection cuts along
+  // the tags' positions, which the first solves of an incremental flow only
+  // roughly know, so a grown problem (by a quarter) gets a fresh order even if
+  // its co-visibility graph barely changed (incremental cfg2: an order kept
+  // from the first load gave 18 elimination-tree levels, a fresh one 10)
+  int prev_order_nc = 0;
+  int prev_order_height = 0;   // tile elimination-tree height of the layout the order was computed for
+  static int etree_height(const arslam::ReducedLayout &L) {
+    std::vector<uint8_t> P = L.pattern;
+    std::vector<int> parent;
+    arslam::tile_fill(L.T, P, parent);
+    std::vector<int> lev(L.T, 1);
+    int h = 0;
+    for (int k = 0; k < L.T; ++k) {   // (parents have larger indices)
+      if (parent[k] >= 0) lev[parent[k]] = std::max(lev[parent[k]], lev[k] + 1);
+      h = std::max(h, lev[k]);
+    }
+    return h;
+  }
   void linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
   // linearize split at the host read: enqueue (results copied to h_lin), collect after a sync
   void linearize_launch();
@@ -462,7 +508,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   // are unchanged keeps the previous elimination order: the ordering (nested
   // dissection) is the largest part of the host setup
   const bool can_reuse = reuse_order && !prev_tag_row.empty() && prev_ordering == opt.reduced_ordering &&
-                         prev_skip == opt.cholesky_skip_zero_tiles;
+                         prev_skip == opt.cholesky_skip_zero_tiles && 4L * p->n_cap <= 5L * prev_order_nc;
   arslam::HostProblem h;
   arslam::ReducedLayout L;
   std::vector<int> col_class;
@@ -522,8 +568,16 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
       if (sl >= 3) sl -= (int)shift;
   } else {
     h = arslam::host_problem(p, nullptr);   // validates p
+    // (a grown pointer-keyed problem: a fresh order takes the faster separator search)
     L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
-                               can_reuse ? &prev_tag_row : nullptr, prev_order_edges);
+                               can_reuse ? &prev_tag_row : nullptr, prev_order_edges, reuse_order);
+    // A kept order whose tile elimination tree grew taller than the fresh
+    // order's by more than a level (new co-visibility across its separators:
+    // 10 -> 14 -> 20 levels within a few loads of the incremental cfg2 flow)
+    // is recomputed: the factorization is chain-bound, the order ~3 ms.
+    if (L.order_reused && L.nR > 0 && etree_height(L) > prev_order_height + 1)
+      L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
+                                 nullptr, 0, true);
   }
   tp[1] = now_s();
   ensure_stream();
@@ -535,8 +589,13 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   nb_global = h.nb_global;
   slot_free = h.slot_free;
   x0 = h.x0;
+  if (!L.order_reused) {
+    prev_order_nc = h.nc;
+    prev_order_height = L.nR > 0 ? etree_height(L) : 0;
+  }
   prev_tag_row = L.tag_row;
   prev_order_edges = L.order_edges;
+  if (nranks == 1) covis_build(h, L);
   prev_ordering = opt.reduced_ordering;
   prev_skip = opt.cholesky_skip_zero_tiles;
   tp[2] = now_s();
@@ -561,8 +620,9 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   pk_appended_only = true;
   setup_s = now_s() - t_load;
   if (prof)
-    std::fprintf(stderr, "arslam setup: nc %d nt %d host+layout %.3f plan %.3f gather+upload %.3f ms\n",
-                 nc, nt, 1e3 * (tp[1] - tp[0]), 1e3 * (tp[3] - tp[2]), 1e3 * (tp[5] - tp[4]));
+    std::fprintf(stderr, "arslam setup: nc %d nt %d host+layout %.3f plan %.3f gather+upload %.3f ms (order %s, %d levels, %ld tiles)\n",
+                 nc, nt, 1e3 * (tp[1] - tp[0]), 1e3 * (tp[3] - tp[2]), 1e3 * (tp[5] - tp[4]),
+                 prev_order_nc == nc ? "fresh" : "kept", plan.nlev, (long)plan.n_tiles);
 }
 
 // Everything the device needs from the host structure, the layout and the
@@ -718,6 +778,11 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
           grown.emplace_back(ts[a], ts[b]);
         }
   }
+  // the co-visibility graph the order was computed for, outgrown by a tenth: reload with a fresh order
+  for (int c = 0; c < h.nc; ++c)
+    if (touched[c]) covis_add(h, lay, c);
+  if (covis_nt && 10 * covis_edges > 11 * prev_order_edges) return false;
+  if (4L * h.nc > 5L * prev_order_nc) return false;   // (a quarter more captures: a fresh order)
   for (const auto &g : grown) lay.pattern[(size_t)g.first * T + g.second] = 1;
   // only new captures got residual blocks: their contributions extend the gather plan
   const int extend_from = first_touched >= nc ? nc : -1;

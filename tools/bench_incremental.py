@@ -45,4 +45,6 @@ print(json.dumps({"flow": f"solveIncremental, {name}: {g.n_cap} captures / {g.n_
                   "other_ms_per_solve": 1e3 * (wall - setup - mini) / n,
                   "device_phase_ms_per_solve": {k[2:-3]: round(v / n, 4) for k, v in ph.items()},
                   "setup_kinds": {"load": kinds[0], "values": kinds[1], "append": kinds[2]},
-                  "final_rms_px": last["final_rms_px"], "final_termination": last["termination"]}))
+                  "final_rms_px": last["final_rms_px"], "final_termination": last["termination"],
+                  "last_plan": {k: last[k] for k in ("n_factor_tiles", "n_levels", "n_update_tiles",
+                                                     "factor_scalar_flops", "n_reduced")}}))
