@@ -1568,7 +1568,7 @@ int arslam_lm_options_init(arslam_lm_options *o) {
   o->reduced_ordering = 2;
   o->kernel_timing = 0;
   o->factor_executor = 1;
-  o->phase_timing = 1;
+  o->phase_timing = 0;
   o->device_loop = 0;   // (measured slower than the host loop: DESIGN.md section 6)
   return ARSLAM_OK;
 }

@@ -471,7 +471,7 @@ void ArSlamSolver::optimize(const Capture &capture) {   // :1001-1018
   rec.capture_uid = capture.uid;
   rec.capture_idx = capture.handle.idx;
   check(arslam_lm_solve(problem_, &rec.summary));
-  solve_log_.push_back(rec);
+  solve_log_.push_back(std::move(rec));
 }
 
 void ArSlamSolver::resetProblem() { check(arslam_lm_reset(problem_)); }   // :1021-1025

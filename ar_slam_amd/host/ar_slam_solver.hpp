@@ -163,7 +163,7 @@ class ArSlamSolver {
   const CameraParams &camera() const { return camera_; }
   std::optional<CaptureHandle> findCapture(const std::string &uid) const;
   std::optional<ArucoHandle> findAruco(const std::string &id) const;
-  const std::vector<SolveRecord> &solveLog() const { return solve_log_; }
+  const std::deque<SolveRecord> &solveLog() const { return solve_log_; }
   const std::unordered_set<CaptureHandle, CaptureHandleHash> &unsolvedCaptures() const { return unsolved_captures_; }
   void setVerbose(bool v) { verbose_ = v; }
 
@@ -193,7 +193,7 @@ class ArSlamSolver {
   // the reference's container and hash (ar_slam_util.hpp:140-145, 492): solveIncremental
   // visits the unsolved captures in its iteration (bucket) order
   std::unordered_set<CaptureHandle, CaptureHandleHash> unsolved_captures_;
-  std::vector<SolveRecord> solve_log_;
+  std::deque<SolveRecord> solve_log_;   // (records are ~90 KB: no reallocation copies)
   bool verbose_ = false;
 };
 

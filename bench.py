@@ -366,14 +366,18 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_incremental and args.config == "cfg3":
+            print("bench: incremental cfg2 flow", file=sys.stderr, flush=True)
             out["incremental_cfg2"] = bench_incremental("cfg2")
         if world == 1 and args.config == "cfg3" and not args.no_localize:
+            print("bench: cfg5 localize batch", file=sys.stderr, flush=True)
             out["localize_cfg5"] = bench_localize(args, world, rank, side=True)
         if world == 1 and not args.no_cpu_baseline:
-            # every CPU this process is granted (the box's cpuset: one GPU's share of the node;
-            # lscpu in host_cpu shows the whole node)
+            # every CPU this process is granted: the box gives one GPU's share of the node
+            # (OMP_NUM_THREADS, 16 on the GPU box) while nproc / lscpu report the whole node
+            # (recorded beside it); more threads than the share only oversubscribe it
             host = host_cpu_info()
-            threads = args.cpu_threads or host["nproc"]
+            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or min(host["nproc"], 16)
+            print(f"bench: CPU baseline on {threads} threads", file=sys.stderr, flush=True)
             out["cpu_baseline"] = cpu_baseline(g, threads, args.config)
             out["cpu_baseline"]["host_cpu"] = host
             if args.config == "cfg3":   # plus the reference's own setting (Ceres num_threads = 1) on cfg2

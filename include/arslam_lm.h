@@ -102,8 +102,8 @@ typedef struct {
   int kernel_timing;                 /* 1: HIP events around every launch of the dominant kernel */
   int factor_executor;               /* reduced-system Cholesky: 0 two launches per elimination-tree
                                         level, 1 one persistent task-graph launch (default) */
-  int phase_timing;                  /* 1 (default): HIP events around each phase of the step
-                                        (summary t_*_ms; host loop only); 0: none (each event
+  int phase_timing;                  /* 1: HIP events around each phase of the step (summary
+                                        t_*_ms; host loop only); 0 (default): none (each event
                                         record costs a few microseconds of GPU time) */
   int device_loop;                   /* 1: the LM decisions (step acceptance, radius, termination)
                                         run on the device and the host enqueues iterations ahead,

@@ -16,12 +16,16 @@ from ar_slam_amd import build, lm, synth  # noqa: E402
 build.build()
 name = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
 g = synth.config_graph(name)
-s = lm.SlamSolver()
+# (default options, as a drop-in user gets them; ARSLAM_PHASES=1: per-phase device times)
+s = lm.SlamSolver(phase_timing=int(os.environ.get("ARSLAM_PHASES", "0")))
 s.set_camera(g.camera)
 t0 = time.perf_counter()
+t_add = 0.0
 for c in range(g.n_cap):
     sel = g.obs_cap == c
+    ta = time.perf_counter()
     s.add_detections(f"cap{c}", [f"tag_{t}" for t in g.obs_tag[sel]], g.corners[sel])
+    t_add += time.perf_counter() - ta
     s.solve_incremental()
 wall = time.perf_counter() - t0
 n = s.num_solves
@@ -43,6 +47,7 @@ print(json.dumps({"flow": f"solveIncremental, {name}: {g.n_cap} captures / {g.n_
                   "wall_s": wall, "solves": n, "lm_iterations": iters,
                   "setup_ms_per_solve": 1e3 * setup / n, "minimizer_ms_per_solve": 1e3 * mini / n,
                   "other_ms_per_solve": 1e3 * (wall - setup - mini) / n,
+                  "add_detections_ms_per_message": 1e3 * t_add / g.n_cap,
                   "device_phase_ms_per_solve": {k[2:-3]: round(v / n, 4) for k, v in ph.items()},
                   "setup_kinds": {"load": kinds[0], "values": kinds[1], "append": kinds[2]},
                   "final_rms_px": last["final_rms_px"], "final_termination": last["termination"],
