@@ -902,8 +902,9 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
     if (plan.arena) (void)hipFree(plan.arena);
     plan.arena = nullptr;
     plan.arena_bytes = 0;
-    check(hipMalloc(&plan.arena, total), "hipMalloc(plan arena)");
-    plan.arena_bytes = total;
+    const size_t want = total + total / 2;   // (grows by half again: a growing problem reallocates rarely)
+    check(hipMalloc(&plan.arena, want), "hipMalloc(plan arena)");
+    plan.arena_bytes = want;
   }
   std::vector<char> host(staged);
   for (size_t i = 0; i < pieces.size(); ++i) {

@@ -101,11 +101,14 @@ struct DevBuf {
 struct PinnedBuf {
   double *p = nullptr;
   size_t cap = 0;
-  void alloc(size_t count) {   // grows only; keeps the buffer across solves
+  void alloc(size_t count) {   // grows only (by half again: page-locking is slow); kept across solves
     if (count <= cap) return;
     if (p) (void)hipHostFree(p);
-    HIP_CHECK(hipHostMalloc(&p, count * sizeof(double), hipHostMallocDefault));
-    cap = count;
+    p = nullptr;
+    cap = 0;
+    const size_t want = count + count / 2;
+    HIP_CHECK(hipHostMalloc(&p, want * sizeof(double), hipHostMallocDefault));
+    cap = want;
   }
   ~PinnedBuf() {
     if (p) (void)hipHostFree(p);
@@ -1477,6 +1480,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->minimizer_time_s = now_s() - t_start;
   write_back(d_xbest.p);
   s->total_time_s = now_s() - t_start;
+  static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
+  if (prof) std::fprintf(stderr, "arslam write_back %.3f ms\n", 1e3 * (s->total_time_s - s->minimizer_time_s));
   const long nb_all = nb_global;
   s->n_obs = (int)nb_all;
   s->final_rms_px = nb_all ? std::sqrt(2.0 * s->final_cost / (4.0 * nb_all)) : 0.0;
@@ -1676,6 +1681,7 @@ int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
       summary->termination = ARSLAM_CONVERGENCE;
       return;
     }
+    const double t_stage = now_s();
     const int nc = (int)h->cap_ptrs.size(), nt = (int)h->tag_ptrs.size();
     std::vector<double> cam(h->camera_ptr, h->camera_ptr + 3), cap(6L * nc), tag(6L * nt);
     std::vector<unsigned char> cc(nc), tc(nt);
@@ -1709,6 +1715,8 @@ int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
       h->pk_loaded = true;
       h->pk_dirty = false;
     }
+    static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
+    if (prof) std::fprintf(stderr, "arslam stage+setup %.3f ms\n", 1e3 * (now_s() - t_stage));
     h->pk_stage = &p;
     // the final write_back also writes the caller's blocks (Ceres writes parameters back;
     // every iteration under update_state_every_iteration)
