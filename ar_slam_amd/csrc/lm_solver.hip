@@ -717,7 +717,8 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.n_items = n_items; P.n_splits = n_splits;
   ++problem_epoch;   // (captured LM iterations hold the old arrays)
   const double tu2 = prof ? now_s() : 0.0;
-  HIP_CHECK(hipStreamSynchronize(stream));   // the upload's sources go out of scope
+  // (no sync: the copy reads the arena's page-locked image, which stays
+  // untouched until the next upload -- after this solve's syncs)
   if (prof)
     std::fprintf(stderr, "arslam upload: gather plan %.3f arena+allocs %.3f sync %.3f ms\n", 1e3 * (tu1 - tu0),
                  1e3 * (tu2 - tu1), 1e3 * (now_s() - tu2));
