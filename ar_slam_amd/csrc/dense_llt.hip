@@ -936,6 +936,38 @@ __device__ __forceinline__ void load_tiles_ltd_wt(const double *__restrict__ g1,
     if (e < kL) *reinterpret_cast<dbl2 *>(LTd + 2 * e) = v[16 + u];
   }
 }
+// Half a 64x64 tile (128 threads, t2 = 0..127: 16-byte element u * 128 + t2
+// into v[u]) as sixteen sc1 loads, ISSUED ONLY -- the registers hold the data
+// after ld_wt16x16_wait, and nothing may read them before (the caller keeps
+// them untouched; the pair shares one address, the second at +2048 bytes).
+__device__ __forceinline__ void ld_wt16x16_issue(const double *__restrict__ g, int t2, dbl2 v[16]) {
+  const double *p[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) p[m] = g + 2 * (2 * m * 128 + t2);
+  asm volatile(
+      "global_load_dwordx4 %0, %16, off sc1\n\t"
+      "global_load_dwordx4 %1, %16, off offset:2048 sc1\n\t"
+      "global_load_dwordx4 %2, %17, off sc1\n\t"
+      "global_load_dwordx4 %3, %17, off offset:2048 sc1\n\t"
+      "global_load_dwordx4 %4, %18, off sc1\n\t"
+      "global_load_dwordx4 %5, %18, off offset:2048 sc1\n\t"
+      "global_load_dwordx4 %6, %19, off sc1\n\t"
+      "global_load_dwordx4 %7, %19, off offset:2048 sc1\n\t"
+      "global_load_dwordx4 %8, %20, off sc1\n\t"
+      "global_load_dwordx4 %9, %20, off offset:2048 sc1\n\t"
+      "global_load_dwordx4 %10, %21, off sc1\n\t"
+      "global_load_dwordx4 %11, %21, off offset:2048 sc1\n\t"
+      "global_load_dwordx4 %12, %22, off sc1\n\t"
+      "global_load_dwordx4 %13, %22, off offset:2048 sc1\n\t"
+      "global_load_dwordx4 %14, %23, off sc1\n\t"
+      "global_load_dwordx4 %15, %23, off offset:2048 sc1\n\t"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+__device__ __forceinline__ void ld_wt16x16_wait(dbl2 v[16]) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])::"memory");
+}
 // eight 8-byte sc1 loads, waited
 __device__ __forceinline__ void ld_wt8x8(const double *const p[8], double v[8]) {
   asm volatile(
@@ -986,12 +1018,13 @@ __device__ __forceinline__ void load_two_tiles_wt(const double *__restrict__ g1,
   }
 }
 
-// 256-thread write-through store of a 64x64 LDS tile (pitch LQ), optionally
+// NT-thread write-through store of a 64x64 LDS tile (pitch LQ), optionally
 // lower triangle only
+template <int NT = 256>
 __device__ __forceinline__ void store_tile_wt(double *__restrict__ g, const double *lds, int tid, bool lower) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int e = q * 256 + tid, r = e >> 5, c2 = (e & 31) * 2;
+  for (int q = 0; q < 2048 / NT; ++q) {
+    const int e = q * NT + tid, r = e >> 5, c2 = (e & 31) * 2;
     dbl2 v = *reinterpret_cast<const dbl2 *>(lds + r * LQ + c2);
     if (lower) {
       if (c2 > r) v.x = 0.0;
@@ -1062,6 +1095,9 @@ struct DagArgs {
   const int2 *sub;            // [n_tasks] TRSM fused into a POTRF task: {tile id or -1, late-wait start}
   const int *cont;            // [n_tasks] POTRF task the same workgroup may continue with (or -1)
   const int *maxdep;          // [n_tasks] continuation targets: largest ticket they wait on; else -1
+  const int *cont_akk;        // [n_tasks] the continuation's A_kk tile if it folds this column alone, else -1
+  const int *rec;             // [n_tasks][32] each ticket's record (DagRecField)
+  const int2 *ks_tiles;       // [ks] operand tile ids of an update column
   int *claimed;               // [n_tasks] continuation targets: claimed by the predecessor or the drawer
   const int *wait_off;
   const int2 *waits;
@@ -1082,6 +1118,32 @@ struct DagArgs {
   const int *gate;            // device LM loop: the launch returns at once while *gate != 0
 };
 
+// A ticket's 32-int record: two scalar loads in flight, one wait (the record
+// array is read-only in the launch).  From LDS for a claimed continuation
+// (its predecessor copied it there beside its POTRF).
+typedef int int16v __attribute__((ext_vector_type(16)));
+struct DagRecV {
+  int16v a, b;
+  __device__ __forceinline__ int operator[](int i) const { return i < 16 ? a[i] : b[i - 16]; }
+};
+__device__ __forceinline__ DagRecV load_rec(const int *p) {
+  DagRecV r;
+  asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(r.a), "=s"(r.b)
+               : "s"(p)
+               : "memory");
+  return r;
+}
+__device__ __forceinline__ DagRecV lds_rec(const int *s) {
+  DagRecV r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    r.a[i] = __builtin_amdgcn_readfirstlane(s[i]);
+    r.b[i] = __builtin_amdgcn_readfirstlane(s[16 + i]);
+  }
+  return r;
+}
+
 __device__ __forceinline__ unsigned long long realtime() {
   unsigned long long t;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1098,12 +1160,14 @@ __device__ __forceinline__ unsigned long long realtime() {
 __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   if (gated(a.gate)) return;
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
-  __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 8 + T64];
+  __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 12 + 16 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
   // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation,
-  // [6] its fetch requested, [8..10] the POTRF pipeline's flags, [11] thirds of that tile loaded
+  // [6] its fetch requested, [8..10] the POTRF pipeline's flags, [11] thirds of that tile loaded,
+  // [16..17] the continuation's A_kk halves in D, [20..21] its early waits seen met by waves 2-3
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
-  double *colx = LTd + 4 * 16 * LI + 8;   // POTRF pivot scratch (X stays free for the prefetch)
+  int *sh_rec = sh + 24;                        // the claimed continuation's record
+  double *colx = LTd + 4 * 16 * LI + 12 + 16;   // POTRF pivot scratch (X stays free for the prefetch)
   int *ready = a.counters, *applied = a.counters + a.n_tiles, *ticket = a.ticket;
   // claimed continuation targets in flight.  A target is claimed once its
   // EARLY waits are all drawn; its late waits may name undrawn tickets, so at
@@ -1152,7 +1216,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       next = sh[0];
       __syncthreads();
     }
-    const int t = next;
+    const int t = __builtin_amdgcn_readfirstlane(next);
     const int pk = prev_k;   // a claimed continuation: the predecessor's column (its L_{k,pk} is in X)
     const bool premet = cont && next_met;   // (only for the claimed target it was polled for)
     next = -1;
@@ -1161,18 +1225,19 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     DAG_PROGRESS(0, t);
     DAG_PROGRESS(1, 1);
     if (t >= a.t_end) break;
-    const int4 task = a.tasks[t];
+    const DagRecV r = cont ? lds_rec(sh_rec) : load_rec(a.rec + (long)t * kDagRecInts);
+    const int4 task = make_int4(r[kRecType], r[kRecY], r[kRecZ], r[kRecW]);
     DAG_PROGRESS(2, task.x);
     if (a.trace && tid == 0) { a.trace[8L * t] = realtime(); a.trace[8L * t + 3] = blockIdx.x; }
-    const int2 sub = a.sub[t];
+    const int2 sub = make_int2(r[kRecSub], r[kRecLate]);
     if (w == 0) {
       // (sub.y: the end of the early waits; the late ones are a fused TRSM's,
       // or a folded TRSM's L_kk)
-      const bool ok = premet || dag_wait(a.counters, a.waits, a.wait_off[t], sub.y, a.flag, lane, task.x != 2);
+      const bool ok = premet || dag_wait(a.counters, a.waits, r[kRecWait0], sub.y, a.flag, lane, task.x != 2);
       if (lane == 0) {
         if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
         // a drawn continuation target: run it only if its predecessor did not claim it
-        sh[2] = (cont || a.maxdep[t] < 0 || atomicCAS(a.claimed + t, 0, 1) == 0) ? 1 : 0;
+        sh[2] = (cont || r[kRecMaxdep] < 0 || atomicCAS(a.claimed + t, 0, 1) == 0) ? 1 : 0;
       }
     }
     __syncthreads();
@@ -1185,20 +1250,42 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // ---- POTRF k: publish L_kk and its 16x16 block inverses, then (off the
       // critical path) the full inverse for the backward solve ----
       const int k = task.y;
+      // The continuation's A_kk, prefetched by waves 2-3 into registers beside
+      // the last POTRF panel once its early waits are met (apf: the target
+      // folds this task's solved tile alone, so A_kk is all it loads).  This
+      // task's tile stores are then made by waves 0-1 alone, so their release
+      // (s_waitcnt vmcnt(0)) never waits for those loads; waves 2-3 move the
+      // registers into D after the fused solve, as the target's A_kk.
+      const int c = sub.x >= 0 ? r[kRecCont] : -1;
+#ifndef ARSLAM_NO_APF
+      const int apf_tile = sub.x >= 0 ? r[kRecContAkk] : -1;
+#else
+      const int apf_tile = -1;
+#endif
+      const bool apf = apf_tile >= 0;
+      const double *apf_src = a.S + (long)max(apf_tile, 0) * (T64 * T64);
+      bool ap_met = false;   // waves 2-3: the target's early waits seen met beside the last panel
+      int c_rec = 0;         // wave 3 (lanes 0-31): the target's record, bound for sh_rec
+      int2 c_wait = make_int2(0, 0);   // waves 2-3: lane q's early wait of the target
+      dbl2 apv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) apv[u] = dbl2{0.0, 0.0};
+      bool ap_ok = false;
       // this CU's flag is up from the fold to the end of the factorization,
       // never across a wait (an update held on this CU may be what a wait
       // needs; the early waits are met here, the late ones come after)
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int4 fit = task.z >= 0 ? a.items[task.z] : make_int4(0, 0, 0, 0);
+      const int4 fit = make_int4(0, r[kRecQ0], r[kRecQ1], 0);
       // a one-column folded update runs inside the factorization (fold_f: its
       // L_kj tile in X -- the predecessor's solved tile for a continuation,
       // else loaded beside A_kk); several columns fold first, as one GEMM pass
       const bool fold_in = task.z >= 0 && fit.z - fit.y == 1;
       if (fold_in) {
-        const double *Akk = tile_ptr(a.S, a.tid_map, a.T, k, k);
-        if (cont && a.ks[fit.y] == pk) load_tile_wt(Akk, D, tid);
-        else load_two_tiles_wt(Akk, D, tile_ptr(a.S, a.tid_map, a.T, k, a.ks[fit.y]), X, tid);
+        const double *Akk = a.S + (long)task.w * (T64 * T64);
+        if (cont && r[kRecFoldK0] == pk) {
+          if (!(sh[16] && sh[17])) load_tile_wt(Akk, D, tid);   // (else its predecessor's waves 2-3 put it in D)
+        } else load_two_tiles_wt(Akk, D, a.S + (long)r[kRecFoldTile0] * (T64 * T64), X, tid);
       } else if (task.z >= 0) {
         // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
         const int4 it = fit;
@@ -1207,7 +1294,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // accumulator layout, sc1 loads in flight during the fold's GEMMs
         double akk[16];
         {
-          const double *Akk = tile_ptr(a.S, a.tid_map, a.T, k, k);
+          const double *Akk = a.S + (long)task.w * (T64 * T64);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
@@ -1224,7 +1311,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
             continue;
           }
           if (q > it.y) __syncthreads();
-          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, a.ks[q]), D, tid);
+          load_tile_wt(a.S + (long)a.ks_tiles[q].x * (T64 * T64), D, tid);
           __syncthreads();
           gemm64_nt(D, D, tid, acc);
         }
@@ -1236,7 +1323,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           for (int reg = 0; reg < 4; ++reg) D[(rb + lk + 4 * reg) * LQ + cb + li] = akk[4 * q + reg] - acc[q][reg];
         }
       } else {
-        load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, k, k), D, tid);
+        load_tile_wt(a.S + (long)task.w * (T64 * T64), D, tid);
       }
       __syncthreads();
       if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
@@ -1244,7 +1331,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // the first diagonal block, if its late waits are already met;
       // otherwise it is waited for and loaded after L_kk is published.
       const double *pf_src = sub.x >= 0 ? a.S + (long)sub.x * (T64 * T64) : nullptr;
-      const int pw0 = sub.y, pw1 = a.wait_off[t + 1];
+      const int pw0 = sub.y, pw1 = r[kRecWait1];
       // A tile whose waits were not met at panel 0 is polled again by wave 1
       // beside panels 1 and 2 (the request in sh[6]) and fetched by waves 1-3,
       // a third each, beside the next panel: on the late elimination-tree chain
@@ -1257,6 +1344,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // the whole tile.
       bool third_done = false;
       const bool ok = blocked_potrf64_async(D, inv, LTd, sh + 1, sh + 8, tid, colx, [&](int p, int wv, int ln) {
+        auto fetch_third = [&]() {
         auto poll = [&]() {
           if (!pf_src || pw1 - pw0 > 64) return false;
           const int q = pw0 + ln;
@@ -1313,6 +1401,34 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           third_done = true;
           lds_add(sh + 11, ln);
         }
+        };
+        fetch_third();
+        // waves 2-3 and the continuation target: its record into LDS (wave 3,
+        // issued beside panel 1, stored beside panel 2), its early-wait list
+        // (beside panel 2) and their counters (beside panel 3, where wave 0
+        // waits for nothing from them): loads in flight across a panel, so no
+        // round trip delays an update round wave 0 waits for
+        if (c >= 0 && wv >= 2) {
+          const int cw0 = r[kRecContWait0], cw1 = r[kRecContLate];
+          if (p == 1 && wv == 3 && ln < kDagRecInts) c_rec = a.rec[(long)c * kDagRecInts + ln];
+          if (p == 2) {
+            if (wv == 3 && ln < kDagRecInts) sh_rec[ln] = c_rec;
+            const int q = cw0 + ln;
+            if (q < cw1) c_wait = a.waits[q];
+          }
+          if (p == 3) {
+            bool met = false;
+            if (cw1 - cw0 <= 64) {
+              const int q = cw0 + ln;
+              // (the tile this task solves counts as met)
+              const bool mine = q < cw1 && c_wait.x != sub.x;
+              const int got = mine ? ld_acquire_relaxed(a.counters + c_wait.x) : 0;
+              met = __builtin_amdgcn_ballot_w64(mine && got < c_wait.y) == 0;
+            }
+            if (ln == 0) sh[20 + wv - 2] = met ? 1 : 0;
+            ap_met = met && apf;
+          }
+        }
       }, X, fold_in);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1322,8 +1438,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         while (first < T64 && D[first * LQ + first] > 0.0) ++first;
         atomicCAS(a.flag, 0, 1 + k * T64 + first);
       }
-      store_tile_wt(a.Ld + (long)k * T64 * T64, D, tid, true);
       double *ltd_g = a.ltd + (long)k * kLtdSize;
+      store_tile_wt(a.Ld + (long)k * T64 * T64, D, tid, true);
       for (int e = tid; e < kLtdSize / 2; e += 256)
         st_wt16(ltd_g + 2 * e, *reinterpret_cast<const dbl2 *>(LTd + 2 * e));
       dag_release(tid);
@@ -1334,12 +1450,11 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         const bool pref = sh[11] >= 3;   // (written inside the POTRF, barriers since)
         if (!pref) {
           if (w == 0) {
-            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, a.wait_off[t + 1], a.flag, lane, true);
+            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, r[kRecWait1], a.flag, lane, true);
             if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
           }
           __syncthreads();
         }
-        const int c = a.cont[t];
         double *Ct = a.S + (long)sub.x * (T64 * T64);
         // The continuation claim's round trips ride along the solve instead of
         // following it: the ticket count and the in-flight reservation go out
@@ -1352,46 +1467,56 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // prefetched into registers here was measured neutral: the release
         // before the counter bump, s_waitcnt vmcnt(0), then waits for it.)
         int tk_seen = 0, infl_old = 0;
-        bool c_poll = false, c_mine = false;
-        int c_got = 0, c_need = 0;
-        if (c >= 0) {
-          if (tid == 0) {
-            tk_seen = ld_acquire_relaxed(ticket);
-            infl_old = atomicAdd(inflight, 1);
-          }
-          const int cw0 = a.wait_off[c], cw1 = a.sub[c].y;
-          c_poll = cw1 - cw0 <= 63;
-          const int q = cw0 + lane - 1;
-          if (c_poll && lane >= 1 && q < cw1) {
-            const int2 cv = a.waits[q];
-            if (cv.x != sub.x) {   // (the tile this task publishes below counts as met)
-              c_mine = true;
-              c_need = cv.y;
-              c_got = ld_acquire_relaxed(a.counters + cv.x);
-            }
-          }
+        if (c >= 0 && tid == 0) {
+          tk_seen = ld_acquire_relaxed(ticket);
+          infl_old = atomicAdd(inflight, 1);
         }
         if (!pref) load_tile_wt(Ct, X, tid);
+        if (ap_met) {   // waves 2-3: the continuation's A_kk in flight during the solve
+          int t2 = tid - 128;
+          asm volatile("" : "+v"(t2));
+          ld_wt16x16_issue(apf_src, t2, apv);
+          ap_ok = true;
+        }
         __syncthreads();
         // blocked_trsm64, its steps inline (row block w per wave)
         trsm_step(X, D, LTd, w, 0, lane);
         trsm_step(X, D, LTd, w, 1, lane);
-        const bool c_met = c_poll && __builtin_amdgcn_ballot_w64(c_mine && c_got < c_need) == 0;
         trsm_step(X, D, LTd, w, 2, lane);
         trsm_step(X, D, LTd, w, 3, lane);
-        if (lane == 0) sh[12 + w] = c_met ? 1 : 0;
         __syncthreads();
         // claim the continuation target before the tile is published: its
         // drawer waits for this tile, so it cannot have claimed it yet
         int claim = -1;
         if (c >= 0 && tid == 0) {
-          if (a.t_begin + tk_seen > a.maxdep[c] && infl_old < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0)
+          if (a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0)
             claim = c;
           else
             atomicSub(inflight, 1);
         }
-        store_tile_wt(Ct, X, tid, false);
-        dag_release(tid);
+        if (!apf) {
+          store_tile_wt(Ct, X, tid, false);
+          if (tid == 0) sh[16] = sh[17] = 0;
+          dag_release(tid);
+        } else {
+          if (w < 2) {
+            store_tile_wt<128>(Ct, X, tid, false);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          } else {
+            // the continuation's A_kk into D (free: L_kk's last reader was the solve)
+            if (ap_ok) {
+              ld_wt16x16_wait(apv);
+              const int t2 = tid - 128;
+#pragma unroll
+              for (int u = 0; u < 16; ++u) {
+                const int e = u * 128 + t2, r = e >> 5, c2 = (e & 31) * 2;
+                *reinterpret_cast<dbl2 *>(D + r * LQ + c2) = apv[u];
+              }
+            }
+            if (lane == 0) sh[16 + w - 2] = ap_ok ? 1 : 0;
+          }
+          __syncthreads();
+        }
         if (tid == 0) {
           sh[4] = claim;
           __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1399,7 +1524,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
         __syncthreads();
         next = sh[4];
-        next_met = next >= 0 && sh[12] && sh[13] && sh[14] && sh[15];
+        next_met = next >= 0 && sh[20] && sh[21];
         if (next >= 0) prev_k = k;
       }
     } else if (task.x == 3) {
@@ -1417,8 +1542,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       }
     } else if (task.x == 1) {
       // ---- TRSM i,k: L_ik L_kk^T = A_ik, blocked with the 16x16 inverses ----
-      const int i = task.y, k = task.z;
-      double *Ct = tile_ptr(a.S, a.tid_map, a.T, i, k);
+      const int k = task.z;
+      double *Ct = a.S + (long)task.w * (T64 * T64);
       // the tile, L_kk and its block inverses in one round trip
       load_tiles_ltd_wt(Ct, X, a.Ld + (long)k * T64 * T64, D, a.ltd + (long)k * kLtdSize, LTd, tid);
       __syncthreads();
@@ -1430,12 +1555,11 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       if (tid == 0) __hip_atomic_fetch_add(ready + task.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       // ---- update item ----
-      const int4 it = a.items[task.y];
-      const int2 pr = a.targets[it.x];
-      const int ti = pr.x, tj = pr.y, sid = it.w;
+      const int4 it = make_int4(0, r[kRecQ0], r[kRecQ1], r[kRecSid]);
+      const int ti = r[kRecTi], tj = r[kRecTj], sid = it.w;
       dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
       for (int q = it.y; q < it.z; ++q) {
-        const int k = a.ks[q];
+        const int2 kt = a.ks_tiles[q];   // (operand tile ids: no column -> tile lookup chain)
         if (q > it.y) __syncthreads();
         {   // hold the GEMM while a POTRF runs on this CU (bounded)
           if (tid == 0) {
@@ -1447,15 +1571,15 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           __syncthreads();
         }
         if (ti != tj)   // both operands in one round trip
-          load_two_tiles_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tile_ptr(a.S, a.tid_map, a.T, tj, k), X, tid);
+          load_two_tiles_wt(a.S + (long)kt.x * (T64 * T64), D, a.S + (long)kt.y * (T64 * T64), X, tid);
         else
-          load_tile_wt(tile_ptr(a.S, a.tid_map, a.T, ti, k), D, tid);
+          load_tile_wt(a.S + (long)kt.x * (T64 * T64), D, tid);
         __syncthreads();
         gemm64_nt(D, ti != tj ? X : D, tid, acc);   // a diagonal target: one operand tile, fetched once
       }
       bool apply = true;
       if (sid >= 0) {
-        const int2 sp = a.split[sid >> 8];
+        const int2 sp = make_int2(r[kRecSplitN], r[kRecSplitP]);
         double *mine = a.part + (long)(sp.y + (sid & 255)) * 4096;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -1503,7 +1627,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           if (!ok) atomicCAS(a.flag, 0, -(2000000 + t));
         }
         __syncthreads();
-        double *C = tile_ptr(a.S, a.tid_map, a.T, ti, tj);
+        double *C = a.S + (long)task.w * (T64 * T64);
         double cv[16];   // two groups of eight loads in flight
         {
           const double *p8[16];
@@ -1812,7 +1936,7 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
     if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
   }
   DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
-            P.dag_maxdep, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
+            P.dag_maxdep, P.dag_cont_akk, P.dag_rec, P.dag_ks_tiles, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
             (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
             P.upd_part, P.upd_cnt, flag, t_begin, t_end,
             P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagCounterExtra - 1 : 0), progress, trace, gate};

@@ -431,6 +431,14 @@ void dag_build(LltPlan &plan) {
       if (plan.h_dag_phase[potrf_of[par]] != plan.h_dag_phase[t]) continue;   // never across the exchange
       plan.h_dag_cont[t] = potrf_of[par];
     }
+    plan.h_dag_cont_akk.assign(n, -1);
+    for (long t = 0; t < n; ++t) {
+      const int c = plan.h_dag_cont[t];
+      if (c < 0 || plan.h_dag_tasks[c].z < 0) continue;
+      const int4 it = plan.h_items[plan.h_dag_tasks[c].z];
+      if (it.z - it.y == 1 && plan.h_ks[it.y] == plan.h_dag_tasks[t].y)
+        plan.h_dag_cont_akk[t] = tid(plan.h_dag_tasks[c].y, plan.h_dag_tasks[c].y);
+    }
     // (generic successor claims -- every task claiming the successor it is the
     // last producer of -- and ready claims of near-critical successors were
     // measured slower in round 2 and removed: the claimed successors were
@@ -445,6 +453,34 @@ void dag_build(LltPlan &plan) {
       for (int u : prod[c])
         if (std::find(claimers[c].begin(), claimers[c].end(), u) == claimers[c].end()) md = std::max(md, u);
       plan.h_dag_maxdep[c] = md;
+    }
+    plan.h_dag_rec.assign((size_t)n * kDagRecInts, -1);
+    for (long t = 0; t < n; ++t) {
+      int *r = plan.h_dag_rec.data() + t * kDagRecInts;
+      const int4 tk = plan.h_dag_tasks[t];
+      r[kRecType] = tk.x, r[kRecY] = tk.y, r[kRecZ] = tk.z, r[kRecW] = tk.w;
+      r[kRecSub] = plan.h_dag_sub[t].x, r[kRecLate] = plan.h_dag_sub[t].y;
+      r[kRecWait0] = plan.h_dag_wait_off[t], r[kRecWait1] = plan.h_dag_wait_off[t + 1];
+      const int c = plan.h_dag_cont[t];
+      r[kRecCont] = c, r[kRecContAkk] = plan.h_dag_cont_akk[t], r[kRecMaxdep] = plan.h_dag_maxdep[t];
+      if (c >= 0)
+        r[kRecContMaxdep] = plan.h_dag_maxdep[c], r[kRecContWait0] = plan.h_dag_wait_off[c],
+        r[kRecContLate] = plan.h_dag_sub[c].y;
+      if (tk.x == 0 && tk.z >= 0) {
+        const int4 it = plan.h_items[tk.z];
+        r[kRecQ0] = it.y, r[kRecQ1] = it.z, r[kRecFoldK0] = plan.h_ks[it.y], r[kRecFoldTile0] = tid(tk.y, plan.h_ks[it.y]);
+      } else if (tk.x == 2) {
+        const int4 it = plan.h_items[tk.y];
+        const int2 tg = plan.h_targets[it.x];
+        r[kRecQ0] = it.y, r[kRecQ1] = it.z, r[kRecSid] = it.w, r[kRecTi] = tg.x, r[kRecTj] = tg.y;
+        if (it.w >= 0) r[kRecSplitN] = plan.h_split[it.w >> 8].x, r[kRecSplitP] = plan.h_split[it.w >> 8].y;
+      }
+    }
+    plan.h_dag_ks_tiles.assign(std::max<size_t>(plan.h_ks.size(), 1), make_int2(-1, -1));
+    for (const int4 &it : plan.h_items) {
+      const int2 tg = plan.h_targets[it.x];
+      for (int q = it.y; q < it.z; ++q)
+        plan.h_dag_ks_tiles[q] = make_int2(tid(tg.x, plan.h_ks[q]), tid(tg.y, plan.h_ks[q]));
     }
   }
   long n_potrf = 0, n_trsm = 0;
@@ -883,6 +919,9 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   addv(&plan.dag_sub, plan.h_dag_sub);
   addv(&plan.dag_cont, plan.h_dag_cont);
   addv(&plan.dag_maxdep, plan.h_dag_maxdep);
+  addv(&plan.dag_cont_akk, plan.h_dag_cont_akk);
+  addv(&plan.dag_rec, plan.h_dag_rec);
+  addv(&plan.dag_ks_tiles, plan.h_dag_ks_tiles);
   add(reinterpret_cast<void **>(&plan.dag_claimed), nullptr, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int));
   add(reinterpret_cast<void **>(&plan.dag_counters), nullptr, (2 * (size_t)plan.n_tiles + kDagCounterExtra) * sizeof(int));
   size_t total = 0, staged = 0;

@@ -103,6 +103,19 @@ __device__ inline double *reduced_elem(double *S, const DevProblem &P, long r, l
   return S + (long)P.tile_id[(r >> 6) * P.T + (c >> 6)] * 4096 + (r & 63) * 64 + (c & 63);
 }
 
+// Fields of a ticket's record (LltPlan::dag_rec, 32 ints).  -1 where absent.
+enum DagRecField {
+  kRecType = 0, kRecY, kRecZ, kRecW,           // the task (type, y, z, w)
+  kRecSub, kRecLate, kRecWait0, kRecWait1,     // fused TRSM tile, start of the late waits, the wait list
+  kRecCont, kRecContAkk, kRecMaxdep,           // continuation target, its A_kk tile, own maxdep
+  kRecContMaxdep, kRecContWait0, kRecContLate, // the target's maxdep and early-wait range
+  kRecQ0 = 16, kRecQ1,                         // POTRF fold / update item: columns [q0, q1) of ks
+  kRecFoldK0, kRecFoldTile0,                   // POTRF: ks[q0] and tid(k, ks[q0])
+  kRecSid = 18, kRecTi, kRecTj,                // update item: split slot, target tile (ti, tj)
+  kRecSplitN, kRecSplitP,                      // update item of a split target: pieces, first partial slot
+  kDagRecInts = 32
+};
+
 // Tile plan of the reduced-system Cholesky (dense_llt.hip), level-scheduled
 // over the tile elimination tree.  Device arrays, host per-level offsets.
 struct LltPlan {
@@ -163,8 +176,21 @@ struct LltPlan {
   // next (the parent column, whose fold is exactly the tile t solved) or -1;
   // dag_maxdep[t]: for such targets the largest ticket t waits on, else -1;
   // dag_claimed[t]: taken by the predecessor's workgroup or by the drawer
-  int *dag_cont = nullptr, *dag_maxdep = nullptr, *dag_claimed = nullptr;
-  std::vector<int> h_dag_cont, h_dag_maxdep;
+  // dag_cont_akk[t]: the storage index of the target's A_kk when the target
+  // folds task t's column alone (its A_kk is then all it loads, and task t's
+  // workgroup prefetches it beside the fused solve), else -1.
+  int *dag_cont = nullptr, *dag_maxdep = nullptr, *dag_claimed = nullptr, *dag_cont_akk = nullptr;
+  std::vector<int> h_dag_cont, h_dag_maxdep, h_dag_cont_akk;
+  // dag_rec[32 t ..]: every field the executor reads about ticket t, in one
+  // 128-byte record (kDagRec* offsets), fetched with two scalar loads -- the
+  // separate arrays were a chain of dependent loads (task -> item -> column
+  // -> tile id), each a memory round trip under the factorization's traffic.
+  // dag_ks_tiles[q]: the operand tile ids {tid(ti, ks[q]), tid(tj, ks[q])} of
+  // column q of an update item with target (ti, tj).
+  int *dag_rec = nullptr;
+  int2 *dag_ks_tiles = nullptr;
+  std::vector<int> h_dag_rec;
+  std::vector<int2> h_dag_ks_tiles;
   int *dag_wait_off = nullptr;
   // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags | phase-1 ticket])
   int2 *dag_waits = nullptr;

@@ -359,8 +359,8 @@ struct arslam_lm {
   void allreduce(double *buf, size_t count, int op) { allreduce_any(buf, count, ARSLAM_DT_F64, op); }
 
   int dag_workgroups = 512;
-  bool dag_traced = false;
-  int dag_trace_seen = 0;
+  static inline bool dag_traced = false;   // debug trace: one per process
+  static inline int dag_trace_seen = 0;
 
   void ensure_stream() {
     if (opt.device >= 0) HIP_CHECK(hipSetDevice(opt.device));

@@ -1,0 +1,5 @@
+mkdir -p gpurun_out
+timeout -k 10 120 python tools/lib_cmp.py cfg2 cfg3 medium > gpurun_out/cmp_new.txt 2>&1 || { tail gpurun_out/cmp_new.txt; exit 1; }
+ARSLAM_LIB=$PWD/ar_slam_amd/var_noapf.so timeout -k 10 120 python tools/lib_cmp.py cfg2 cfg3 medium > gpurun_out/cmp_old.txt 2>&1 || { tail gpurun_out/cmp_old.txt; exit 1; }
+cat gpurun_out/cmp_new.txt gpurun_out/cmp_old.txt
+bash tools/variant_bench.sh noapf
