@@ -442,29 +442,38 @@ SchurSide ceres_schur_side(const arslam_soa_problem *p) {
   auto cap_free = [&](int c) { return !(p->cap_const && p->cap_const[c]); };
   auto tag_free = [&](int t) { return !(p->tag_const && p->tag_const[t]); };
   const bool cam_free = !p->camera_const;
-  // distinct (capture, tag) pairs in both directions
-  std::vector<std::pair<int, int>> ct(nb);
-  for (int b = 0; b < nb; ++b) ct[b] = {p->obs_cap[b], p->obs_tag[b]};
+  // distinct (capture, tag) pairs of free blocks in both directions, in
+  // O(observations): bucketed by capture (a counting sort), duplicates dropped
+  // with a last-seen capture per tag (the adjacency lists are sets: their
+  // order does not change the independent set)
   std::vector<int> tag_nobs(nt, 0);
   for (int b = 0; b < nb; ++b) out.max_tag_obs = std::max(out.max_tag_obs, ++tag_nobs[p->obs_tag[b]]);
-  std::sort(ct.begin(), ct.end());
-  ct.erase(std::unique(ct.begin(), ct.end()), ct.end());
-  std::vector<int> cap_adj_start(nc + 1, 0), tag_adj_start(nt + 1, 0);
-  for (auto &e : ct) {
-    if (!cap_free(e.first) || !tag_free(e.second)) continue;
-    cap_adj_start[e.first + 1]++;
-    tag_adj_start[e.second + 1]++;
-  }
-  for (int c = 0; c < nc; ++c) cap_adj_start[c + 1] += cap_adj_start[c];
-  for (int t = 0; t < nt; ++t) tag_adj_start[t + 1] += tag_adj_start[t];
-  std::vector<int> cap_adj(cap_adj_start[nc]), tag_adj(tag_adj_start[nt]);
+  std::vector<int> by_cap_start(nc + 1, 0), by_cap(nb);
+  for (int b = 0; b < nb; ++b) by_cap_start[p->obs_cap[b] + 1]++;
+  for (int c = 0; c < nc; ++c) by_cap_start[c + 1] += by_cap_start[c];
   {
-    std::vector<int> fc(cap_adj_start.begin(), cap_adj_start.end() - 1), ft(tag_adj_start.begin(), tag_adj_start.end() - 1);
-    for (auto &e : ct) {
-      if (!cap_free(e.first) || !tag_free(e.second)) continue;
-      cap_adj[fc[e.first]++] = e.second;
-      tag_adj[ft[e.second]++] = e.first;
-    }
+    std::vector<int> fill(by_cap_start.begin(), by_cap_start.end() - 1);
+    for (int b = 0; b < nb; ++b) by_cap[fill[p->obs_cap[b]]++] = b;
+  }
+  std::vector<int> cap_adj_start(nc + 1, 0), cap_adj, tag_adj_start(nt + 1, 0), mark(nt, -1);
+  cap_adj.reserve(nb);
+  for (int c = 0; c < nc; ++c) {
+    if (cap_free(c))
+      for (int q = by_cap_start[c]; q < by_cap_start[c + 1]; ++q) {
+        const int t = p->obs_tag[by_cap[q]];
+        if (!tag_free(t) || mark[t] == c) continue;
+        mark[t] = c;
+        cap_adj.push_back(t);
+        tag_adj_start[t + 1]++;
+      }
+    cap_adj_start[c + 1] = (int)cap_adj.size();
+  }
+  for (int t = 0; t < nt; ++t) tag_adj_start[t + 1] += tag_adj_start[t];
+  std::vector<int> tag_adj(tag_adj_start[nt]);
+  {
+    std::vector<int> ft(tag_adj_start.begin(), tag_adj_start.end() - 1);
+    for (int c = 0; c < nc; ++c)
+      for (int q = cap_adj_start[c]; q < cap_adj_start[c + 1]; ++q) tag_adj[ft[cap_adj[q]]++] = c;
   }
   // vertex ids: 0 camera, 1 + c capture, 1 + nc + t tag; program order
   const int nv = 1 + nc + nt;
@@ -487,8 +496,15 @@ SchurSide ceres_schur_side(const arslam_soa_problem *p) {
     return tag_adj_start[t + 1] - tag_adj_start[t] + (cam_free ? 1 : 0);
   };
   std::vector<int> deg(nv, 0);
-  for (int v : order) deg[v] = degree(v);
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return deg[a] < deg[b]; });
+  int max_deg = 0;
+  for (int v : order) max_deg = std::max(max_deg, deg[v] = degree(v));
+  {   // stable sort by ascending degree: a counting sort
+    std::vector<int> cnt(max_deg + 2, 0), sorted(order.size());
+    for (int v : order) cnt[deg[v] + 1]++;
+    for (int d = 0; d <= max_deg; ++d) cnt[d + 1] += cnt[d];
+    for (int v : order) sorted[cnt[deg[v]]++] = v;
+    order.swap(sorted);
+  }
   enum : char { kWhite = 0, kGrey = 1, kBlack = 2 };
   std::vector<char> color(nv, kWhite);
   for (int v : order) {
