@@ -1277,6 +1277,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int4 fit = make_int4(0, r[kRecQ0], r[kRecQ1], 0);
+      const bool akk_in_d = cont && sh[16] && sh[17];   // (its predecessor's waves 2-3 put A_kk in D)
       // a one-column folded update runs inside the factorization (fold_f: its
       // L_kj tile in X -- the predecessor's solved tile for a continuation,
       // else loaded beside A_kk); several columns fold first, as one GEMM pass
@@ -1284,7 +1285,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       if (fold_in) {
         const double *Akk = a.S + (long)task.w * (T64 * T64);
         if (cont && r[kRecFoldK0] == pk) {
-          if (!(sh[16] && sh[17])) load_tile_wt(Akk, D, tid);   // (else its predecessor's waves 2-3 put it in D)
+          if (!akk_in_d) load_tile_wt(Akk, D, tid);
         } else load_two_tiles_wt(Akk, D, a.S + (long)r[kRecFoldTile0] * (T64 * T64), X, tid);
       } else if (task.z >= 0) {
         // folded final update: A_kk -= sum over the item's columns j of L_kj L_kj^T
@@ -1345,6 +1346,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       bool third_done = false;
       const bool ok = blocked_potrf64_async(D, inv, LTd, sh + 1, sh + 8, tid, colx, [&](int p, int wv, int ln) {
         auto fetch_third = [&]() {
+#ifdef ARSLAM_NO_IDLE_LOADS
+        return;   // (debug: the pipeline without the fused tile's idle-time fetch)
+#endif
         auto poll = [&]() {
           if (!pf_src || pw1 - pw0 > 64) return false;
           const int q = pw0 + ln;
@@ -1458,14 +1462,10 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         double *Ct = a.S + (long)sub.x * (T64 * T64);
         // The continuation claim's round trips ride along the solve instead of
         // following it: the ticket count and the in-flight reservation go out
-        // now; the claim itself (after the solve) answers during the tile's
-        // store; wave 0's other lanes poll the target's early waits, so a
-        // claimed target whose waits were already met skips its own poll.
-        // Every wave polls the target's early waits (lanes 1..63) and reads
-        // the answer after its first two solve steps: a claimed continuation
-        // whose waits all four waves saw met skips its own poll.  (Its A_kk
-        // prefetched into registers here was measured neutral: the release
-        // before the counter bump, s_waitcnt vmcnt(0), then waits for it.)
+        // now, the claim itself after the solve, answered during the tile's
+        // stores (its target's early waits were polled beside the last POTRF
+        // panel, sh[20..21]: a claimed target whose waits were seen met skips
+        // its own poll).
         int tk_seen = 0, infl_old = 0;
         if (c >= 0 && tid == 0) {
           tk_seen = ld_acquire_relaxed(ticket);
@@ -1486,14 +1486,12 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         trsm_step(X, D, LTd, w, 3, lane);
         __syncthreads();
         // claim the continuation target before the tile is published: its
-        // drawer waits for this tile, so it cannot have claimed it yet
-        int claim = -1;
-        if (c >= 0 && tid == 0) {
-          if (a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap && atomicCAS(a.claimed + c, 0, 1) == 0)
-            claim = c;
-          else
-            atomicSub(inflight, 1);
-        }
+        // drawer waits for this tile, so it cannot have claimed it yet.  (The
+        // CAS is complete at the release below -- s_waitcnt vmcnt(0) -- and its
+        // answer is read after it: no round trip of its own.)
+        const bool want = c >= 0 && tid == 0 && a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap;
+        int cas_old = 1;
+        if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
         if (!apf) {
           store_tile_wt(Ct, X, tid, false);
           if (tid == 0) sh[16] = sh[17] = 0;
@@ -1509,8 +1507,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
               const int t2 = tid - 128;
 #pragma unroll
               for (int u = 0; u < 16; ++u) {
-                const int e = u * 128 + t2, r = e >> 5, c2 = (e & 31) * 2;
-                *reinterpret_cast<dbl2 *>(D + r * LQ + c2) = apv[u];
+                const int e = u * 128 + t2, row = e >> 5, c2 = (e & 31) * 2;
+                *reinterpret_cast<dbl2 *>(D + row * LQ + c2) = apv[u];
               }
             }
             if (lane == 0) sh[16 + w - 2] = ap_ok ? 1 : 0;
@@ -1518,10 +1516,19 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           __syncthreads();
         }
         if (tid == 0) {
+          const int claim = want && cas_old == 0 ? c : -1;
+          if (c >= 0 && claim < 0) atomicSub(inflight, 1);
           sh[4] = claim;
           __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (a.trace && tid == 0) a.trace[8L * t + 7] = realtime();
+        if (a.trace && tid == 0) {
+          a.trace[8L * t + 7] = realtime();
+          // (debug flags above the workgroup: premet, A_kk prefetched into D, fused tile prefetched,
+          // the continuation's early waits seen met, claimed)
+          const unsigned long long fl = (premet ? 1 : 0) | (akk_in_d ? 2 : 0) | (pref ? 4 : 0) |
+                                        (sh[20] && sh[21] ? 8 : 0) | (sh[4] >= 0 ? 16 : 0);
+          a.trace[8L * t + 3] = blockIdx.x | (fl << 32);
+        }
         __syncthreads();
         next = sh[4];
         next_met = next >= 0 && sh[20] && sh[21];
@@ -1558,8 +1565,16 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       const int4 it = make_int4(0, r[kRecQ0], r[kRecQ1], r[kRecSid]);
       const int ti = r[kRecTi], tj = r[kRecTj], sid = it.w;
       dbl4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+      // The target's in-order wait (its earlier levels applied) is polled
+      // beside the first operand fetch; when it is met then, the target's own
+      // loads go out before the last GEMM and land during it (one round trip
+      // fewer after the GEMM).  (Unsplit items: a split piece stores a partial.)
+      double *C = a.S + (long)task.w * (T64 * T64);
+      double cv[16];
+      bool c_pre = false;
       for (int q = it.y; q < it.z; ++q) {
-        const int2 kt = a.ks_tiles[q];   // (operand tile ids: no column -> tile lookup chain)
+        // (operand tile ids: the first column's in the record, no column -> tile lookup chain)
+        const int2 kt = q == it.y ? make_int2(r[kRecTile0I], r[kRecTile0J]) : a.ks_tiles[q];
         if (q > it.y) __syncthreads();
         {   // hold the GEMM while a POTRF runs on this CU (bounded)
           if (tid == 0) {
@@ -1570,11 +1585,27 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           }
           __syncthreads();
         }
+        if (q == it.y && sid < 0 && tid == 0)
+          sh[3] = (task.z == 0 || ld_acquire_relaxed(applied + task.w) >= task.z) ? 1 : 0;
         if (ti != tj)   // both operands in one round trip
           load_two_tiles_wt(a.S + (long)kt.x * (T64 * T64), D, a.S + (long)kt.y * (T64 * T64), X, tid);
         else
           load_tile_wt(a.S + (long)kt.x * (T64 * T64), D, tid);
         __syncthreads();
+#ifndef ARSLAM_NO_UPF
+        const bool c_issue = q == it.z - 1 && sid < 0 && sh[3];
+#else
+        const bool c_issue = false;
+#endif
+        if (c_issue) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int rb = r0 + (u >> 1) * 16, cb = c0 + (u & 1) * 16;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) cv[4 * u + reg] = ld_wt(C + (rb + lk + 4 * reg) * T64 + cb + li);
+          }
+          c_pre = true;
+        }
         gemm64_nt(D, ti != tj ? X : D, tid, acc);   // a diagonal target: one operand tile, fetched once
       }
       bool apply = true;
@@ -1612,7 +1643,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         }
       }
       DAG_PROGRESS(1, 3);
-      if (apply) {
+      if (apply && !c_pre) {
         // in level order: wait until the target's earlier levels were applied
         if (tid == 0) {
           long spins = 0;
@@ -1627,19 +1658,14 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           if (!ok) atomicCAS(a.flag, 0, -(2000000 + t));
         }
         __syncthreads();
-        double *C = a.S + (long)task.w * (T64 * T64);
-        double cv[16];   // two groups of eight loads in flight
-        {
-          const double *p8[16];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
+        for (int q = 0; q < 4; ++q) {   // (sixteen loads in flight)
+          const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) p8[4 * q + reg] = C + (rb + lk + 4 * reg) * T64 + cb + li;
-          }
-          ld_wt8x8(p8, cv);
-          ld_wt8x8(p8 + 8, cv + 8);
+          for (int reg = 0; reg < 4; ++reg) cv[4 * q + reg] = ld_wt(C + (rb + lk + 4 * reg) * T64 + cb + li);
         }
+      }
+      if (apply) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int rb = r0 + (q >> 1) * 16, cb = c0 + (q & 1) * 16;

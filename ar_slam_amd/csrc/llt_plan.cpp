@@ -474,6 +474,7 @@ void dag_build(LltPlan &plan) {
         const int2 tg = plan.h_targets[it.x];
         r[kRecQ0] = it.y, r[kRecQ1] = it.z, r[kRecSid] = it.w, r[kRecTi] = tg.x, r[kRecTj] = tg.y;
         if (it.w >= 0) r[kRecSplitN] = plan.h_split[it.w >> 8].x, r[kRecSplitP] = plan.h_split[it.w >> 8].y;
+        r[kRecTile0I] = tid(tg.x, plan.h_ks[it.y]), r[kRecTile0J] = tid(tg.y, plan.h_ks[it.y]);
       }
     }
     plan.h_dag_ks_tiles.assign(std::max<size_t>(plan.h_ks.size(), 1), make_int2(-1, -1));

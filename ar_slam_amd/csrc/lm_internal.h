@@ -113,6 +113,7 @@ enum DagRecField {
   kRecFoldK0, kRecFoldTile0,                   // POTRF: ks[q0] and tid(k, ks[q0])
   kRecSid = 18, kRecTi, kRecTj,                // update item: split slot, target tile (ti, tj)
   kRecSplitN, kRecSplitP,                      // update item of a split target: pieces, first partial slot
+  kRecTile0I, kRecTile0J,                      // update item: its first column's operand tile ids
   kDagRecInts = 32
 };
 

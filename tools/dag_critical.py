@@ -22,6 +22,7 @@ f = open(sys.argv[1], "rb")
 n = int(np.frombuffer(f.read(8), np.int64)[0])
 tasks = np.frombuffer(f.read(16 * n), np.int32).reshape(n, 4)
 tr = np.frombuffer(f.read(64 * n), np.uint64).reshape(n, 8).astype(np.int64)
+tr[:, 3] &= 0xffffffff   # (debug flags above the workgroup)
 nw = int(np.frombuffer(f.read(8), np.int64)[0])
 woff = np.frombuffer(f.read(4 * (n + 1)), np.int32)
 waits = np.frombuffer(f.read(8 * nw), np.int32).reshape(nw, 2)

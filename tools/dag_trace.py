@@ -5,6 +5,7 @@ f = open(sys.argv[1], "rb")
 n = int(np.frombuffer(f.read(8), np.int64)[0])
 tasks = np.frombuffer(f.read(16 * n), np.int32).reshape(n, 4)
 tr = np.frombuffer(f.read(64 * n), np.uint64).reshape(n, 8).astype(np.int64)
+tr[:, 3] &= 0xffffffff   # (debug flags above the workgroup)
 t0 = tr[:, 0].min()
 draw, ready, end = (tr[:, 0] - t0) / 100.0, (tr[:, 1] - t0) / 100.0, (tr[:, 2] - t0) / 100.0   # 100 MHz -> us
 print(f"tasks {n}, makespan {end.max():.1f} us, workgroups {len(np.unique(tr[:, 3]))}")
