@@ -1333,6 +1333,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // otherwise it is waited for and loaded after L_kk is published.
       const double *pf_src = sub.x >= 0 ? a.S + (long)sub.x * (T64 * T64) : nullptr;
       const int pw0 = sub.y, pw1 = r[kRecWait1];
+      // lane q's late wait of the fused tile (loaded now, polled beside the panels)
+      const int2 pw_wait = (sub.x >= 0 && pw0 + lane < pw1) ? a.waits[pw0 + lane] : make_int2(0, 0);
       // A tile whose waits were not met at panel 0 is polled again by wave 1
       // beside panels 1 and 2 (the request in sh[6]) and fetched by waves 1-3,
       // a third each, beside the next panel: on the late elimination-tree chain
@@ -1352,60 +1354,53 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         auto poll = [&]() {
           if (!pf_src || pw1 - pw0 > 64) return false;
           const int q = pw0 + ln;
-          const int2 cv = q < pw1 ? a.waits[q] : make_int2(0, 0);
-          const int got = q < pw1 ? ld_acquire_relaxed(a.counters + cv.x) : 0;
-          return __builtin_amdgcn_ballot_w64(q < pw1 && got < cv.y) == 0;
+          const int got = q < pw1 ? ld_acquire_relaxed(a.counters + pw_wait.x) : 0;
+          return __builtin_amdgcn_ballot_w64(q < pw1 && got < pw_wait.y) == 0;
         };
         int lnl = ln;   // laundered: the prefetch addresses are formed here, not hoisted and spilled
         asm volatile("" : "+v"(lnl));
-        if (p == 0) {
-          if (wv != 1) return;
-          const bool met = poll();
-          if (fold_in) {   // X still holds the fold's operand: fetch beside panel 1 instead
-            if (ln == 0 && met) *as_lds(sh + 6) = -1;
-            return;
-          }
-          if (met) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const double *p8[8];
-              dbl2 v[8];
-#pragma unroll
-              for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * ((g * 8 + u) * 64 + lnl);
-              ld_wt16x8(p8, v);
-#pragma unroll
-              for (int u = 0; u < 8; ++u) {
-                const int e = (g * 8 + u) * 64 + ln, r = e >> 5, c2 = (e & 31) * 2;
-                *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
-              }
-            }
-            lds_set(sh + 11, 3);
-          }
+        if (p == 0) {   // (X may still hold the fold's operand: the thirds go out beside panel 1)
+          if (wv == 1 && poll() && ln == 0) *as_lds(sh + 6) = -1;
           return;
         }
         if (third_done || lds_get(sh + 11) >= 3) return;
         const int req = lds_get(sh + 6);
-        if (req == 0) {   // not requested yet: poll beside panels 1 and 2
-          if (wv == 1 && p < 3 && poll() && ln == 0) *as_lds(sh + 6) = p;
-        } else if (req < p) {   // requested beside an earlier panel: the three thirds
+        // not requested yet: wave 1 polls beside panels 1 and 2; beside the
+        // last panel every wave polls for itself and takes its own third
+        bool take = req != 0 && req < p;
+        if (req == 0) {
+          if (p < 3) {
+            if (wv == 1 && poll() && ln == 0) *as_lds(sh + 6) = p;
+          } else {
+            take = poll();
+          }
+        }
+        if (take) {   // the three thirds, one batch of sc1 loads each
           // 2048 16-byte elements of the 64x64 tile: wave w takes e in [(w-1)*683, min(w*683, 2048))
           const int e0 = (wv - 1) * 683, e1 = min(wv * 683, 2048);
-          for (int base = e0; base < e1; base += 8 * 64) {
-            const double *p8[8];
-            dbl2 v[8];
+          const double *p11[11];
+          dbl2 v[11];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) p8[u] = pf_src + 2 * min(base + u * 64 + lnl, e1 - 1);
-            ld_wt16x8(p8, v);
+          for (int u = 0; u < 11; ++u) p11[u] = pf_src + 2 * min(e0 + u * 64 + lnl, e1 - 1);
+          ld_wt16x11(p11, v);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int e = base + u * 64 + ln, r = e >> 5, c2 = (e & 31) * 2;
-              if (e < e1) *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
-            }
+          for (int u = 0; u < 11; ++u) {
+            const int e = e0 + u * 64 + ln, r = e >> 5, c2 = (e & 31) * 2;
+            if (e < e1) *reinterpret_cast<dbl2 *>(X + r * LQ + c2) = v[u];
           }
           third_done = true;
           lds_add(sh + 11, ln);
         }
         };
+        // (beside the last panel the continuation's counters are read first,
+        // so their round trip overlaps the fused tile's)
+        int c_got = 0;
+        bool c_mine = false;
+        if (p == 3 && c >= 0 && wv >= 2 && r[kRecContLate] - r[kRecContWait0] <= 64) {
+          const int q = r[kRecContWait0] + ln;
+          c_mine = q < r[kRecContLate] && c_wait.x != sub.x;   // (the tile this task solves counts as met)
+          if (c_mine) c_got = ld_acquire_relaxed(a.counters + c_wait.x);
+        }
         fetch_third();
         // waves 2-3 and the continuation target: its record into LDS (wave 3,
         // issued beside panel 1, stored beside panel 2), its early-wait list
@@ -1421,14 +1416,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
             if (q < cw1) c_wait = a.waits[q];
           }
           if (p == 3) {
-            bool met = false;
-            if (cw1 - cw0 <= 64) {
-              const int q = cw0 + ln;
-              // (the tile this task solves counts as met)
-              const bool mine = q < cw1 && c_wait.x != sub.x;
-              const int got = mine ? ld_acquire_relaxed(a.counters + c_wait.x) : 0;
-              met = __builtin_amdgcn_ballot_w64(mine && got < c_wait.y) == 0;
-            }
+            const bool met = cw1 - cw0 <= 64 && __builtin_amdgcn_ballot_w64(c_mine && c_got < c_wait.y) == 0;
             if (ln == 0) sh[20 + wv - 2] = met ? 1 : 0;
             ap_met = met && apf;
           }
@@ -1443,6 +1431,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         atomicCAS(a.flag, 0, 1 + k * T64 + first);
       }
       double *ltd_g = a.ltd + (long)k * kLtdSize;
+      // (Measured slower: L_kk stored by one wave and released beside the
+      // solve or by the continuation -- the other TRSMs of the column, on the
+      // path to the continuation's fused tile, then start later.)
       store_tile_wt(a.Ld + (long)k * T64 * T64, D, tid, true);
       for (int e = tid; e < kLtdSize / 2; e += 256)
         st_wt16(ltd_g + 2 * e, *reinterpret_cast<const dbl2 *>(LTd + 2 * e));
@@ -1482,45 +1473,46 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // blocked_trsm64, its steps inline (row block w per wave)
         trsm_step(X, D, LTd, w, 0, lane);
         trsm_step(X, D, LTd, w, 1, lane);
+        // claim the continuation target before the tile is published: its
+        // drawer waits for this tile, so it cannot have claimed it yet.  (The
+        // CAS goes out here and is answered beside the last two steps.)
+        const bool want = c >= 0 && tid == 0 && a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap;
+        int cas_old = 1;
+#ifndef ARSLAM_CAS_LATE
+        if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
+#endif
         trsm_step(X, D, LTd, w, 2, lane);
         trsm_step(X, D, LTd, w, 3, lane);
         __syncthreads();
-        // claim the continuation target before the tile is published: its
-        // drawer waits for this tile, so it cannot have claimed it yet.  (The
-        // CAS is complete at the release below -- s_waitcnt vmcnt(0) -- and its
-        // answer is read after it: no round trip of its own.)
-        const bool want = c >= 0 && tid == 0 && a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap;
-        int cas_old = 1;
+#ifdef ARSLAM_CAS_LATE
         if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
-        if (!apf) {
-          store_tile_wt(Ct, X, tid, false);
-          if (tid == 0) sh[16] = sh[17] = 0;
-          dag_release(tid);
-        } else {
-          if (w < 2) {
-            store_tile_wt<128>(Ct, X, tid, false);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          } else {
-            // the continuation's A_kk into D (free: L_kk's last reader was the solve)
-            if (ap_ok) {
-              ld_wt16x16_wait(apv);
-              const int t2 = tid - 128;
+#endif
+        // wave 1 stores the solved tile, waves 2-3 move the continuation's
+        // A_kk into D (free: L_kk's last reader was the solve)
+        if (w == 1) {
+          store_tile_wt<64>(Ct, X, tid - 64, false);
+        } else if (w >= 2) {
+          if (ap_ok) {
+            ld_wt16x16_wait(apv);
+            const int t2 = tid - 128;
 #pragma unroll
-              for (int u = 0; u < 16; ++u) {
-                const int e = u * 128 + t2, row = e >> 5, c2 = (e & 31) * 2;
-                *reinterpret_cast<dbl2 *>(D + row * LQ + c2) = apv[u];
-              }
+            for (int u = 0; u < 16; ++u) {
+              const int e = u * 128 + t2, row = e >> 5, c2 = (e & 31) * 2;
+              *reinterpret_cast<dbl2 *>(D + row * LQ + c2) = apv[u];
             }
-            if (lane == 0) sh[16 + w - 2] = ap_ok ? 1 : 0;
           }
-          __syncthreads();
+          if (lane == 0) sh[16 + w - 2] = ap_ok ? 1 : 0;
         }
         if (tid == 0) {
           const int claim = want && cas_old == 0 ? c : -1;
           if (c >= 0 && claim < 0) atomicSub(inflight, 1);
           sh[4] = claim;
-          __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        // (wave 1 alone waits for the stores' acknowledgements; releasing
+        // the tile from the continuation instead was measured slower)
+        if (w == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.trace && tid == 0) {
           a.trace[8L * t + 7] = realtime();
           // (debug flags above the workgroup: premet, A_kk prefetched into D, fused tile prefetched,
