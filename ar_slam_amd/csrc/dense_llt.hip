@@ -1087,27 +1087,19 @@ __device__ __forceinline__ void gemm64_nt(const double *sA, const double *sB, in
 
 struct DagArgs {
   double *S;
-  const int *tid_map;
   int T;
   double *Ld;                 // [2T][4096]: L_kk then L_kk^{-1}
   double *ltd;                // [T][kLtdSize]: the 16x16 diagonal-block inverses of each L_kk
-  const int4 *tasks;
-  const int2 *sub;            // [n_tasks] TRSM fused into a POTRF task: {tile id or -1, late-wait start}
-  const int *cont;            // [n_tasks] POTRF task the same workgroup may continue with (or -1)
-  const int *maxdep;          // [n_tasks] continuation targets: largest ticket they wait on; else -1
-  const int *cont_akk;        // [n_tasks] the continuation's A_kk tile if it folds this column alone, else -1
+  // (the task, its fused TRSM, continuation, fold and update-item fields are
+  // all in the ticket's record; LltPlan::dag_rec)
   const int *rec;             // [n_tasks][32] each ticket's record (DagRecField)
   const int2 *ks_tiles;       // [ks] operand tile ids of an update column
+  const int *ks;              // [ks] the column of each (a multi-column fold's own term test)
   int *claimed;               // [n_tasks] continuation targets: claimed by the predecessor or the drawer
-  const int *wait_off;
-  const int2 *waits;
+  const int2 *waits;          // wait lists {counter, value} (ranges in the records)
   int *counters;              // ready[n_tiles] | applied[n_tiles] | ticket
   int n_tiles;
   int n_tasks;
-  const int2 *targets;
-  const int4 *items;
-  const int *ks;
-  const int2 *split;
   double *part;
   int *split_cnt;
   int *flag;
@@ -1257,11 +1249,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // (s_waitcnt vmcnt(0)) never waits for those loads; waves 2-3 move the
       // registers into D after the fused solve, as the target's A_kk.
       const int c = sub.x >= 0 ? r[kRecCont] : -1;
-#ifndef ARSLAM_NO_APF
       const int apf_tile = sub.x >= 0 ? r[kRecContAkk] : -1;
-#else
-      const int apf_tile = -1;
-#endif
       const bool apf = apf_tile >= 0;
       const double *apf_src = a.S + (long)max(apf_tile, 0) * (T64 * T64);
       bool ap_met = false;   // waves 2-3: the target's early waits seen met beside the last panel
@@ -1348,9 +1336,6 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       bool third_done = false;
       const bool ok = blocked_potrf64_async(D, inv, LTd, sh + 1, sh + 8, tid, colx, [&](int p, int wv, int ln) {
         auto fetch_third = [&]() {
-#ifdef ARSLAM_NO_IDLE_LOADS
-        return;   // (debug: the pipeline without the fused tile's idle-time fetch)
-#endif
         auto poll = [&]() {
           if (!pf_src || pw1 - pw0 > 64) return false;
           const int q = pw0 + ln;
@@ -1478,15 +1463,10 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // CAS goes out here and is answered beside the last two steps.)
         const bool want = c >= 0 && tid == 0 && a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap;
         int cas_old = 1;
-#ifndef ARSLAM_CAS_LATE
         if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
-#endif
         trsm_step(X, D, LTd, w, 2, lane);
         trsm_step(X, D, LTd, w, 3, lane);
         __syncthreads();
-#ifdef ARSLAM_CAS_LATE
-        if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
-#endif
         // wave 1 stores the solved tile, waves 2-3 move the continuation's
         // A_kk into D (free: L_kk's last reader was the solve)
         if (w == 1) {
@@ -1584,11 +1564,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         else
           load_tile_wt(a.S + (long)kt.x * (T64 * T64), D, tid);
         __syncthreads();
-#ifndef ARSLAM_NO_UPF
         const bool c_issue = q == it.z - 1 && sid < 0 && sh[3];
-#else
-        const bool c_issue = false;
-#endif
         if (c_issue) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -1953,10 +1929,8 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
     (void)hipMemsetAsync(P.dag_claimed, 0, (size_t)P.n_dag_tasks * sizeof(int), s);
     if (P.n_split) (void)hipMemsetAsync(P.upd_cnt, 0, P.n_split * sizeof(int), s);
   }
-  DagArgs a{S, P.tile_id, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_tasks, P.dag_sub, P.dag_cont,
-            P.dag_maxdep, P.dag_cont_akk, P.dag_rec, P.dag_ks_tiles, P.dag_claimed, P.dag_wait_off, P.dag_waits, P.dag_counters,
-            (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_targets, P.upd_items, P.upd_ks, P.upd_split,
-            P.upd_part, P.upd_cnt, flag, t_begin, t_end,
+  DagArgs a{S, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_rec, P.dag_ks_tiles, P.upd_ks, P.dag_claimed,
+            P.dag_waits, P.dag_counters, (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_part, P.upd_cnt, flag, t_begin, t_end,
             P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagCounterExtra - 1 : 0), progress, trace, gate};
   const int grid = (int)std::min<long>(n_workgroups, t_end - t_begin);
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);

@@ -914,13 +914,7 @@ void llt_plan_upload(LltPlan &plan, hipStream_t s) {
   addv(&plan.tile_class, cls);
   // L_kk, L_kk^{-1}, and the 16x16 block inverses (4 x 16 x 18) of each column
   add(reinterpret_cast<void **>(&plan.ldiag), nullptr, ((size_t)2 * T * 64 * 64 + (size_t)T * 1152) * sizeof(double));
-  addv(&plan.dag_tasks, plan.h_dag_tasks);
-  addv(&plan.dag_wait_off, plan.h_dag_wait_off);
   addv(&plan.dag_waits, plan.h_dag_waits);
-  addv(&plan.dag_sub, plan.h_dag_sub);
-  addv(&plan.dag_cont, plan.h_dag_cont);
-  addv(&plan.dag_maxdep, plan.h_dag_maxdep);
-  addv(&plan.dag_cont_akk, plan.h_dag_cont_akk);
   addv(&plan.dag_rec, plan.h_dag_rec);
   addv(&plan.dag_ks_tiles, plan.h_dag_ks_tiles);
   add(reinterpret_cast<void **>(&plan.dag_claimed), nullptr, std::max<long>(plan.n_dag_tasks, 1) * sizeof(int));

@@ -164,23 +164,21 @@ struct LltPlan {
   std::vector<int> h_bs_off;        // [nlev+1], in backward (root-first) order
   std::vector<int> h_bsg_off;       // [nlev+1], gather tasks per backward level
   std::vector<double> h_upd_flops;  // useful flops of each level's update
-  // persistent task-graph executor (launch_dense_llt_dag): tasks in ticket
-  // order {type, a, b, c} (0 POTRF k; 1 TRSM i,k; 2 update item a, level
-  // sequence b, target tile c), each with a list of {counter, value} waits;
-  // counters = [ready(n_tiles) | applied(n_tiles) | ticket].  dag_sub[t] =
-  // {tile id of the TRSM fused into POTRF task t or -1, index in dag_waits
-  // where that TRSM's late waits begin}.
-  int4 *dag_tasks = nullptr;
-  int2 *dag_sub = nullptr;
-  std::vector<int2> h_dag_sub;
-  // dag_cont[t]: the POTRF task the workgroup finishing POTRF task t may run
+  // persistent task-graph executor (launch_dense_llt_dag), host side: tasks
+  // in ticket order {type, a, b, c} (0 POTRF k; 1 TRSM i,k; 2 update item a,
+  // level sequence b, target tile c), each with a list of {counter, value}
+  // waits (h_dag_wait_off); counters = [ready(n_tiles) | applied(n_tiles) |
+  // ticket].  h_dag_sub[t] = {tile id of the TRSM fused into POTRF task t or
+  // -1, index in the waits where that TRSM's late waits begin}.
+  // h_dag_cont[t]: the POTRF task the workgroup finishing POTRF task t may run
   // next (the parent column, whose fold is exactly the tile t solved) or -1;
-  // dag_maxdep[t]: for such targets the largest ticket t waits on, else -1;
-  // dag_claimed[t]: taken by the predecessor's workgroup or by the drawer
-  // dag_cont_akk[t]: the storage index of the target's A_kk when the target
+  // h_dag_maxdep[t]: for such targets the largest ticket t waits on, else -1;
+  // h_dag_cont_akk[t]: the storage index of the target's A_kk when the target
   // folds task t's column alone (its A_kk is then all it loads, and task t's
   // workgroup prefetches it beside the fused solve), else -1.
-  int *dag_cont = nullptr, *dag_maxdep = nullptr, *dag_claimed = nullptr, *dag_cont_akk = nullptr;
+  // dag_claimed[t] (device): taken by the predecessor's workgroup or by the drawer.
+  std::vector<int2> h_dag_sub;
+  int *dag_claimed = nullptr;
   std::vector<int> h_dag_cont, h_dag_maxdep, h_dag_cont_akk;
   // dag_rec[32 t ..]: every field the executor reads about ticket t, in one
   // 128-byte record (kDagRec* offsets), fetched with two scalar loads -- the
@@ -192,7 +190,6 @@ struct LltPlan {
   int2 *dag_ks_tiles = nullptr;
   std::vector<int> h_dag_rec;
   std::vector<int2> h_dag_ks_tiles;
-  int *dag_wait_off = nullptr;
   // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags | phase-1 ticket])
   int2 *dag_waits = nullptr;
   int *dag_counters = nullptr;
