@@ -248,8 +248,10 @@ void llt_plan_reset(LltPlan &plan);                // host side only; the arena 
 // ---- lm_kernels.hip ----
 void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
                       double *obs_tg, double *parts, hipStream_t s);
-void launch_tag_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
-                       hipStream_t s);
+// k_linearize's reductions in one launch: the per-capture partials into
+// out[0..NPART+1] (launch_reduce_parts without fparts) and the tag slots' g and colnorm
+void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
+                       const double *parts, double *out, hipStream_t s);
 void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale,
                   hipStream_t s);
 void launch_lm_diag(const DevProblem &P, const double *scale, const double *colnorm, double dmin,
@@ -280,12 +282,13 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts,
                          double *out, hipStream_t s, const int *flag = nullptr, const int *gate = nullptr);
 void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, hipStream_t s);
-void launch_camera_slots(const DevProblem &P, const double *red, double *g, double *colnorm,
-                         hipStream_t s);
-// norms over free parameter slots: out[0..2] = max|g|, sum g^2, sum x^2 over capture slots,
-// out[3..5] the same over camera + tag slots
-void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out,
-                       hipStream_t s);
+// The camera slots of g and colnorm from the reduced partials red (P_GF, P_CF),
+// then the norms over free parameter slots: out[0..2] = max|g|, sum g^2, sum x^2
+// over capture slots, out[3..5] the same over camera + tag slots.  out[7] is
+// the launch's block count (must be zero before the first launch), out[8..]
+// its per-block partials.
+void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
+                       double *out, hipStream_t s);
 
 // Optional per-launch event pairs around the dominant kernel (trailing update).
 struct LaunchTiming {

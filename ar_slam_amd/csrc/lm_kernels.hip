@@ -107,24 +107,41 @@ __device__ void fill_rows(const DevProblem &P, const double *x, const double *sc
 }
 
 // LDS rows of capture c from the copy fill_rows stored at the same point,
-// Jacobi-scaled.
-__device__ void load_rows(const DevProblem &P, const double *scale, int c, int o0, int nrows,
-                          double *rows) {
+// Jacobi-scaled, and each row's reduced-side product
+//   qv[row] = F_row . y_F = J_f y_f + J_t . y_F[tag rows]
+// formed from the row the lane just scaled (its tag row and y_F loads go out
+// beside the Jacobian loads instead of after a barrier).
+__device__ void load_rows_q(const DevProblem &P, const double *scale, const double *yF, double yf, int c, int o0,
+                            int nrows, double *rows, double *qv) {
   const double *sc = scale + slot_cap(P, c);
   for (int row = threadIdx.x; row < nrows; row += kWave) {
     const double *g = P.jrows + 8L * o0 * kRowStride + row;
+    const int t = P.obs_tag[o0 + (row >> 3)];
+    const int tr = P.tag_row[t];
     double v[14];
 #pragma unroll
     for (int j = 0; j < 14; ++j) v[j] = g[(long)j * nrows];
-    const double *st = scale + slot_tag(P, P.obs_tag[o0 + (row >> 3)]);
+    const double *st = scale + slot_tag(P, t);
+    double yt[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) yt[j] = tr >= 0 ? yF[tr + j] : 0.0;
     double *dst = rows + (long)row * kRowStride;
-    dst[0] = v[0] * scale[0];
+    double d[14];
+    d[0] = v[0] * scale[0];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      dst[1 + j] = v[1 + j] * sc[j];
-      dst[7 + j] = v[7 + j] * st[j];
+      d[1 + j] = v[1 + j] * sc[j];
+      d[7 + j] = v[7 + j] * st[j];
     }
-    dst[13] = v[13];
+    d[13] = v[13];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) dst[j] = d[j];
+    double q = d[0] * yf;
+    if (tr >= 0) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) q += d[7 + j] * yt[j];
+    }
+    qv[row] = q;
   }
 }
 
@@ -183,6 +200,14 @@ __device__ void inv6(const double *U, double *Ui) {
 // Kernels
 // ---------------------------------------------------------------------------
 
+// rr[ca] * rr[cb], rounded before it is added (no FMA contraction: the
+// per-capture sums of k_linearize have always rounded product and sum
+// separately, the per-observation ones use FMAs; kept as they were)
+__device__ __forceinline__ double row_prod(const double *rr, int ca, int cb) {
+#pragma clang fp contract(off)
+  return rr[ca] * rr[cb];
+}
+
 // (4 waves per SIMD instead of the 3 its 143 VGPRs allow: a 28-byte spill,
 // 84 -> 71 us on cfg3; 5 waves spills 148 bytes and is slower)
 // Linearize at x: per-observation tag gradient/column norms, per-capture
@@ -201,38 +226,27 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
   double *ocost = rows + (long)nrows * kRowStride;   // [k]
   fill_rows(P, x, nullptr, c, o0, nrows, rows, P.jrows);
   __syncthreads();
-  // per observation: cost, tag gradient (6), tag column norms (6)
+  // Every sum below is over rows of one product of two LDS columns (ca, cb),
+  // picked per lane up front: one code path for the whole wave (a divergent
+  // if-chain ran each case's LDS round trips one after another)
+  // per observation: cost (r'r), tag gradient (6: F_t'r), tag column norms (6)
   for (int e = lane; e < 13 * k; e += kWave) {
     const int q = e / 13, it = e % 13;
     const double *rq = rows + (long)q * 8 * kRowStride;
+    const int ca = it == 0 ? 13 : it <= 6 ? 6 + it : it, cb = it <= 6 ? 13 : it;
     double s = 0.0;
-    if (it == 0) {
 #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + 13] * rq[rr * kRowStride + 13];
-      ocost[q] = 0.5 * s;
-    } else if (it <= 6) {
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + 6 + it] * rq[rr * kRowStride + 13];
-      obs_tg[12L * (o0 + q) + (it - 1)] = s;
-    } else {
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        const double v = rq[rr * kRowStride + it];
-        s += v * v;
-      }
-      obs_tg[12L * (o0 + q) + (it - 1)] = s;
-    }
+    for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + ca] * rq[rr * kRowStride + cb];
+    if (it == 0) ocost[q] = 0.5 * s;
+    else obs_tg[12L * (o0 + q) + (it - 1)] = s;
   }
-  // per capture: capture gradient (6), capture column norms (6), f gradient, f column norm
+  // per capture: capture gradient (6: E'r), capture column norms (6), f gradient, f column norm
   if (lane < 14) {
+    const int ca = lane < 6 ? 1 + lane : lane < 12 ? lane - 5 : 0;
+    const int cb = lane < 6 ? 13 : lane < 12 ? lane - 5 : lane == 12 ? 13 : 0;
     double s = 0.0;
-    for (int r = 0; r < nrows; ++r) {
-      const double *rr = rows + (long)r * kRowStride;
-      if (lane < 6) s += rr[1 + lane] * rr[13];
-      else if (lane < 12) s += rr[1 + lane - 6] * rr[1 + lane - 6];
-      else if (lane == 12) s += rr[0] * rr[13];
-      else s += rr[0] * rr[0];
-    }
+#pragma unroll 8
+    for (int r = 0; r < nrows; ++r) s += row_prod(rows + (long)r * kRowStride, ca, cb);
     if (lane < 12) {
       const long slot = slot_cap(P, c) + (lane % 6);
       const double v = P.slot_free[slot] ? s : 0.0;
@@ -258,10 +272,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
   }
 }
 
-__global__ void k_tag_reduce(DevProblem P, const double *__restrict__ obs_tg,
-                             double *__restrict__ g, double *__restrict__ colnorm) {
-  if (gated(P.gate_lin)) return;
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// Per tag slot: the gradient / column-norm sums over the tag's observations
+// (obs_tg from k_linearize), in observation order.  Element e = 12 t + j.
+__device__ __forceinline__ void tag_reduce_elem(const DevProblem &P, const double *__restrict__ obs_tg, long e,
+                                                double *__restrict__ g, double *__restrict__ colnorm) {
   if (e >= 12L * P.nt) return;
   const int t = (int)(e / 12), j = (int)(e % 12);
   double s = 0.0;
@@ -338,6 +352,18 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   int *lblk = (int *)(FF + 28 * nblk);           // k
   double *ff00 = reinterpret_cast<double *>(lblk + k + (k & 1));   // F_0'F_0
 
+  // the first eight observations' Jacobian rows (the Gram loop's operands
+  // below) are loaded before the prologue's dependent loads (obs_tag -> the
+  // tag scales), so the two latencies overlap
+  const int li = lane & 15, lk = lane >> 4;
+  const bool valid = li < 14;
+  const double *jb = P.jrows + 8L * o0 * kRowStride;
+  double jv[16];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+      jv[2 * u + st] = (valid && u < k) ? jb[(long)li * nrows + 8 * u + 4 * st + lk] : 0.0;
   for (int q = lane; q < k; q += kWave) lblk[q] = P.obs_lblk[o0 + q];
   for (int e = lane; e < 6 * k; e += kWave) tscale[e] = scale[slot_tag(P, P.obs_tag[o0 + e / 6]) + e % 6];
   __syncthreads();
@@ -351,7 +377,6 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   // products (W_u = E'F_u, F_u'r, F_u'F_u, f'F_u) are added into LDS per
   // observation (a tag seen twice in one capture sums into one block).
   {
-    const int li = lane & 15, lk = lane >> 4;
     for (int e = lane; e < 6 * m + m + (m & 1) + 28 * nblk; e += kWave) W[e] = 0.0;   // W, Ftr, FF: contiguous
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -362,13 +387,36 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
     // capture's column-major Jacobian block (load_rows' layout), eight
     // observations' loads in flight at once, and scales it as load_rows does
     // (the same products: the Grams are bit-identical)
-    const double *jb = P.jrows + 8L * o0 * kRowStride;
     const double *sc = scale + slot_cap(P, c);
     const double cs = li == 0 ? scale[0] : li <= 6 ? sc[li - 1] : 1.0;   // (tag columns: tscale)
-    const bool tagcol = li >= 7 && li <= 12, valid = li < 14;
-    double jv[16];
+    const bool tagcol = li >= 7 && li <= 12;
+    // Where this lane's Gram entries G[lk + 4 reg][li] go, as an LDS index
+    // (W, Ftr and FF are contiguous) plus a stride per tag block u: one LDS
+    // add per register and observation instead of a divergent if-chain
+    //   E'F_u  : W[(r-1) m + 1 + 6u + (c-7)]          r 1..6,  c 7..12
+    //   F_u'r  : Ftr[1 + 6u + (r-7)]                    r 7..12, c 13
+    //   F_u'F_u: FF[28u + a*6 - a(a-1)/2 + (b-a)]       r 7..12, r <= c <= 12
+    //   f'F_u  : FF[28u + 21 + (c-7)]                   r 0,     c 7..12
+    int acc_off[4], acc_stride[4];
+    const int w_base = (int)(W - sm);
+    {
+      const int c = li, ftr0 = 6 * m, ff0 = ftr0 + m + (m & 1);
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int r = lk + 4 * reg;
+        int off = -1, st = 0;
+        if (r >= 1 && r <= 6 && c >= 7 && c <= 12) { off = (r - 1) * m + 1 + (c - 7); st = 6; }
+        else if (r >= 7 && r <= 12 && c == 13) { off = ftr0 + 1 + (r - 7); st = 6; }
+        else if (r >= 7 && r <= 12 && c >= r && c <= 12) {
+          const int a = r - 7, b = c - 7;
+          off = ff0 + a * 6 - a * (a - 1) / 2 + (b - a); st = 28;
+        } else if (r == 0 && c >= 7 && c <= 12) { off = ff0 + 21 + (c - 7); st = 28; }
+        acc_off[reg] = off >= 0 ? w_base + off : 0;   // (no destination: stage[0], dead here)
+        acc_stride[reg] = st;
+      }
+    }
     for (int q = 0; q < k; ++q) {
-      if ((q & 7) == 0) {
+      if ((q & 7) == 0 && q > 0) {
 #pragma unroll
         for (int u = 0; u < 8; ++u)
 #pragma unroll
@@ -395,17 +443,17 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
       }
       tot += g;
       const int u = lblk[q] - 1;   // the observation's tag block
+      // this lane's entries G[lk + 4 reg][li] (acc_off above): the four
+      // destinations are distinct, so their reads go out together
+      int di[4];
+      double dv[4];
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
-        const int r = lk + 4 * reg, c = li;   // this lane's entry G[r][c]
-        const double v = g[reg];
-        if (r >= 1 && r <= 6 && c >= 7 && c <= 12) W[(r - 1) * m + 1 + 6 * u + (c - 7)] += v;        // E'F_u
-        else if (r >= 7 && r <= 12 && c == 13) Ftr[1 + 6 * u + (r - 7)] += v;                       // F_u'r
-        else if (r >= 7 && r <= 12 && c >= r && c <= 12) {                                           // F_u'F_u
-          const int a = r - 7, b = c - 7;
-          FF[28 * u + a * 6 - a * (a - 1) / 2 + (b - a)] += v;
-        } else if (r == 0 && c >= 7 && c <= 12) FF[28 * u + 21 + (c - 7)] += v;                     // f'F_u
+        di[reg] = acc_off[reg] + acc_stride[reg] * u;
+        dv[reg] = sm[di[reg]];
       }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) sm[di[reg]] = dv[reg] + g[reg];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -816,19 +864,8 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   double *Ui = U + 36;                            // 36
   double *v = Ui + 36;                            // 8
   double *yc = v + 8;                             // 8
-  load_rows(P, scale, c, o0, nrows, rows);
-  __syncthreads();
   const double yf = P.cam_row >= 0 ? yF[P.cam_row] : 0.0;
-  for (int row = lane; row < nrows; row += kWave) {
-    const double *rr = rows + (long)row * kRowStride;
-    const int tr = P.tag_row[P.obs_tag[o0 + (row >> 3)]];
-    double q = rr[0] * yf;
-    if (tr >= 0) {
-#pragma unroll
-      for (int j = 0; j < 6; ++j) q += rr[7 + j] * yF[tr + j];
-    }
-    qv[row] = q;
-  }
+  load_rows_q(P, scale, yF, yf, c, o0, nrows, rows, qv);
   __syncthreads();
   if (reuse_ui) {
     // (U_c + D_c^2)^{-1} as k_schur formed it for this step
@@ -966,14 +1003,11 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
 // out[NPART+1] = F-side non-finite flag.
 // One block per LM scalar p (deterministic: fixed element -> thread
 // assignment, fixed tree); 8 loads in flight per thread.
-__global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
-                                                       const double *__restrict__ fparts,
-                                                       int nfparts, double *__restrict__ out,
-                                                       const int *__restrict__ flag, const int *gate) {
-  if (gated(gate)) return;
-  __shared__ double red[1024];
+__device__ __forceinline__ void reduce_parts_block(int p, const double *__restrict__ parts, int nc,
+                                                   const double *__restrict__ fparts, int nfparts,
+                                                   double *__restrict__ out, const int *__restrict__ flag,
+                                                   double *red) {
   const int t = threadIdx.x;
-  const int p = blockIdx.x;
   const bool is_max = (p == P_YBAD || p == P_CBAD || p == NPART + 1);
   const double *src = p < NPART ? parts + (long)p * nc : fparts;
   const int len = p < NPART ? nc : (fparts ? nfparts : 0);
@@ -1004,6 +1038,29 @@ __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict_
   }
 }
 
+__global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
+                                                       const double *__restrict__ fparts,
+                                                       int nfparts, double *__restrict__ out,
+                                                       const int *__restrict__ flag, const int *gate) {
+  if (gated(gate)) return;
+  __shared__ double red[1024];
+  reduce_parts_block(blockIdx.x, parts, nc, fparts, nfparts, out, flag, red);
+}
+
+// The linearization's two reductions of k_linearize's output in one launch
+// (they are independent): blocks 0 .. NPART+1 reduce the per-capture partials
+// (k_reduce_parts), the rest sum the tag slots (k_tag_reduce, 1024 slots each).
+__global__ __launch_bounds__(1024) void k_lin_reduce(DevProblem P, const double *__restrict__ obs_tg,
+                                                     double *__restrict__ g, double *__restrict__ colnorm,
+                                                     const double *__restrict__ parts, double *__restrict__ out) {
+  if (gated(P.gate_lin)) return;
+  __shared__ double red[1024];
+  if ((int)blockIdx.x < NPART + 2)
+    reduce_parts_block(blockIdx.x, parts, P.nc, nullptr, 0, out, nullptr, red);
+  else
+    tag_reduce_elem(P, obs_tg, (long)(blockIdx.x - (NPART + 2)) * 1024 + threadIdx.x, g, colnorm);
+}
+
 // Norms over free parameter slots, split into capture slots (out[0..2]) and
 // camera + tag slots (out[3..5]): max |g|, sum g^2, sum x^2.  The split lets
 // the capture-sharded path reduce only the disjoint capture part across ranks.
@@ -1011,63 +1068,71 @@ constexpr int kNormBlocks = 64;
 
 __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long cap_hi,
                                                     const unsigned char *__restrict__ free_,
-                                                    const double *__restrict__ g,
+                                                    double *__restrict__ g, double *__restrict__ colnorm,
+                                                    const double *__restrict__ red,
                                                     const double *__restrict__ x,
-                                                    double *__restrict__ part, const int *gate) {
+                                                    double *__restrict__ out, const int *gate) {
   if (gated(gate)) return;
-  __shared__ double red[6][256];
+  __shared__ double rs[6][256];
+  __shared__ int last;
   const int t = threadIdx.x;
-  double v[6] = {0, 0, 0, 0, 0, 0};
-  for (long i = (long)blockIdx.x * 256 + t; i < n; i += (long)kNormBlocks * 256) {
-    if (!free_[i]) continue;
-    const int o = (i >= cap_lo && i < cap_hi) ? 0 : 3;
-    const double gv = g[i], xv = x[i];
-    v[o] = fmax(v[o], fabs(gv));
-    v[o + 1] += gv * gv;
-    v[o + 2] += xv * xv;
-  }
-  for (int q = 0; q < 6; ++q) red[q][t] = v[q];
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (t < off) {
-      red[0][t] = fmax(red[0][t], red[0][t + off]);
-      red[1][t] += red[1][t + off];
-      red[2][t] += red[2][t + off];
-      red[3][t] = fmax(red[3][t], red[3][t + off]);
-      red[4][t] += red[4][t + off];
-      red[5][t] += red[5][t + off];
-    }
-    __syncthreads();
-  }
-  if (t < 6) part[6L * blockIdx.x + t] = red[t][0];
-}
-
-// second stage: out[q] = reduction over the kNormBlocks partials (fixed tree)
-__global__ __launch_bounds__(64) void k_slot_norms_final(const double *__restrict__ part,
-                                                         double *__restrict__ out, const int *gate) {
-  if (gated(gate)) return;
-  __shared__ double red[6][kNormBlocks];
-  const int t = threadIdx.x;
-  for (int q = 0; q < 6; ++q) red[q][t] = part[6L * t + q];
-  __syncthreads();
-  for (int off = kNormBlocks / 2; off > 0; off >>= 1) {
-    if (t < off)
-      for (int q = 0; q < 6; ++q)
-        red[q][t] = (q % 3 == 0) ? fmax(red[q][t], red[q][t + off]) : red[q][t] + red[q][t + off];
-    __syncthreads();
-  }
-  if (t < 6) out[t] = red[t][0];
-}
-
-// camera slots from the reduced per-capture partials (masked by freedom)
-__global__ void k_camera_slots(const unsigned char *__restrict__ free_, const double *__restrict__ red,
-                               double *__restrict__ g, double *__restrict__ colnorm, const int *gate) {
-  if (threadIdx.x == 0 && !gated(gate)) {
-    g[0] = free_[0] ? red[P_GF] : 0.0;
+  // the camera slots from the reduced per-capture partials (f gradient and
+  // column norm; l1, l2 have no Jacobian column): written once, and used here
+  // in place of g[0..2]
+  const double g0 = free_[0] ? red[P_GF] : 0.0;
+  if (blockIdx.x == 0 && t == 0) {
+    g[0] = g0;
     colnorm[0] = free_[0] ? red[P_CF] : 0.0;
     g[1] = g[2] = 0.0;
     colnorm[1] = colnorm[2] = 0.0;
   }
+  double v[6] = {0, 0, 0, 0, 0, 0};
+  for (long i = (long)blockIdx.x * 256 + t; i < n; i += (long)kNormBlocks * 256) {
+    if (!free_[i]) continue;
+    const int o = (i >= cap_lo && i < cap_hi) ? 0 : 3;
+    const double gv = i >= 3 ? g[i] : (i == 0 ? g0 : 0.0), xv = x[i];
+    v[o] = fmax(v[o], fabs(gv));
+    v[o + 1] += gv * gv;
+    v[o + 2] += xv * xv;
+  }
+  for (int q = 0; q < 6; ++q) rs[q][t] = v[q];
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      rs[0][t] = fmax(rs[0][t], rs[0][t + off]);
+      rs[1][t] += rs[1][t + off];
+      rs[2][t] += rs[2][t + off];
+      rs[3][t] = fmax(rs[3][t], rs[3][t + off]);
+      rs[4][t] += rs[4][t + off];
+      rs[5][t] += rs[5][t + off];
+    }
+    __syncthreads();
+  }
+  // out[8 + 6 b + q]: block b's partials; out[7] (as an int): blocks done.
+  // The last block to finish reduces the kNormBlocks partials over a fixed
+  // tree (independent of which block is last) into out[0..5], and resets the
+  // count for the next launch.
+  double *part = out + 8;
+  int *done = reinterpret_cast<int *>(out + 7);
+  if (t == 0) {
+    for (int q = 0; q < 6; ++q) part[6L * blockIdx.x + q] = rs[q][0];
+    __threadfence();   // the partials before the count (agent scope: the blocks span XCDs)
+    last = atomicAdd(done, 1) == kNormBlocks - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();     // every block's partials after the count
+  if (t < kNormBlocks)
+    for (int q = 0; q < 6; ++q) rs[q][t] = part[6L * t + q];
+  __syncthreads();
+  for (int off = kNormBlocks / 2; off > 0; off >>= 1) {
+    if (t < off)
+      for (int q = 0; q < 6; ++q)
+        rs[q][t] = (q % 3 == 0) ? fmax(rs[q][t], rs[q][t + off]) : rs[q][t] + rs[q][t + off];
+    __syncthreads();
+  }
+  if (t < 6) out[t] = rs[t][0];
+  if (t == 0) atomicExch(done, 0);
 }
 
 // one thread per (observation, row): residual and 15-column Jacobian row
@@ -1121,11 +1186,11 @@ void launch_linearize(const DevProblem &P, const double *x, double *g, double *c
   hipLaunchKernelGGL(k_linearize, dim3(P.nc), dim3(kWave), lds, s, P, x, g, colnorm, obs_tg, parts);
 }
 
-void launch_tag_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
-                       hipStream_t s) {
-  if (P.nt == 0) return;
-  const long n = 12L * P.nt;
-  hipLaunchKernelGGL(k_tag_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, obs_tg, g, colnorm);
+void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
+                       const double *parts, double *out, hipStream_t s) {
+  const unsigned tag_blocks = (unsigned)((12L * P.nt + 1023) / 1024);
+  hipLaunchKernelGGL(k_lin_reduce, dim3(NPART + 2 + tag_blocks), dim3(1024), 0, s, P, obs_tg, g, colnorm, parts,
+                     out);
 }
 
 void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale, hipStream_t s) {
@@ -1197,16 +1262,11 @@ void launch_reduce_parts(const double *parts, int nc, const double *fparts, int 
   hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, gate);
 }
 
-void launch_slot_norms(const DevProblem &P, const double *g, const double *x, double *out, hipStream_t s) {
-  // out[0..7] results, out[8..] the per-block partials (see d_norms)
-  hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g, x,
-                     out + 8, P.gate_lin);
-  hipLaunchKernelGGL(k_slot_norms_final, dim3(1), dim3(kNormBlocks), 0, s, out + 8, out, P.gate_lin);
-}
-
-void launch_camera_slots(const DevProblem &P, const double *red, double *g, double *colnorm,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_camera_slots, dim3(1), dim3(64), 0, s, P.slot_free, red, g, colnorm, P.gate_lin);
+void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
+                       double *out, hipStream_t s) {
+  // out[0..5] results, out[7] the block count (zero between launches), out[8..] the per-block partials
+  hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g,
+                     colnorm, red, x, out, P.gate_lin);
 }
 
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,

@@ -683,8 +683,10 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   d_fparts.alloc(2L * std::max(n_fparts, 1));
   // stays zero when there are no reduced rows (k_update_f is then not launched)
   if (!has_f) HIP_CHECK(hipMemsetAsync(d_fparts.p, 0, d_fparts.n * sizeof(double), stream));
-  d_red.alloc(16 + 8 + 6 * 64);   // LM scalars | slot norms: results + k_slot_norms block partials
+  const double *red_prev = d_red.p;
+  d_red.alloc(16 + 8 + 6 * 64);   // LM scalars | slot norms: results, block count, k_slot_norms block partials
   d_norms_p = d_red.p + 16;       // (one D2H carries both after a linearization)
+  if (d_red.p != red_prev) HIP_CHECK(hipMemsetAsync(d_norms_p + 7, 0, sizeof(double), stream));   // the count
   d_flag.alloc(1);
   if (has_f) {
     d_slab.alloc(std::max(sg.cap_off[nc], 1L));
@@ -840,16 +842,14 @@ void arslam_lm::linearize_launch() {
   h_lin.alloc(32);
   timers[PH_LIN].start(stream);
   arslam::launch_linearize(P, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
-  arslam::launch_tag_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, stream);
-  arslam::launch_reduce_parts(d_parts.p, nc, nullptr, 0, d_red.p, stream);
+  arslam::launch_lin_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream);
   if (nranks > 1) {
     const long t0 = 3 + 6L * nc;
     allreduce(d_g.p + t0, n - t0, ARSLAM_OP_SUM);
     allreduce(d_colnorm.p + t0, n - t0, ARSLAM_OP_SUM);
     allreduce(d_red.p, 4, ARSLAM_OP_SUM);   // cost, fixed, g_f, col_f
   }
-  arslam::launch_camera_slots(P, d_red.p, d_g.p, d_colnorm.p, stream);
-  arslam::launch_slot_norms(P, d_g.p, x, d_norms_p, stream);
+  arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream);
   if (nranks > 1) {
     // capture slots are disjoint across ranks, tag/camera slots replicated:
     // norms[0..2] cover captures (max, sum, sum), norms[3..5] the rest
@@ -996,10 +996,8 @@ void arslam_lm::enqueue_iteration(int part, const arslam::LmDevConsts &c) {
     arslam::launch_lm_decide(st, d_red.p, c, stream);
     arslam::launch_lm_copy(x, xc, n, &st->accept, stream);
     arslam::launch_linearize(Q, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
-    arslam::launch_tag_reduce(Q, d_obs_tg.p, d_g.p, d_colnorm.p, stream);
-    arslam::launch_reduce_parts(d_parts.p, nc, nullptr, 0, d_red.p, stream, nullptr, &st->gate_lin);
-    arslam::launch_camera_slots(Q, d_red.p, d_g.p, d_colnorm.p, stream);
-    arslam::launch_slot_norms(Q, d_g.p, x, d_norms_p, stream);
+    arslam::launch_lin_reduce(Q, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream);
+    arslam::launch_slot_norms(Q, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream);
     arslam::launch_lm_finalize(st, d_red.p, c, stream);
     arslam::launch_lm_copy(d_xbest.p, x, n, &st->copy_best, stream);
   }
