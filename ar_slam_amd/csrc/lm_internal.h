@@ -251,7 +251,7 @@ void launch_linearize(const DevProblem &P, const double *x, double *g, double *c
 // k_linearize's reductions in one launch: the per-capture partials into
 // out[0..NPART+1] (launch_reduce_parts without fparts) and the tag slots' g and colnorm
 void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
-                       const double *parts, double *out, hipStream_t s);
+                       const double *parts, double *out, hipStream_t s, double *hout = nullptr);
 void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale,
                   hipStream_t s);
 void launch_lm_diag(const DevProblem &P, const double *scale, const double *colnorm, double dmin,
@@ -280,7 +280,8 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 // (flag: also out[NPART + 2] = indefinite (flag > 0), out[NPART + 3] = executor
 // fault (flag < 0), out[NPART + 4] = the raw flag)
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts,
-                         double *out, hipStream_t s, const int *flag = nullptr, const int *gate = nullptr);
+                         double *out, hipStream_t s, const int *flag = nullptr, const int *gate = nullptr,
+                         double *hout = nullptr);
 void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, hipStream_t s);
 // The camera slots of g and colnorm from the reduced partials red (P_GF, P_CF),
 // then the norms over free parameter slots: out[0..2] = max|g|, sum g^2, sum x^2
@@ -288,7 +289,9 @@ void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, 
 // the launch's block count (must be zero before the first launch), out[8..]
 // its per-block partials.
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
-                       double *out, hipStream_t s);
+                       double *out, hipStream_t s, double *hout = nullptr);
+// (hout, in the three launchers above: page-locked host words that also receive
+// the results, so a single-rank solve needs no device-to-host copy for them)
 
 // Optional per-launch event pairs around the dominant kernel (trailing update).
 struct LaunchTiming {

@@ -280,12 +280,15 @@ __device__ __forceinline__ void tag_reduce_elem(const DevProblem &P, const doubl
   const int t = (int)(e / 12), j = (int)(e % 12);
   double s = 0.0;
   const int qa = P.tag_start[t], qb = P.tag_start[t + 1];
-  for (int q0 = qa; q0 < qb; q0 += 8) {   // 8 gathers in flight; summed in observation order
-    double v[8];
+  for (int q0 = qa; q0 < qb; q0 += 32) {   // 32 gathers in flight; summed in observation order
+    int o[32];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = obs_tg[12L * P.tag_obs[min(q0 + u, qb - 1)] + j];
+    for (int u = 0; u < 32; ++u) o[u] = P.tag_obs[min(q0 + u, qb - 1)];
+    double v[32];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s += (q0 + u < qb) ? v[u] : 0.0;
+    for (int u = 0; u < 32; ++u) v[u] = obs_tg[12L * o[u] + j];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) s += (q0 + u < qb) ? v[u] : 0.0;
   }
   const long slot = slot_tag(P, t) + (j % 6);
   const double v = P.slot_free[slot] ? s : 0.0;
@@ -552,6 +555,83 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   const bool one_chunk = m + 1 <= kWave;
   double z[6];
   if (one_chunk) make_z(lane, z);
+  if (one_chunk) {
+    // All M = m + 1 local rows at once as one MFMA product C = Wx' Z (K = 6,
+    // padded to 8), Wx = [W | E'r] (6 x M), Z = [z_0 .. z_{m-1} | 0] (6 x M):
+    // C[p][q] = W_p' z_q, the rhs row's (E'r)' z_q at p = m.  Only the 16x16
+    // tiles that hold stored (lower block-triangle) entries are formed; each
+    // lane then writes its entries F_p'F_q - C[p][q] (the F'F / F'r / f'f
+    // terms where they are nonzero) straight to their block-packed slab slots.
+    const int M = m + 1;
+    const int li = lane & 15, lk = lane >> 4;
+    double *Zs = stage;   // 6 M doubles: Zs[a M + q]
+    if (lane < M)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) Zs[a * M + lane] = z[a];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double Aop[4][2], Bop[4][2];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int a = 4 * kb + lk, pq = 16 * r + li;
+        const bool in = a < 6 && pq < M;
+        Aop[r][kb] = in ? (pq < m ? W[a * m + pq] : Etr[a]) : 0.0;
+        Bop[r][kb] = in ? Zs[a * M + pq] : 0.0;
+      }
+    typedef double dbl4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (16 * r >= M) break;
+      // this lane's rows p = 16 r + lk + 4 reg: block row, row inside it, last stored column
+      int pU[4], pI[4], pEnd[4];
+      long pOff[4];
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int pp = 16 * r + lk + 4 * reg;
+        const int up = pp >= 1 && pp < m ? (pp - 1) / 6 : -1;
+        const int U = pp == 0 ? 0 : (pp < m ? 1 + up : nblk + 1);
+        pU[reg] = U;
+        pI[reg] = up >= 0 ? pp - 1 - 6 * up : 0;
+        pEnd[reg] = pp == 0 ? 1 : (pp < m ? 7 + 6 * up : M);   // columns q < pEnd are stored
+        pOff[reg] = schur_block_off(U, 0, nblk);               // the block row's first element
+      }
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        if (cc > r + 1 || 16 * cc >= M) break;
+        dbl4v acc = {0, 0, 0, 0};
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[r][0], Bop[cc][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[r][1], Bop[cc][1], acc, 0, 0, 0);
+        const int q = 16 * cc + li;
+        const int uq = q >= 1 && q < m ? (q - 1) / 6 : -1;   // q's tag block
+        const int V = q == 0 ? 0 : (q < m ? 1 + uq : nblk + 1);
+        const int sV = schur_blk_size(V, nblk), q0V = schur_blk_start(V, nblk);
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int pp = 16 * r + lk + 4 * reg;
+          if (pp >= M || q >= pEnd[reg]) continue;
+          const int U = pU[reg], sU = schur_blk_size(U, nblk);
+          double ff = 0.0;
+          if (pp == 0) {
+            ff = *ff00;                                     // (q == 0 only)
+          } else if (pp == m) {
+            ff = q < m ? Ftr[q] : 0.0;
+          } else {
+            const int up = U - 1, i = pI[reg];
+            if (q == 0) {
+              ff = FF[28 * up + 21 + i];                    // f'F_u
+            } else if (uq == up) {                          // F_u'F_u packed upper (a <= b)
+              const int iq = q - 1 - 6 * uq, lo = min(i, iq), hi = max(i, iq);
+              ff = FF[28 * up + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+            }
+          }
+          out[pOff[reg] + (long)sU * q0V + pI[reg] * sV + (q - q0V)] = ff - acc[reg];
+        }
+      }
+    }
+  } else
   for (int U = 0; U <= nblk + 1; ++U) {
     const int sU = schur_blk_size(U, nblk), p0U = schur_blk_start(U, nblk), ncol = p0U + sU;
     for (int q0 = 0; q0 < ncol; q0 += kWave) {
@@ -1006,7 +1086,7 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
 __device__ __forceinline__ void reduce_parts_block(int p, const double *__restrict__ parts, int nc,
                                                    const double *__restrict__ fparts, int nfparts,
                                                    double *__restrict__ out, const int *__restrict__ flag,
-                                                   double *red) {
+                                                   double *red, double *__restrict__ hout) {
   const int t = threadIdx.x;
   const bool is_max = (p == P_YBAD || p == P_CBAD || p == NPART + 1);
   const double *src = p < NPART ? parts + (long)p * nc : fparts;
@@ -1029,22 +1109,30 @@ __device__ __forceinline__ void reduce_parts_block(int p, const double *__restri
     if (t < off) red[t] = is_max ? fmax(red[t], red[t + off]) : red[t] + red[t + off];
     __syncthreads();
   }
-  if (t == 0) out[p] = red[0];
-  if (flag && p == 0 && t == 0) {   // rides along the step's one D2H
+  if (t == 0) {
+    out[p] = red[0];
+    if (hout) hout[p] = red[0];
+  }
+  if (flag && p == 0 && t == 0) {   // rides along the step's one host read
     const int f = *flag;
-    out[NPART + 2] = f > 0 ? 1.0 : 0.0;   // indefinite reduced system: an invalid LM step (max over ranks)
-    out[NPART + 3] = f < 0 ? 1.0 : 0.0;   // executor fault: an error, never a step (max over ranks)
-    out[NPART + 4] = (double)f;           // this rank's raw code, for the error message
+    const double v[3] = {f > 0 ? 1.0 : 0.0,   // indefinite reduced system: an invalid LM step (max over ranks)
+                         f < 0 ? 1.0 : 0.0,   // executor fault: an error, never a step (max over ranks)
+                         (double)f};          // this rank's raw code, for the error message
+    for (int q = 0; q < 3; ++q) {
+      out[NPART + 2 + q] = v[q];
+      if (hout) hout[NPART + 2 + q] = v[q];
+    }
   }
 }
 
 __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
                                                        const double *__restrict__ fparts,
                                                        int nfparts, double *__restrict__ out,
-                                                       const int *__restrict__ flag, const int *gate) {
+                                                       const int *__restrict__ flag, const int *gate,
+                                                       double *__restrict__ hout) {
   if (gated(gate)) return;
   __shared__ double red[1024];
-  reduce_parts_block(blockIdx.x, parts, nc, fparts, nfparts, out, flag, red);
+  reduce_parts_block(blockIdx.x, parts, nc, fparts, nfparts, out, flag, red, hout);
 }
 
 // The linearization's two reductions of k_linearize's output in one launch
@@ -1052,11 +1140,12 @@ __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict_
 // (k_reduce_parts), the rest sum the tag slots (k_tag_reduce, 1024 slots each).
 __global__ __launch_bounds__(1024) void k_lin_reduce(DevProblem P, const double *__restrict__ obs_tg,
                                                      double *__restrict__ g, double *__restrict__ colnorm,
-                                                     const double *__restrict__ parts, double *__restrict__ out) {
+                                                     const double *__restrict__ parts, double *__restrict__ out,
+                                                     double *__restrict__ hout) {
   if (gated(P.gate_lin)) return;
   __shared__ double red[1024];
   if ((int)blockIdx.x < NPART + 2)
-    reduce_parts_block(blockIdx.x, parts, P.nc, nullptr, 0, out, nullptr, red);
+    reduce_parts_block(blockIdx.x, parts, P.nc, nullptr, 0, out, nullptr, red, hout);
   else
     tag_reduce_elem(P, obs_tg, (long)(blockIdx.x - (NPART + 2)) * 1024 + threadIdx.x, g, colnorm);
 }
@@ -1071,7 +1160,8 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
                                                     double *__restrict__ g, double *__restrict__ colnorm,
                                                     const double *__restrict__ red,
                                                     const double *__restrict__ x,
-                                                    double *__restrict__ out, const int *gate) {
+                                                    double *__restrict__ out, const int *gate,
+                                                    double *__restrict__ hout) {
   if (gated(gate)) return;
   __shared__ double rs[6][256];
   __shared__ int last;
@@ -1131,7 +1221,10 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
         rs[q][t] = (q % 3 == 0) ? fmax(rs[q][t], rs[q][t + off]) : rs[q][t] + rs[q][t + off];
     __syncthreads();
   }
-  if (t < 6) out[t] = rs[t][0];
+  if (t < 6) {
+    out[t] = rs[t][0];
+    if (hout) hout[t] = rs[t][0];
+  }
   if (t == 0) atomicExch(done, 0);
 }
 
@@ -1187,10 +1280,10 @@ void launch_linearize(const DevProblem &P, const double *x, double *g, double *c
 }
 
 void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
-                       const double *parts, double *out, hipStream_t s) {
+                       const double *parts, double *out, hipStream_t s, double *hout) {
   const unsigned tag_blocks = (unsigned)((12L * P.nt + 1023) / 1024);
   hipLaunchKernelGGL(k_lin_reduce, dim3(NPART + 2 + tag_blocks), dim3(1024), 0, s, P, obs_tg, g, colnorm, parts,
-                     out);
+                     out, hout);
 }
 
 void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale, hipStream_t s) {
@@ -1258,15 +1351,16 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 }
 
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
-                         hipStream_t s, const int *flag, const int *gate) {
-  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, gate);
+                         hipStream_t s, const int *flag, const int *gate, double *hout) {
+  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, gate,
+                     hout);
 }
 
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
-                       double *out, hipStream_t s) {
+                       double *out, hipStream_t s, double *hout) {
   // out[0..5] results, out[7] the block count (zero between launches), out[8..] the per-block partials
   hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g,
-                     colnorm, red, x, out, P.gate_lin);
+                     colnorm, red, x, out, P.gate_lin, hout);
 }
 
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,

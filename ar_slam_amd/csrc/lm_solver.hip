@@ -840,16 +840,20 @@ void arslam_lm::reload_values(const arslam_soa_problem *p_in) {
 // and the norms the minimizer reads.  Ceres EvaluateGradientAndJacobian.
 void arslam_lm::linearize_launch() {
   h_lin.alloc(32);
+  // one rank: the reductions also store their results straight into the
+  // page-locked h_lin (no copy launch); several: h_lin is copied after the exchanges
+  const bool direct = nranks == 1;
   timers[PH_LIN].start(stream);
   arslam::launch_linearize(P, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
-  arslam::launch_lin_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream);
+  arslam::launch_lin_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream,
+                            direct ? h_lin.p : nullptr);
   if (nranks > 1) {
     const long t0 = 3 + 6L * nc;
     allreduce(d_g.p + t0, n - t0, ARSLAM_OP_SUM);
     allreduce(d_colnorm.p + t0, n - t0, ARSLAM_OP_SUM);
     allreduce(d_red.p, 4, ARSLAM_OP_SUM);   // cost, fixed, g_f, col_f
   }
-  arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream);
+  arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, direct ? h_lin.p + 16 : nullptr);
   if (nranks > 1) {
     // capture slots are disjoint across ranks, tag/camera slots replicated:
     // norms[0..2] cover captures (max, sum, sum), norms[3..5] the rest
@@ -857,7 +861,7 @@ void arslam_lm::linearize_launch() {
     allreduce(d_norms_p + 1, 2, ARSLAM_OP_SUM);
   }
   timers[PH_LIN].stop(stream);
-  HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 22 * sizeof(double), hipMemcpyDeviceToHost, stream));
+  if (!direct) HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 22 * sizeof(double), hipMemcpyDeviceToHost, stream));
 }
 
 // (after a stream sync that covers linearize_launch)
@@ -1393,7 +1397,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     arslam::launch_backsub(P, x, d_scale.p, d_diag.p, radius, d_yF.p, xc, d_parts.p, stream, has_f, true);
     timers[PH_BACK].stop(stream);
     timers[PH_COST].start(stream);
-    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p);
+    h_step.alloc(16);
+    // (one rank: the scalars are also stored straight into the page-locked h_step)
+    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p, nullptr,
+                                nranks == 1 ? h_step.p : nullptr);
     if (nranks > 1) {
       // model change, capture step^2, candidate cost, fixed; flags by max
       allreduce(d_red.p + arslam::P_COST, 2, ARSLAM_OP_SUM);
@@ -1403,8 +1410,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       allreduce(d_red.p + arslam::NPART + 1, 3, ARSLAM_OP_MAX);
     }
     timers[PH_COST].stop(stream);
-    h_step.alloc(16);
-    HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 5) * sizeof(double), hipMemcpyDeviceToHost, stream));
+    if (nranks > 1)
+      HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 5) * sizeof(double), hipMemcpyDeviceToHost, stream));
     spin_sync();
     const double *red = h_step.p;
     // A stuck dependency wait of a persistent executor is a device fault, not
