@@ -1894,6 +1894,22 @@ void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagA
                      P.upd_cnt, nc, P.bs_counters, nd, l);
 }
 
+ExecReset exec_reset_args(const LltPlan &P, int *flag, double *ysent, long nys) {
+  ExecReset r;
+  r.flag = flag;
+  r.na = P.n_dag_tasks ? 2 * P.n_tiles + kDagCounterExtra : 0;
+  r.a = P.dag_counters;
+  r.nb = P.n_dag_tasks;
+  r.b = P.dag_claimed;
+  r.nc = P.n_split;
+  r.c = P.upd_cnt;
+  r.nd = P.h_bcols.empty() ? 0 : (long)P.T + 1;
+  r.d = P.bs_counters;
+  r.ysent = ysent;
+  r.nys = nys;
+  return r;
+}
+
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s) {
   if (P.n_tiles) (void)hipMemsetAsync(S, 0, (size_t)P.n_tiles * T64 * T64 * sizeof(double), s);
 }

@@ -246,22 +246,28 @@ void llt_plan_reset(LltPlan &plan);                // host side only; the arena 
 
 
 // ---- lm_kernels.hip ----
+struct ExecReset;   // (dense_llt section below)
 void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
                       double *obs_tg, double *parts, hipStream_t s);
 // k_linearize's reductions in one launch: the per-capture partials into
 // out[0..NPART+1] (launch_reduce_parts without fparts) and the tag slots' g and colnorm
 void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
                        const double *parts, double *out, hipStream_t s, double *hout = nullptr);
+struct LmDiagArgs;
+// (ld: also the LM diagonal from the new scale, ld->diag / dmin / dmax)
 void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale,
-                  hipStream_t s);
+                  hipStream_t s, const LmDiagArgs *ld = nullptr);
 void launch_lm_diag(const DevProblem &P, const double *scale, const double *colnorm, double dmin,
                     double dmax, double *diag, hipStream_t s);
 // (prep = true: k_prep_reduced's diagonal work is done by the gather itself --
 // single rank only, where the gathered S is final)
 // (zero_tiles: the first zero_tiles 64x64 tiles of S are cleared by extra
 // k_schur blocks before the gather writes S)
+// (er: the persistent executors' reset rides along in k_schur's blocks past
+// the tiles; only with P.nc > 0)
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                  double radius, double *S, hipStream_t s, bool prep = false, long zero_tiles = 0);
+                  double radius, double *S, hipStream_t s, bool prep = false, long zero_tiles = 0,
+                  const ExecReset *er = nullptr);
 // (which: -1 every row; 0 / 1 only the rows of tile columns of that class)
 void launch_prep_reduced(const DevProblem &P, const double *diag, double radius, double *S,
                          hipStream_t s, int which = -1);
@@ -288,8 +294,9 @@ void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, 
 // over capture slots, out[3..5] the same over camera + tag slots.  out[7] is
 // the launch's block count (must be zero before the first launch), out[8..]
 // its per-block partials.
+// (ld: also the LM diagonal clamp(s^2 colnorm) of every slot from ld->scale, into ld->diag)
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
-                       double *out, hipStream_t s, double *hout = nullptr);
+                       double *out, hipStream_t s, double *hout = nullptr, const LmDiagArgs *ld = nullptr);
 // (hout, in the three launchers above: page-locked host words that also receive
 // the results, so a single-rank solve needs no device-to-host copy for them)
 
@@ -364,6 +371,26 @@ constexpr unsigned long long kYSentinel = 0x7ff47ff47ff47ff4ull;
 // *flag and every counter of the two persistent executors to zero, one launch
 // (with ld: the LM diagonal in the same launch)
 void launch_exec_reset(const LltPlan &P, int *flag, hipStream_t s, const LmDiagArgs *ld = nullptr);
+// The same reset as element-wise work another launch can carry (k_schur's
+// blocks past the captures and tiles, when the diagonal needs no update):
+// element e < n() zeroes one counter / writes one y sentinel; e == 0 also the flag.
+struct ExecReset {
+  int *flag = nullptr;
+  int *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+  long na = 0, nb = 0, nc = 0, nd = 0;
+  double *ysent = nullptr;
+  long nys = 0;
+  __host__ __device__ long n() const { return na + nb + nc + nd > nys ? na + nb + nc + nd : nys; }
+};
+ExecReset exec_reset_args(const LltPlan &P, int *flag, double *ysent, long nys);
+__device__ __forceinline__ void exec_reset_elem(const ExecReset &r, long e) {
+  if (e < r.nys) r.ysent[e] = __longlong_as_double((long long)kYSentinel);
+  if (e < r.na) r.a[e] = 0;
+  else if (e < r.na + r.nb) r.b[e - r.na] = 0;
+  else if (e < r.na + r.nb + r.nc) r.c[e - r.na - r.nb] = 0;
+  else if (e < r.na + r.nb + r.nc + r.nd) r.d[e - r.na - r.nb - r.nc] = 0;
+  if (e == 0 && r.flag) *r.flag = 0;
+}
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,
                              const int *flag, hipStream_t s);
 // The same backward solve as one persistent launch (columns in root-first

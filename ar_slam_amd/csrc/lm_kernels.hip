@@ -295,12 +295,15 @@ __device__ __forceinline__ void tag_reduce_elem(const DevProblem &P, const doubl
   if (j < 6) g[slot] = v; else colnorm[slot] = v;
 }
 
+// (diag: also the LM diagonal clamp(s^2 colnorm, dmin, dmax) from the new scale: k_lm_diag's work)
 __global__ void k_scale(long n, const unsigned char *__restrict__ free_, const double *__restrict__ colnorm,
-                        int jacobi, double *__restrict__ scale) {
+                        int jacobi, double *__restrict__ scale, double dmin, double dmax, double *__restrict__ diag) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // jacobian_scaling = 1 / (1 + sqrt(SquaredColumnNorm)) at iteration 0
-  scale[i] = free_[i] ? (jacobi ? 1.0 / (1.0 + sqrt(colnorm[i])) : 1.0) : 0.0;
+  const double sv = free_[i] ? (jacobi ? 1.0 / (1.0 + sqrt(colnorm[i])) : 1.0) : 0.0;
+  scale[i] = sv;
+  if (diag) diag[i] = fmin(fmax(sv * sv * colnorm[i], dmin), dmax);
 }
 
 __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double *__restrict__ colnorm,
@@ -319,12 +322,18 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
 // stored for k_schur_gather.  One wave per capture.
 __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ scale,
                                                  const double *__restrict__ diag, double radius,
-                                                 double *__restrict__ zero_tiles) {
+                                                 double *__restrict__ zero_tiles, long n_zero, ExecReset er) {
   if (gated(P.gate_step)) return;
   radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   SCHUR_STAMP_INIT;
   const int c = blockIdx.x, lane = threadIdx.x;
+  if (c >= P.nc + n_zero) {
+    // the blocks past the tiles: the persistent executors' reset (ExecReset;
+    // launch_exec_reset's work when the LM diagonal needs no update)
+    exec_reset_elem(er, (long)(c - P.nc - n_zero) * kWave + lane);
+    return;
+  }
   if (c >= P.nc) {
     // the blocks past the captures clear one 64x64 tile of S each (the gather
     // writes only the assembled blocks; the rest of S must be zero): the
@@ -1161,7 +1170,8 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
                                                     const double *__restrict__ red,
                                                     const double *__restrict__ x,
                                                     double *__restrict__ out, const int *gate,
-                                                    double *__restrict__ hout) {
+                                                    double *__restrict__ hout, const double *__restrict__ scale,
+                                                    double dmin, double dmax, double *__restrict__ diag) {
   if (gated(gate)) return;
   __shared__ double rs[6][256];
   __shared__ int last;
@@ -1176,8 +1186,13 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
     g[1] = g[2] = 0.0;
     colnorm[1] = colnorm[2] = 0.0;
   }
+  const double cn0 = free_[0] ? red[P_CF] : 0.0;   // (colnorm[0], as block 0 writes it)
   double v[6] = {0, 0, 0, 0, 0, 0};
   for (long i = (long)blockIdx.x * 256 + t; i < n; i += (long)kNormBlocks * 256) {
+    if (diag) {   // the LM diagonal of the new linearization (launch_exec_reset's k_lm_diag work)
+      const double cn = i >= 3 ? colnorm[i] : (i == 0 ? cn0 : 0.0);
+      diag[i] = fmin(fmax(scale[i] * scale[i] * cn, dmin), dmax);
+    }
     if (!free_[i]) continue;
     const int o = (i >= cap_lo && i < cap_hi) ? 0 : 3;
     const double gv = i >= 3 ? g[i] : (i == 0 ? g0 : 0.0), xv = x[i];
@@ -1286,9 +1301,10 @@ void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, dou
                      out, hout);
 }
 
-void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale, hipStream_t s) {
+void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale, hipStream_t s,
+                  const LmDiagArgs *ld) {
   hipLaunchKernelGGL(k_scale, dim3((unsigned)((P.n + 255) / 256)), dim3(256), 0, s, P.n, P.slot_free,
-                     colnorm, jacobi, scale);
+                     colnorm, jacobi, scale, ld ? ld->dmin : 0.0, ld ? ld->dmax : 0.0, ld ? ld->diag : nullptr);
 }
 
 void launch_lm_diag(const DevProblem &P, const double *scale, const double *colnorm, double dmin,
@@ -1298,7 +1314,8 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
 }
 
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
-                  double radius, double *S, hipStream_t s, bool prep, long zero_tiles) {
+                  double radius, double *S, hipStream_t s, bool prep, long zero_tiles, const ExecReset *er) {
+  const ExecReset r = er ? *er : ExecReset{};
   if (P.nc == 0) {
     if (zero_tiles) (void)hipMemsetAsync(S, 0, (size_t)zero_tiles * 4096 * sizeof(double), s);
     if (prep) launch_prep_reduced(P, diag, radius, S, s);
@@ -1308,7 +1325,9 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
   const int m = 1 + 6 * maxk;
   const size_t lds = sizeof(double) * (6L * (m + 1) + 6L * maxk + 36 + 36 + 8 + 7L * m + 4 + 28L * maxk) +
                      sizeof(int) * (maxk + 2) + 2 * sizeof(double) + 64;
-  hipLaunchKernelGGL(k_schur, dim3((unsigned)(P.nc + zero_tiles)), dim3(kWave), lds, s, P, scale, diag, radius, S);
+  const long reset_blocks = (r.n() + kWave - 1) / kWave;
+  hipLaunchKernelGGL(k_schur, dim3((unsigned)(P.nc + zero_tiles + reset_blocks)), dim3(kWave), lds, s, P, scale, diag,
+                     radius, S, zero_tiles, r);
   const double *pd = prep ? diag : nullptr;
   const unsigned gb = (unsigned)((P.n_items + 3) / 4) + (prep ? (unsigned)((P.N + 255) / 256) : 0u);
   if (gb) hipLaunchKernelGGL(k_schur_gather, dim3(gb), dim3(256), 0, s, P, S, pd, radius);
@@ -1357,10 +1376,11 @@ void launch_reduce_parts(const double *parts, int nc, const double *fparts, int 
 }
 
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
-                       double *out, hipStream_t s, double *hout) {
+                       double *out, hipStream_t s, double *hout, const LmDiagArgs *ld) {
   // out[0..5] results, out[7] the block count (zero between launches), out[8..] the per-block partials
   hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g,
-                     colnorm, red, x, out, P.gate_lin, hout);
+                     colnorm, red, x, out, P.gate_lin, hout, ld ? ld->scale : nullptr, ld ? ld->dmin : 0.0,
+                     ld ? ld->dmax : 0.0, ld ? ld->diag : nullptr);
 }
 
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,

@@ -449,6 +449,10 @@ struct arslam_lm {
   void linearize_launch();
   void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
   PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [16..21] slot norms
+  // host LM loop: the Jacobi scale of this solve is set, so each later
+  // linearization also forms the LM diagonal (k_slot_norms) and the step's
+  // executor reset rides in k_schur's launch
+  bool diag_in_lin = false;
   PinnedBuf h_x;     // [n] parameter download (write_back)
   PinnedBuf h_step;  // [0..NPART+1] the step's reduced scalars, [NPART+2..4] the factorization flags
   hipEvent_t ev_sync = nullptr;
@@ -853,7 +857,9 @@ void arslam_lm::linearize_launch() {
     allreduce(d_colnorm.p + t0, n - t0, ARSLAM_OP_SUM);
     allreduce(d_red.p, 4, ARSLAM_OP_SUM);   // cost, fixed, g_f, col_f
   }
-  arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, direct ? h_lin.p + 16 : nullptr);
+  const arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, opt.min_lm_diagonal, opt.max_lm_diagonal, d_diag.p};
+  arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, direct ? h_lin.p + 16 : nullptr,
+                            diag_in_lin ? &ld : nullptr);
   if (nranks > 1) {
     // capture slots are disjoint across ranks, tag/camera slots replicated:
     // norms[0..2] cover captures (max, sum, sum), norms[3..5] the rest
@@ -1172,7 +1178,16 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     s->total_time_s = now_s() - t_start;
     return;
   }
-  arslam::launch_scale(P, d_colnorm.p, o.jacobi_scaling, d_scale.p, stream);
+  {
+    // the scale, and from it the first step's LM diagonal (k_lm_diag's work)
+    const arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal, d_diag.p};
+    arslam::launch_scale(P, d_colnorm.p, o.jacobi_scaling, d_scale.p, stream, &ld);
+  }
+  diag_in_lin = true;
+  struct DiagInLin {   // (off again when the solve ends, however it ends)
+    arslam_lm *h;
+    ~DiagInLin() { h->diag_in_lin = false; }
+  } diag_in_lin_guard{this};
 
   double radius = o.initial_trust_region_radius, decrease_factor = 2.0;
   bool reuse_diag = false;
@@ -1278,10 +1293,16 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     // ---- ComputeTrustRegionStep: LM diagonal, DENSE_SCHUR solve ----
     s->num_linear_solves++;
     const bool exec_dag = has_f && opt.factor_executor == 1;
-    if (exec_dag) {
-      // flag + executor counters (+ the LM diagonal when it changed), one launch
-      const arslam::LmDiagArgs ld{reuse_diag ? 0 : n, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal,
-                                  d_diag.p, d_yF.p, nR};
+    // the LM diagonal is current: k_scale formed it for the first step and
+    // every accepted step's linearization re-forms it (k_slot_norms); a
+    // rejected or invalid step keeps it
+    arslam::ExecReset er{};
+    const bool reset_in_schur = exec_dag && has_f && nc > 0;
+    if (reset_in_schur) {
+      // flag + executor counters + the backward solve's y sentinels: in k_schur's launch
+      er = arslam::exec_reset_args(plan, d_flag.p, d_yF.p, nR);
+    } else if (exec_dag) {
+      const arslam::LmDiagArgs ld{0, d_scale.p, d_colnorm.p, o.min_lm_diagonal, o.max_lm_diagonal, d_diag.p, d_yF.p, nR};
       arslam::launch_exec_reset(plan, d_flag.p, stream, &ld);
     } else {
       if (!reuse_diag)
@@ -1295,7 +1316,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       // included).  Several: this rank's captures' share; the D_f^2 of the
       // rank's own subtree rows now, of the top rows after their exchange
       // (below).  k_schur's extra blocks clear S's tiles first.
-      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1, plan.n_tiles);
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1, plan.n_tiles,
+                           reset_in_schur ? &er : nullptr);
       const bool force_indefinite = dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull;
       const long hook_row = P.cam_row >= 0 ? P.cam_row : nR - 1;   // (a top row with several ranks)
       if (nranks > 1) arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream, 0);
