@@ -455,6 +455,21 @@ SchurSide ceres_schur_side(const arslam_soa_problem *p) {
     std::vector<int> fill(by_cap_start.begin(), by_cap_start.end() - 1);
     for (int b = 0; b < nb; ++b) by_cap[fill[p->obs_cap[b]]++] = b;
   }
+  {   // the most distinct tags of one capture and captures of one tag, constant blocks included
+      // (the local system an e-block's k_schur wave holds: kMaxSchurBlocks)
+    std::vector<int> last(nt, -1), ncap(nt, 0);
+    for (int c = 0; c < nc; ++c) {
+      int d = 0;
+      for (int q = by_cap_start[c]; q < by_cap_start[c + 1]; ++q) {
+        const int t = p->obs_tag[by_cap[q]];
+        if (last[t] == c) continue;
+        last[t] = c;
+        ++d;
+        out.max_tag_blk = std::max(out.max_tag_blk, ++ncap[t]);
+      }
+      out.max_cap_blk = std::max(out.max_cap_blk, d);
+    }
+  }
   std::vector<int> cap_adj_start(nc + 1, 0), cap_adj, tag_adj_start(nt + 1, 0), mark(nt, -1);
   cap_adj.reserve(nb);
   for (int c = 0; c < nc; ++c) {
@@ -564,7 +579,6 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
     h.maxk = std::max(h.maxk, h.cap_start[c + 1]);
     h.cap_start[c + 1] += h.cap_start[c];
   }
-  api_check(h.maxk <= kMaxObsPerCapture, ARSLAM_E_UNSUPPORTED, "more than 64 observations in one capture");
   std::vector<int> order(nb);
   {
     std::vector<int> fill(h.cap_start.begin(), h.cap_start.end() - 1);
@@ -588,8 +602,11 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
       if (u < 0) { u = (int)h.blk_tag.size() - h.cap_blk_start[c]; h.blk_tag.push_back(t); }
       h.obs_lblk[q] = u + 1;
     }
+    h.maxblk = std::max(h.maxblk, (int)h.blk_tag.size() - h.cap_blk_start[c]);
   }
   h.cap_blk_start[nc] = (int)h.blk_tag.size();
+  api_check(h.maxblk <= kMaxSchurBlocks, ARSLAM_E_UNSUPPORTED,
+            "an eliminated block (capture, or tag under tag elimination) couples more than 256 distinct blocks");
   // tag CSR over the capture-major order
   h.tag_start.assign(nt + 1, 0);
   h.tag_obs.resize(nb);

@@ -15,7 +15,11 @@
 namespace arslam {
 
 constexpr int kTileRows = 64;
-constexpr int kMaxObsPerCapture = 64;
+// the most distinct f-blocks (tags; captures under tag elimination) one
+// eliminated block may couple: its k_schur wave holds the local system in LDS
+// (lm_internal.h schur_lds_bytes; every ArUco dictionary the reference
+// supports has at most 250 ids, aruco_detector.cpp:146-150)
+constexpr int kMaxSchurBlocks = 256;
 
 // An error with the C-ABI code it maps to.
 struct ApiError : std::runtime_error {
@@ -42,6 +46,7 @@ struct HostProblem {
   int nc = 0, nt = 0, nb = 0;
   long n = 0;                       // 3 + 6 nc + 6 nt parameter slots
   int maxk = 0;                     // most observations in one capture
+  int maxblk = 0;                   // most distinct tags of one capture
   std::vector<int> cap_start;       // [nc+1] observations of capture c (capture-major)
   std::vector<int> obs_tag;         // [nb]
   std::vector<int> obs_lblk;        // [nb] 1 + local tag block of the observation in its capture
@@ -70,10 +75,12 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
 // Ceres 2.0's e-block set for DENSE_SCHUR with no user ordering
 // (ReorderProgramForSchurTypeLinearSolver -> ComputeStableSchurOrdering ->
 // StableIndependentSetOrdering), counted by kind; max_tag_obs = most
-// observations of one tag (the per-e-block limit if tags are eliminated).
+// observations of one tag; max_cap_blk / max_tag_blk = most distinct tags of
+// one capture / captures of one tag (kMaxSchurBlocks bounds the eliminated side's).
 struct SchurSide {
   int e_cap = 0, e_tag = 0, e_cam = 0;
   int max_tag_obs = 0;
+  int max_cap_blk = 0, max_tag_blk = 0;
 };
 SchurSide ceres_schur_side(const arslam_soa_problem *p);
 // the same problem with the roles of captures and tags exchanged (pointers only)

@@ -25,7 +25,26 @@ constexpr int kDagCounterExtra = 2 + kCuFlags + 1;
 constexpr int kWave = 64;
 constexpr int kTile = 64;          // reduced-system Cholesky tile
 constexpr int kRowStride = 14;     // LDS row: 13 Jacobian entries + residual
-constexpr int kMaxTagsPerCapture = 64;
+// The per-capture kernels take a capture's observations through LDS in
+// chunks of kObsChunk (8 observations = one wave's 64 residual rows), so
+// k_linearize, k_backsub and the cost take any number of observations per
+// capture.  k_schur keeps the capture's local system over its distinct tags
+// in LDS: up to kSchurMfmaBlocks tags (m + 1 <= 64 local rows) it forms it as
+// one MFMA product in the main launch; captures with more tags run in a second
+// launch sized for them, up to kMaxSchurBlocks distinct tags (its LDS at
+// schur_lds_bytes(kMaxSchurBlocks) <= 160 KiB, the CU's LDS).
+constexpr int kObsChunk = 8;
+constexpr int kSchurMfmaBlocks = 10;
+// k_schur's dynamic LDS for captures of at most nblk distinct tags (the
+// layout at the top of k_schur)
+constexpr size_t schur_lds_bytes(int nblk) {
+  // stage 6 min(m + 1, 64) | tscale 6 kObsChunk | U 36 | Ui 36 | Etr 8 | W 6 m | Ftr m (+1) | FF 28 nblk |
+  // lblk (ints, kObsChunk + 2) | ff00
+  return sizeof(double) * (6 * ((6 * nblk + 2) < 64 ? (6 * nblk + 2) : 64) + 6 * kObsChunk + 36 + 36 + 8 +
+                           7 * (6 * nblk + 1) + 2 + 28 * nblk) +
+         sizeof(int) * (kObsChunk + 2) + 2 * sizeof(double) + 64;
+}
+static_assert(schur_lds_bytes(kMaxSchurBlocks) <= 160 * 1024, "k_schur's LDS at kMaxSchurBlocks");
 
 // number of per-capture partial sums written by the per-capture kernels
 enum PartIdx {
@@ -47,6 +66,11 @@ struct DevProblem {
   long N;              // padded matrix size (multiple of kTile, > nR)
   long lda;            // leading dimension of S
   int max_obs_per_cap;
+  int max_blk_per_cap;       // most distinct tags (f-blocks) of one capture
+  // captures with more than kSchurMfmaBlocks distinct tags (k_schur's second
+  // launch); null when there are none
+  const int *big_caps = nullptr;
+  int n_big_caps = 0;
   // 1: the e-blocks (the "capture" slots, CSR cap_start) are the problem's tags
   // and the f-blocks (the "tag" slots) its captures -- ARSLAM_ELIM_TAGS: the
   // residual is then evaluated with the two pose arguments exchanged and the

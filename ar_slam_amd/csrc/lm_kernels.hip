@@ -53,17 +53,19 @@ __device__ __forceinline__ double lm_d2(const double *diag, long slot, double ra
   return d * d;
 }
 
-// Fill LDS rows [nrows][kRowStride] of capture c: 13 Jacobian entries (scaled
-// by the Jacobi scale if scale != nullptr) and the residual in column 13.
+// Fill LDS rows [nr][kRowStride] with rows [row0, row0 + nr) of capture c
+// (nrows rows in all, observations from o0): 13 Jacobian entries (scaled by
+// the Jacobi scale if scale != nullptr) and the residual in column 13.
 // With gout, the unscaled rows are also stored there column-major per capture
 // (entry (row, j) at gout + 8 o0 kRowStride + j nrows + row): the Schur and
 // back-substitution passes at the same point reload them instead of
 // re-evaluating the projection.
 __device__ void fill_rows(const DevProblem &P, const double *x, const double *scale, int c,
-                          int o0, int nrows, double *rows, double *gout = nullptr) {
+                          int o0, int row0, int nr, int nrows, double *rows, double *gout = nullptr) {
   const double *cam = x;
   const double *cap = x + slot_cap(P, c);
-  for (int row = threadIdx.x; row < nrows; row += kWave) {
+  for (int lr = threadIdx.x; lr < nr; lr += kWave) {
+    const int row = row0 + lr;
     const int q = row >> 3, corner = (row >> 1) & 3, comp = row & 1;
     const int obs = o0 + q;
     const int t = P.obs_tag[obs];
@@ -82,7 +84,7 @@ __device__ void fill_rows(const DevProblem &P, const double *x, const double *sc
         J[j + 6] = v;
       }
     }
-    double *dst = rows + (long)row * kRowStride;
+    double *dst = rows + (long)lr * kRowStride;
     if (scale) {
       const double *sc = scale + slot_cap(P, c);
       const double *st = scale + slot_tag(P, t);
@@ -106,15 +108,17 @@ __device__ void fill_rows(const DevProblem &P, const double *x, const double *sc
   }
 }
 
-// LDS rows of capture c from the copy fill_rows stored at the same point,
-// Jacobi-scaled, and each row's reduced-side product
+// LDS rows [row0, row0 + nr) of capture c (nrows rows in all) from the copy
+// fill_rows stored at the same point, Jacobi-scaled, and each row's
+// reduced-side product
 //   qv[row] = F_row . y_F = J_f y_f + J_t . y_F[tag rows]
 // formed from the row the lane just scaled (its tag row and y_F loads go out
 // beside the Jacobian loads instead of after a barrier).
 __device__ void load_rows_q(const DevProblem &P, const double *scale, const double *yF, double yf, int c, int o0,
-                            int nrows, double *rows, double *qv) {
+                            int row0, int nr, int nrows, double *rows, double *qv) {
   const double *sc = scale + slot_cap(P, c);
-  for (int row = threadIdx.x; row < nrows; row += kWave) {
+  for (int lr = threadIdx.x; lr < nr; lr += kWave) {
+    const int row = row0 + lr;
     const double *g = P.jrows + 8L * o0 * kRowStride + row;
     const int t = P.obs_tag[o0 + (row >> 3)];
     const int tr = P.tag_row[t];
@@ -125,7 +129,7 @@ __device__ void load_rows_q(const DevProblem &P, const double *scale, const doub
     double yt[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) yt[j] = tr >= 0 ? yF[tr + j] : 0.0;
-    double *dst = rows + (long)row * kRowStride;
+    double *dst = rows + (long)lr * kRowStride;
     double d[14];
     d[0] = v[0] * scale[0];
 #pragma unroll
@@ -141,7 +145,7 @@ __device__ void load_rows_q(const DevProblem &P, const double *scale, const doub
 #pragma unroll
       for (int j = 0; j < 6; ++j) q += d[7 + j] * yt[j];
     }
-    qv[row] = q;
+    qv[lr] = q;
   }
 }
 
@@ -222,53 +226,59 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
   const int c = blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
   const int nrows = 8 * k;
+  // The rows go through LDS in chunks of kObsChunk observations (one wave's
+  // 64 rows), so any number of observations per capture fits; every sum runs
+  // on over the chunks in the same order as over the whole capture at once
   double *rows = sm;
-  double *ocost = rows + (long)nrows * kRowStride;   // [k]
-  fill_rows(P, x, nullptr, c, o0, nrows, rows, P.jrows);
-  __syncthreads();
-  // Every sum below is over rows of one product of two LDS columns (ca, cb),
-  // picked per lane up front: one code path for the whole wave (a divergent
-  // if-chain ran each case's LDS round trips one after another)
-  // per observation: cost (r'r), tag gradient (6: F_t'r), tag column norms (6)
-  for (int e = lane; e < 13 * k; e += kWave) {
-    const int q = e / 13, it = e % 13;
-    const double *rq = rows + (long)q * 8 * kRowStride;
-    const int ca = it == 0 ? 13 : it <= 6 ? 6 + it : it, cb = it <= 6 ? 13 : it;
-    double s = 0.0;
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + ca] * rq[rr * kRowStride + cb];
-    if (it == 0) ocost[q] = 0.5 * s;
-    else obs_tg[12L * (o0 + q) + (it - 1)] = s;
-  }
+  double *ocost = rows + (long)8 * kObsChunk * kRowStride;   // [kObsChunk]
   // per capture: capture gradient (6: E'r), capture column norms (6), f gradient, f column norm
-  if (lane < 14) {
-    const int ca = lane < 6 ? 1 + lane : lane < 12 ? lane - 5 : 0;
-    const int cb = lane < 6 ? 13 : lane < 12 ? lane - 5 : lane == 12 ? 13 : 0;
-    double s = 0.0;
+  const int pca = lane < 6 ? 1 + lane : lane < 12 ? lane - 5 : 0;
+  const int pcb = lane < 6 ? 13 : lane < 12 ? lane - 5 : lane == 12 ? 13 : 0;
+  double ps = 0.0, act = 0.0, fix = 0.0;
+  for (int q0 = 0; q0 < k; q0 += kObsChunk) {
+    const int kc = min(kObsChunk, k - q0), nr = 8 * kc;
+    if (q0) __syncthreads();   // the previous chunk's LDS reads are done
+    fill_rows(P, x, nullptr, c, o0, 8 * q0, nr, nrows, rows, P.jrows);
+    __syncthreads();
+    // Every sum below is over rows of one product of two LDS columns (ca, cb),
+    // picked per lane up front: one code path for the whole wave (a divergent
+    // if-chain ran each case's LDS round trips one after another)
+    // per observation: cost (r'r), tag gradient (6: F_t'r), tag column norms (6)
+    for (int e = lane; e < 13 * kc; e += kWave) {
+      const int q = e / 13, it = e % 13;
+      const double *rq = rows + (long)q * 8 * kRowStride;
+      const int ca = it == 0 ? 13 : it <= 6 ? 6 + it : it, cb = it <= 6 ? 13 : it;
+      double s = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + ca] * rq[rr * kRowStride + cb];
+      if (it == 0) ocost[q] = 0.5 * s;
+      else obs_tg[12L * (o0 + q0 + q) + (it - 1)] = s;
+    }
+    if (lane < 14) {
 #pragma unroll 8
-    for (int r = 0; r < nrows; ++r) s += row_prod(rows + (long)r * kRowStride, ca, cb);
+      for (int r = 0; r < nr; ++r) ps += row_prod(rows + (long)r * kRowStride, pca, pcb);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      for (int q = 0; q < kc; ++q) {
+        if (P.obs_active[o0 + q0 + q]) act += ocost[q]; else fix += ocost[q];
+      }
+    }
+  }
+  if (lane < 14) {
     if (lane < 12) {
       const long slot = slot_cap(P, c) + (lane % 6);
-      const double v = P.slot_free[slot] ? s : 0.0;
+      const double v = P.slot_free[slot] ? ps : 0.0;
       if (lane < 6) g[slot] = v; else colnorm[slot] = v;
     } else if (lane == 12) {
-      parts[(long)P_GF * P.nc + c] = s;
+      parts[(long)P_GF * P.nc + c] = ps;
     } else {
-      parts[(long)P_CF * P.nc + c] = s;
+      parts[(long)P_CF * P.nc + c] = ps;
     }
   }
-  __syncthreads();
   if (lane == 0) {
-    double act = 0.0, fix = 0.0;
-    for (int q = 0; q < k; ++q) {
-      if (P.obs_active[o0 + q]) act += ocost[q]; else fix += ocost[q];
-    }
     parts[(long)P_COST * P.nc + c] = act;
     parts[(long)P_FIXED * P.nc + c] = fix;
-  }
-  if (k == 0 && lane < 12) {
-    const long slot = slot_cap(P, c) + (lane % 6);
-    if (lane < 6) g[slot] = 0.0; else colnorm[slot] = 0.0;
   }
 }
 
@@ -322,12 +332,15 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
 // stored for k_schur_gather.  One wave per capture.
 __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ scale,
                                                  const double *__restrict__ diag, double radius,
-                                                 double *__restrict__ zero_tiles, long n_zero, ExecReset er) {
+                                                 double *__restrict__ zero_tiles, long n_zero, ExecReset er,
+                                                 const int *__restrict__ cap_list, int skip_big) {
   if (gated(P.gate_step)) return;
   radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   SCHUR_STAMP_INIT;
-  const int c = blockIdx.x, lane = threadIdx.x;
+  // (cap_list: the second launch, over the captures with more than
+  // kSchurMfmaBlocks distinct tags; the main launch then skips them)
+  const int c = cap_list ? cap_list[blockIdx.x] : (int)blockIdx.x, lane = threadIdx.x;
   if (c >= P.nc + n_zero) {
     // the blocks past the tiles: the persistent executors' reset (ExecReset;
     // launch_exec_reset's work when the LM diagonal needs no update)
@@ -349,20 +362,22 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   if (k == 0) return;
   const int nrows = 8 * k;
   const int b0 = P.cap_blk_start[c], nblk = P.cap_blk_start[c + 1] - b0;
+  if (skip_big && nblk > kSchurMfmaBlocks) return;
   const int m = 1 + 6 * nblk;   // local f-side columns: f, then 6 per distinct tag
-  // LDS: no copy of the Jacobian rows (they go from HBM straight into the
-  // MFMA operand registers), so ~8 KB per wave: 4-5 waves per SIMD instead
-  // of the 2.75 the 13.5 KB row-staging layout allowed (latency-bound kernel)
-  double *stage = sm;                            // 6 (m + 1): one block row of the output, staged
-  double *tscale = stage + 6 * (m + 1);          // 6 k: each observation's tag column scales
-  double *U = tscale + 6 * k;                    // 36
+  // LDS (schur_lds_bytes): no copy of the Jacobian rows (they go from HBM
+  // straight into the MFMA operand registers), so ~8 KB per wave at 8 tags:
+  // 4-5 waves per SIMD instead of the 2.75 the 13.5 KB row-staging layout
+  // allowed (latency-bound kernel)
+  double *stage = sm;                            // 6 min(m + 1, 64): the MFMA product's Z operand
+  double *tscale = stage + 6 * min(m + 1, kWave);   // 6 kObsChunk: the chunk's observations' tag column scales
+  double *U = tscale + 6 * kObsChunk;            // 36
   double *Ui = U + 36;                           // 36
   double *Etr = Ui + 36;                         // 8
   double *W = Etr + 8;                           // 6*m
   double *Ftr = W + 6 * m;                       // m (+pad)
   double *FF = Ftr + m + (m & 1);                // 28 per tag block: F_u'F_u (21, packed), F_0'F_u (6), pad
-  int *lblk = (int *)(FF + 28 * nblk);           // k
-  double *ff00 = reinterpret_cast<double *>(lblk + k + (k & 1));   // F_0'F_0
+  int *lblk = (int *)(FF + 28 * nblk);           // kObsChunk: the chunk's observations' tag blocks
+  double *ff00 = reinterpret_cast<double *>(lblk + kObsChunk);     // F_0'F_0
 
   // the first eight observations' Jacobian rows (the Gram loop's operands
   // below) are loaded before the prologue's dependent loads (obs_tag -> the
@@ -376,8 +391,15 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
 #pragma unroll
     for (int st = 0; st < 2; ++st)
       jv[2 * u + st] = (valid && u < k) ? jb[(long)li * nrows + 8 * u + 4 * st + lk] : 0.0;
-  for (int q = lane; q < k; q += kWave) lblk[q] = P.obs_lblk[o0 + q];
-  for (int e = lane; e < 6 * k; e += kWave) tscale[e] = scale[slot_tag(P, P.obs_tag[o0 + e / 6]) + e % 6];
+  static_assert(kObsChunk == 8, "k_schur's operand registers hold eight observations");
+  // the tag scales and blocks of a chunk of kObsChunk observations (reloaded
+  // beside the operand registers in the Gram loop)
+  auto stage_chunk = [&](int q0) {
+    const int kc = min(kObsChunk, k - q0);
+    if (lane < kc) lblk[lane] = P.obs_lblk[o0 + q0 + lane];
+    if (lane < 6 * kc) tscale[lane] = scale[slot_tag(P, P.obs_tag[o0 + q0 + lane / 6]) + lane % 6];
+  };
+  stage_chunk(0);
   __syncthreads();
   SCHUR_STAMP(0);
   // Every product below is an entry of an observation's Gram matrix over its
@@ -434,9 +456,13 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
 #pragma unroll
           for (int st = 0; st < 2; ++st)
             jv[2 * u + st] = (valid && q + u < k) ? jb[(long)li * nrows + 8 * (q + u) + 4 * st + lk] : 0.0;
+        stage_chunk(q);   // (the previous iteration ended at a wave barrier: its reads are done)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
       dbl4v g = {0, 0, 0, 0};
-      const double s = tagcol ? tscale[6 * q + li - 7] : cs;
+      const double s = tagcol ? tscale[6 * (q & 7) + li - 7] : cs;
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         double v = 0.0;
@@ -454,7 +480,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
         g = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, g, 0, 0, 0);
       }
       tot += g;
-      const int u = lblk[q] - 1;   // the observation's tag block
+      const int u = lblk[q & 7] - 1;   // the observation's tag block
       // this lane's entries G[lk + 4 reg][li] (acc_off above): the four
       // destinations are distinct, so their reads go out together
       int di[4];
@@ -642,7 +668,10 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
     }
   } else
   for (int U = 0; U <= nblk + 1; ++U) {
+    // (more than kSchurMfmaBlocks tags: one block row U at a time, each entry
+    // stored straight to its block-packed slot)
     const int sU = schur_blk_size(U, nblk), p0U = schur_blk_start(U, nblk), ncol = p0U + sU;
+    double *dst = out + schur_block_off(U, 0, nblk);
     for (int q0 = 0; q0 < ncol; q0 += kWave) {
       const int q = q0 + lane;
       if (!one_chunk) make_z(q, z);
@@ -669,7 +698,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
             const int lo = min(i, iq), hi = max(i, iq);
             ff = FF[28 * up + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
           }
-          if (q < ncol) stage[6 * q0V + i * sV + (q - q0V)] = ff - s;
+          if (q < ncol) dst[6 * q0V + i * sV + (q - q0V)] = ff - s;
         }
       } else {   // the f row (p = 0) or the rhs row (p = m)
         const int p = p0U;
@@ -681,18 +710,9 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
         double ff = 0.0;
         if (p == m) ff = q < m ? Ftr[q] : 0.0;
         else ff = *ff00;   // p == 0: only q == 0 is stored
-        if (q < ncol) stage[q0V + (q - q0V)] = ff - s;
+        if (q < ncol) dst[q0V + (q - q0V)] = ff - s;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double *dst = out + schur_block_off(U, 0, nblk);
-    const int nreg = sU * ncol;
-    for (int e = lane; e < nreg; e += kWave) dst[e] = stage[e];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   SCHUR_STAMP(4);
 }
@@ -868,13 +888,13 @@ __global__ void k_mask_y(DevProblem P, double *__restrict__ yF, int rank) {
 __device__ __forceinline__ void capture_cost(const DevProblem &P, const double *__restrict__ x, const double *cap,
                                              int c, double *__restrict__ parts) {
   __shared__ double sq[kWave];
-  __shared__ double ocost[kMaxTagsPerCapture];
+  __shared__ double ocost[kObsChunk];   // (per 64-row chunk; summed in observation order)
   const int lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
   const int nrows = 8 * k;
   const double *cam = x;
   const AngleAxis ac = aa_prepare(cap + 3);
-  double bad = 0.0;
+  double bad = 0.0, act = 0.0, fix = 0.0;
   for (int base = 0; base < nrows; base += kWave) {
     const int row = base + lane;
     double r2 = 0.0;
@@ -896,16 +916,16 @@ __device__ __forceinline__ void capture_cost(const DevProblem &P, const double *
       double s = 0.0;
 #pragma unroll
       for (int rr = 0; rr < 8; ++rr) s += sq[8 * lane + rr];
-      ocost[base / 8 + lane] = 0.5 * s;
+      ocost[lane] = 0.5 * s;
     }
     __syncthreads();
+    if (lane == 0)
+      for (int q = base / 8; q < min(k, base / 8 + kObsChunk); ++q) {
+        if (P.obs_active[o0 + q]) act += ocost[q - base / 8]; else fix += ocost[q - base / 8];
+      }
   }
   bad = wave_max(bad);
   if (lane == 0) {
-    double act = 0.0, fix = 0.0;
-    for (int q = 0; q < k; ++q) {
-      if (P.obs_active[o0 + q]) act += ocost[q]; else fix += ocost[q];
-    }
     parts[(long)P_COST * P.nc + c] = act;
     parts[(long)P_FIXED * P.nc + c] = fix;
     parts[(long)P_CBAD * P.nc + c] = bad;
@@ -947,75 +967,83 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
     return;
   }
   const int nrows = 8 * k;
+  // the rows go through LDS in chunks of one wave's 64 rows (kObsChunk
+  // observations); each lane's running sum is carried over the chunks in row
+  // order, as over the whole capture at once
+  constexpr int kChunkRows = 8 * kObsChunk;
   double *rows = sm;
-  double *qv = rows + (long)nrows * kRowStride;   // [nrows]
-  double *U = qv + nrows;                         // 36
+  double *qv = rows + (long)kChunkRows * kRowStride;   // [kChunkRows]
+  double *U = qv + kChunkRows;                    // 36
   double *Ui = U + 36;                            // 36
   double *v = Ui + 36;                            // 8
   double *yc = v + 8;                             // 8
   const double yf = P.cam_row >= 0 ? yF[P.cam_row] : 0.0;
-  load_rows_q(P, scale, yF, yf, c, o0, nrows, rows, qv);
-  __syncthreads();
-  if (reuse_ui) {
-    // (U_c + D_c^2)^{-1} as k_schur formed it for this step
-    if (lane < 36) Ui[lane] = P.cap_ui[36L * c + lane];
-    if (lane >= 32 && lane < 38) {
-      const int a = lane - 32;
-      double s = 0.0;
-      for (int r = 0; r < nrows; ++r) {
+  // lanes 0..20: U = E'E (upper triangle entry (ua, ub)); 21..26 (32..37 with
+  // the stored inverse): v = E'(b - F z)
+  const int va = reuse_ui ? lane - 32 : lane - 21;
+  const bool do_u = !reuse_ui && lane < 21, do_v = va >= 0 && va < 6;
+  int ua = 0, ub = 0;
+  if (do_u) upper6(lane, ua, ub);
+  if (reuse_ui && lane < 36) Ui[lane] = P.cap_ui[36L * c + lane];   // (U_c + D_c^2)^{-1} as k_schur formed it
+  double s = 0.0;
+  for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
+    const int nr = min(kChunkRows, nrows - r0);
+    if (r0) __syncthreads();   // the previous chunk's LDS reads are done
+    load_rows_q(P, scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
+    __syncthreads();
+    if (do_u) {
+      for (int r = 0; r < nr; ++r) s += rows[(long)r * kRowStride + 1 + ua] * rows[(long)r * kRowStride + 1 + ub];
+    } else if (do_v) {
+      for (int r = 0; r < nr; ++r) {
         const double *rr = rows + (long)r * kRowStride;
-        s += rr[1 + a] * (rr[13] - qv[r]);   // E'(b - F z)
-      }
-      v[a] = s;
-    }
-    __syncthreads();
-    if (lane < 6) {
-      double s = 0.0;
-#pragma unroll
-      for (int b = 0; b < 6; ++b) s += Ui[6 * lane + b] * v[b];
-      yc[lane] = s;
-    }
-  } else {
-    if (lane < 27) {
-      double s = 0.0;
-      if (lane < 21) {
-        int a, b;
-        upper6(lane, a, b);
-        for (int r = 0; r < nrows; ++r) s += rows[(long)r * kRowStride + 1 + a] * rows[(long)r * kRowStride + 1 + b];
-        U[6 * a + b] = s;
-        U[6 * b + a] = s;
-      } else {
-        const int a = lane - 21;
-        for (int r = 0; r < nrows; ++r) {
-          const double *rr = rows + (long)r * kRowStride;
-          s += rr[1 + a] * (rr[13] - qv[r]);   // E'(b - F z)
-        }
-        v[a] = s;
-      }
-    }
-    __syncthreads();
-    if (lane == 0) {
-#pragma unroll
-      for (int a = 0; a < 6; ++a) U[7 * a] += lm_d2(diag, sc + a, radius);
-      inv6(U, Ui);
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        double s = 0.0;
-#pragma unroll
-        for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * v[b];
-        yc[a] = s;
+        s += rr[1 + va] * (rr[13] - qv[r]);   // E'(b - F z)
       }
     }
   }
+  if (do_u) {
+    U[6 * ua + ub] = s;
+    U[6 * ub + ua] = s;
+  } else if (do_v) {
+    v[va] = s;
+  }
   __syncthreads();
-  // model cost change share: p = Jt y (= -Jt step), sum p (r - p/2)
-  double mpart = 0.0;
-  for (int row = lane; row < nrows; row += kWave) {
-    const double *rr = rows + (long)row * kRowStride;
-    double p = qv[row];
+  if (reuse_ui) {
+    if (lane < 6) {
+      double t = 0.0;
 #pragma unroll
-    for (int a = 0; a < 6; ++a) p += rr[1 + a] * yc[a];
-    mpart += p * (rr[13] - p / 2.0);
+      for (int b = 0; b < 6; ++b) t += Ui[6 * lane + b] * v[b];
+      yc[lane] = t;
+    }
+  } else if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 6; ++a) U[7 * a] += lm_d2(diag, sc + a, radius);
+    inv6(U, Ui);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      double t = 0.0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) t += Ui[6 * a + b] * v[b];
+      yc[a] = t;
+    }
+  }
+  __syncthreads();
+  // model cost change share: p = Jt y (= -Jt step), sum p (r - p/2) (a capture
+  // of more than one chunk loads its rows again)
+  double mpart = 0.0;
+  for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
+    const int nr = min(kChunkRows, nrows - r0);
+    if (nrows > kChunkRows) {
+      __syncthreads();
+      load_rows_q(P, scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
+      __syncthreads();
+    }
+    for (int row = lane; row < nr; row += kWave) {
+      const double *rr = rows + (long)row * kRowStride;
+      double p = qv[row];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) p += rr[1 + a] * yc[a];
+      mpart += p * (rr[13] - p / 2.0);
+    }
   }
   mpart = wave_sum(mpart);
   double st = 0.0, bad = 0.0;
@@ -1290,7 +1318,7 @@ size_t lds_rows(int maxk) { return (size_t)8 * maxk * kRowStride * sizeof(double
 void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
                       double *obs_tg, double *parts, hipStream_t s) {
   if (P.nc == 0) return;
-  const size_t lds = lds_rows(P.max_obs_per_cap) + sizeof(double) * (P.max_obs_per_cap + 2);
+  const size_t lds = lds_rows(kObsChunk) + sizeof(double) * (kObsChunk + 2);
   hipLaunchKernelGGL(k_linearize, dim3(P.nc), dim3(kWave), lds, s, P, x, g, colnorm, obs_tg, parts);
 }
 
@@ -1321,13 +1349,24 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
     if (prep) launch_prep_reduced(P, diag, radius, S, s);
     return;
   }
-  const int maxk = P.max_obs_per_cap;
-  const int m = 1 + 6 * maxk;
-  const size_t lds = sizeof(double) * (6L * (m + 1) + 6L * maxk + 36 + 36 + 8 + 7L * m + 4 + 28L * maxk) +
-                     sizeof(int) * (maxk + 2) + 2 * sizeof(double) + 64;
+  // the main launch: captures of at most kSchurMfmaBlocks distinct tags (and
+  // the tile clears and the executor reset); a second one, its LDS sized for
+  // them, takes the captures with more
+  const size_t lds = schur_lds_bytes(std::min(P.max_blk_per_cap, kSchurMfmaBlocks));
   const long reset_blocks = (r.n() + kWave - 1) / kWave;
   hipLaunchKernelGGL(k_schur, dim3((unsigned)(P.nc + zero_tiles + reset_blocks)), dim3(kWave), lds, s, P, scale, diag,
-                     radius, S, zero_tiles, r);
+                     radius, S, zero_tiles, r, (const int *)nullptr, P.n_big_caps > 0 ? 1 : 0);
+  if (P.n_big_caps > 0) {
+    const size_t lds_big = schur_lds_bytes(P.max_blk_per_cap);
+    static bool attr_set = false;   // (dynamic LDS past 64 KiB)
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_schur), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)schur_lds_bytes(kMaxSchurBlocks));
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(k_schur, dim3((unsigned)P.n_big_caps), dim3(kWave), lds_big, s, P, scale, diag, radius, S, 0L,
+                       ExecReset{}, P.big_caps, 0);
+  }
   const double *pd = prep ? diag : nullptr;
   const unsigned gb = (unsigned)((P.n_items + 3) / 4) + (prep ? (unsigned)((P.N + 255) / 256) : 0u);
   if (gb) hipLaunchKernelGGL(k_schur_gather, dim3(gb), dim3(256), 0, s, P, S, pd, radius);
@@ -1351,8 +1390,7 @@ void launch_backsub(const DevProblem &P, const double *x, const double *scale, c
                     double radius, const double *yF, double *xc, double *parts, hipStream_t s,
                     bool reuse_ui, bool with_cost) {
   if (P.nc == 0) return;
-  const int maxk = P.max_obs_per_cap;
-  const size_t lds = lds_rows(maxk) + sizeof(double) * (8L * maxk + 36 + 36 + 16);
+  const size_t lds = lds_rows(kObsChunk) + sizeof(double) * (8L * kObsChunk + 36 + 36 + 16);
   hipLaunchKernelGGL(k_backsub, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts,
                      reuse_ui ? 1 : 0, with_cost ? 1 : 0);
 }

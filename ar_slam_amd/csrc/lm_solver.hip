@@ -123,12 +123,16 @@ struct UploadArena {
   size_t dev_cap = 0, host_cap = 0;
   struct Piece { void **dst; const void *src; size_t bytes, off; };
   std::vector<Piece> pieces;
+  hipEvent_t copied = nullptr;   // the last commit's transfer has read the host image
   template <class T>
   void add(T **dst, const T *src, size_t count) { pieces.push_back({reinterpret_cast<void **>(dst), src, count * sizeof(T), 0}); }
   // lay the pieces out, copy them into the host image and enqueue the one
   // transfer; the sources may go out of scope once this returns, the image
   // stays untouched until the caller's next stream sync
   void commit(hipStream_t s) {
+    // the previous transfer may still be reading the image (a load with no
+    // reduced system has no stream sync before the next upload)
+    if (copied) HIP_CHECK(hipEventSynchronize(copied));
     size_t used = 0;
     for (Piece &p : pieces) {
       p.off = used;
@@ -152,10 +156,15 @@ struct UploadArena {
       if (p.bytes) std::memcpy(host + p.off, p.src, p.bytes);
       *p.dst = dev + p.off;
     }
-    if (used) HIP_CHECK(hipMemcpyAsync(dev, host, used, hipMemcpyHostToDevice, s));
+    if (used) {
+      HIP_CHECK(hipMemcpyAsync(dev, host, used, hipMemcpyHostToDevice, s));
+      if (!copied) HIP_CHECK(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(copied, s));
+    }
     pieces.clear();
   }
   ~UploadArena() {
+    if (copied) (void)hipEventDestroy(copied);
     if (dev) (void)hipFree(dev);
     if (host) (void)hipHostFree(host);
   }
@@ -232,7 +241,8 @@ struct arslam_lm {
   UploadArena upload;
   int *u_cap_start = nullptr, *u_obs_tag = nullptr, *u_obs_lblk = nullptr, *u_cap_blk_start = nullptr,
       *u_blk_tag = nullptr, *u_tag_start = nullptr, *u_tag_obs = nullptr, *u_tag_row = nullptr,
-      *u_row_slot = nullptr, *u_fslot_row = nullptr, *u_dest_start = nullptr;
+      *u_row_slot = nullptr, *u_fslot_row = nullptr, *u_dest_start = nullptr, *u_big_caps = nullptr;
+  std::vector<int> big_caps;   // captures with more than kSchurMfmaBlocks distinct tags (k_schur's second launch)
   unsigned char *u_obs_active = nullptr, *u_slot_free = nullptr;
   double *u_corners = nullptr, *u_x0 = nullptr;
   long *u_cap_off = nullptr;
@@ -495,16 +505,20 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   const arslam::SchurSide cs = arslam::ceres_schur_side(p_in);
   ceres_e_cap = cs.e_cap;
   ceres_e_tag = cs.e_tag;
+  // (an eliminated block's local system over its distinct f-blocks lives in
+  // one wave's LDS: at most kMaxSchurBlocks of them)
+  const bool tags_fit = cs.max_tag_blk <= arslam::kMaxSchurBlocks, caps_fit = cs.max_cap_blk <= arslam::kMaxSchurBlocks;
   int side = opt.elimination;
   if (side == ARSLAM_ELIM_AUTO)
-    side = (nranks == 1 && cs.e_tag > cs.e_cap && cs.max_tag_obs <= arslam::kMaxObsPerCapture) ? ARSLAM_ELIM_TAGS
-                                                                                              : ARSLAM_ELIM_CAPTURES;
+    side = (nranks == 1 && tags_fit && (cs.e_tag > cs.e_cap || !caps_fit)) ? ARSLAM_ELIM_TAGS : ARSLAM_ELIM_CAPTURES;
   fail_if(side == ARSLAM_ELIM_TAGS && nranks > 1, ARSLAM_E_UNSUPPORTED,
           "tag elimination is single-rank only (the ranks own captures)");
   fail_if(nranks > 1 && opt.factor_executor != 1, ARSLAM_E_UNSUPPORTED,
           "several ranks need the persistent executor (factor_executor = 1)");
-  fail_if(side == ARSLAM_ELIM_TAGS && cs.max_tag_obs > arslam::kMaxObsPerCapture, ARSLAM_E_UNSUPPORTED,
-          "tag elimination: more than 64 observations of one tag");
+  fail_if(side == ARSLAM_ELIM_TAGS && !tags_fit, ARSLAM_E_UNSUPPORTED,
+          "tag elimination: a tag seen by more than 256 distinct captures");
+  fail_if(side == ARSLAM_ELIM_CAPTURES && !caps_fit, ARSLAM_E_UNSUPPORTED,
+          "capture elimination: a capture sees more than 256 distinct tags");
   if (side != elim_used) prev_tag_row.clear();   // the f-side changed: no order to reuse
   elim_used = side;
   const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
@@ -668,6 +682,10 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   upload.add(&u_tag_row, L.tag_row.data(), L.tag_row.size());
   upload.add(&u_row_slot, row_slot.data(), row_slot.size());
   upload.add(&u_fslot_row, fslot_row.data(), fslot_row.size());
+  big_caps.clear();
+  for (int c = 0; c < nc; ++c)
+    if (h.cap_blk_start[c + 1] - h.cap_blk_start[c] > arslam::kSchurMfmaBlocks) big_caps.push_back(c);
+  if (!big_caps.empty()) upload.add(&u_big_caps, big_caps.data(), big_caps.size());
   if (has_f) {
     upload.add(&u_cap_off, sg.cap_off.data(), nc + 1);
     upload.add(&u_dest_row, reinterpret_cast<const int2 *>(sg.dest_row.data()), n_dest);
@@ -707,6 +725,9 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
 
   P.nc = nc; P.nt = nt; P.nb = nb; P.n = n; P.nR = nR; P.N = N; P.lda = N; P.cam_row = L.cam_row;
   P.max_obs_per_cap = std::max(maxk, 1);
+  P.max_blk_per_cap = h.maxblk;
+  P.big_caps = big_caps.empty() ? nullptr : u_big_caps;
+  P.n_big_caps = (int)big_caps.size();
   P.swap_roles = elim_used == ARSLAM_ELIM_TAGS ? 1 : 0;
   P.nf = 3 + 6 * nt;
   P.fslot_row = u_fslot_row;
@@ -744,7 +765,8 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   const double t0 = now_s();
   if (opt.elimination == ARSLAM_ELIM_AUTO) {   // the side Ceres would eliminate may change as the graph grows
     const arslam::SchurSide cs = arslam::ceres_schur_side(p);
-    if (cs.e_tag > cs.e_cap && cs.max_tag_obs <= arslam::kMaxObsPerCapture) return false;
+    if (cs.max_tag_blk <= arslam::kMaxSchurBlocks && (cs.e_tag > cs.e_cap || cs.max_cap_blk > arslam::kMaxSchurBlocks))
+      return false;
     ceres_e_cap = cs.e_cap;
     ceres_e_tag = cs.e_tag;
   }

@@ -50,9 +50,16 @@ CONFIGS = {
     # img1-3, demo_launch.py:39-110), replicated synthetically at 1020x768 --
     # detection needs OpenCV's ArUco dictionaries, absent from the image
     "cfg1": (3, 3, 2, 16),
+    # parity graphs of larger captures (cameras 1.5-4 m from the tag plane):
+    # 8, 11, 16, 40 and 64 tags per capture, capture 0 sees 80 ("kvar"); every
+    # capture sees 24 ("k24"); a wall: 10 captures of 120 tags ("wall")
+    "kvar": (60, 20, 15, 21),
+    "k24": (80, 16, 12, 22),
+    "wall": (10, 16, 12, 23),
 }
 FULL_ROTATION = {"wide"}
-TAGS_PER_CAPTURE = {"cfg1": 4}
+TAGS_PER_CAPTURE = {"cfg1": 4, "kvar": (80, 11, 16, 40, 64, 8, 8, 11, 16, 40, 64, 8), "k24": 24, "wall": 120}
+DEPTH = {"kvar": (1.5, 4.0), "k24": (1.5, 3.0), "wall": (3.5, 4.5)}
 
 
 @dataclasses.dataclass
@@ -158,7 +165,7 @@ def _rot_axis(axis, ang):
     return rodrigues(axis * ang[:, None])
 
 
-def _sample_cameras(rng, n, x_lo, x_hi, y_lo, y_hi, max_tilt, roll_range=0.5 * np.pi):
+def _sample_cameras(rng, n, x_lo, x_hi, y_lo, y_hi, max_tilt, roll_range=0.5 * np.pi, depth=(0.6, 1.2)):
     """World->camera rotations and centres of captures looking at the tag plane.
 
     World z points from the cameras towards the tag plane (z = 0), so an
@@ -167,7 +174,7 @@ def _sample_cameras(rng, n, x_lo, x_hi, y_lo, y_hi, max_tilt, roll_range=0.5 * n
     roll_range = pi is SURVEY.md §8d's U(-pi, pi) (the "wide" parity graph).
     """
     pos = np.stack([rng.uniform(x_lo, x_hi, n), rng.uniform(y_lo, y_hi, n),
-                    -rng.uniform(0.6, 1.2, n)], 1)
+                    -rng.uniform(depth[0], depth[1], n)], 1)
     roll = rng.uniform(-roll_range, roll_range, n)
     tilt = rng.uniform(0.0, max_tilt, n)
     tilt_dir = rng.uniform(-np.pi, np.pi, n)
@@ -197,8 +204,11 @@ def _visible_nearest(R_cw, pos, corners_w, centres, cand, k):
 
 def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
                init_trans_sigma=0.02, init_rot_sigma=0.02, f_init=1.1 * F_TRUE,
-               max_tilt=np.deg2rad(20.0), name="", full_rotation=False):
-    """Generate a connected capture/tag graph with exactly ``k`` tags per capture."""
+               max_tilt=np.deg2rad(20.0), name="", full_rotation=False, depth=(0.6, 1.2)):
+    """Generate a connected capture/tag graph with exactly ``k`` tags per capture (``k`` an int,
+    or a sequence: capture c sees ``k[c % len(k)]`` tags; cameras ``depth`` metres from the plane)."""
+    ks = np.resize(np.asarray(k, np.int64), n_captures) if np.ndim(k) else np.full(n_captures, int(k))
+    kmax = int(ks.max())
     rng = np.random.Generator(np.random.PCG64(seed))
     n_tag = grid_x * grid_y
     gx, gy = np.meshgrid(np.arange(grid_x) * TAG_SPACING, np.arange(grid_y) * TAG_SPACING)
@@ -222,12 +232,12 @@ def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
     x_lo, x_hi = -0.1, (grid_x - 1) * TAG_SPACING + 0.1
     y_lo, y_hi = -0.1, (grid_y - 1) * TAG_SPACING + 0.1
     cap_true = np.zeros((n_captures, 6))
-    obs_tags = np.zeros((n_captures, k), np.int64)
+    obs_tags = [None] * n_captures
     filled = 0
-    n_cand = min(n_tag, 128)
+    n_cand = min(n_tag, max(128, 2 * kmax))
     while filled < n_captures:
         m = max(64, min(4096, (n_captures - filled) * 2))
-        R_cw, pos = _sample_cameras(rng, m, x_lo, x_hi, y_lo, y_hi, max_tilt, rot_range)
+        R_cw, pos = _sample_cameras(rng, m, x_lo, x_hi, y_lo, y_hi, max_tilt, rot_range, depth)
         # 3-D distance order == XY distance order (all tags at z = 0), so the
         # k nearest visible tags lie among the n_cand XY-nearest whenever at
         # least k of those are visible; otherwise fall back to every tag.
@@ -237,9 +247,9 @@ def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
         for i in range(m):
             if filled >= n_captures:
                 break
-            sel = _visible_nearest(R_cw[i], pos[i], corners_w, centres, cand[i], k)
+            sel = _visible_nearest(R_cw[i], pos[i], corners_w, centres, cand[i], ks[filled])
             if sel is None and n_cand < n_tag:
-                sel = _visible_nearest(R_cw[i], pos[i], corners_w, centres, np.arange(n_tag), k)
+                sel = _visible_nearest(R_cw[i], pos[i], corners_w, centres, np.arange(n_tag), ks[filled])
             if sel is None:
                 continue
             obs_tags[filled] = sel
@@ -264,8 +274,8 @@ def make_graph(n_captures, grid_x, grid_y, seed, k=8, noise_px=0.5,
     if len(roots) != 1:
         raise RuntimeError(f"synthetic graph not connected ({len(roots)} components)")
 
-    obs_cap = np.repeat(np.arange(n_captures), k).astype(np.int32)
-    obs_tag = obs_tags.ravel().astype(np.int32)
+    obs_cap = np.repeat(np.arange(n_captures), ks).astype(np.int32)
+    obs_tag = np.concatenate(obs_tags).astype(np.int32)
     corners = project_corners(camera_true, cap_true[obs_cap], tag_true[obs_tag])
     corners += rng.normal(0.0, noise_px, corners.shape)
 
@@ -355,6 +365,8 @@ def config_graph(name, **kw):
         kw.setdefault("full_rotation", True)
     if name in TAGS_PER_CAPTURE:
         kw.setdefault("k", TAGS_PER_CAPTURE[name])
+    if name in DEPTH:
+        kw.setdefault("depth", DEPTH[name])
     return make_graph(n, gx, gy, seed, name=name, **kw)
 
 

@@ -97,12 +97,36 @@ def bench_incremental(name="cfg2"):
             "final_rms_px": sums[-1]["final_rms_px"]}
 
 
+def cgroup_cpu_quota():
+    """The cgroup's CPU bandwidth limit in CPUs (cgroup v2 cpu.max "quota period", or v1's
+    cfs_quota_us / cfs_period_us), with the raw text; None where there is no limit file."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                raw = f.read().strip()
+        except OSError:
+            continue
+        if parse:
+            q, p = (parse(raw) + ["100000"])[:2]
+        else:
+            q = raw
+            try:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    p = f.read().strip()
+            except OSError:
+                p = "100000"
+        cpus = None if q in ("max", "-1") else int(q) / int(p)
+        return {"file": path, "raw": raw, "cpus": cpus}
+    return None
+
+
 def host_cpu_info():
-    """The CPUs this process may run on (the box's cpuset: one GPU's share of the node) and the
-    node's own lscpu summary."""
+    """The CPUs this process may run on (the box's cpuset: one GPU's share of the node), the
+    cgroup's CPU quota, and the node's own lscpu summary."""
     import subprocess
     info = {"nproc": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
-            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_quota": cgroup_cpu_quota()}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         keep = ("Model name", "CPU(s)", "Thread(s) per core", "Core(s) per socket", "Socket(s)")
@@ -174,15 +198,15 @@ def bench_localize(args, world, rank, side=False):
                                      "frac": achieved / HBM_PEAK_GBS,
                                      "bytes_per_query_iteration": bytes_per_qi}},
            "cpu_baseline": None}
-    if not args.no_cpu_baseline and world == 1 and not side:
+    if not args.no_cpu_baseline and world == 1:
+        # (as the side key of the default line: a 4 s sample, so the line stays within minutes)
         from oracle import oracle as O
         O.build()
-        sub = synth.make_localize_batch(n_query=4096)
         t0 = time.perf_counter()
         n = 0
-        while time.perf_counter() - t0 < 10.0:
-            O.localize_many(sub)
-            n += sub.n_query
+        while time.perf_counter() - t0 < (4.0 if side else 10.0):
+            O.localize_many(b)
+            n += b.n_query
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": n / dt, "unit": "queries/s", "cores": 1, "kind": "port",
                                "sample": f"{n} queries (the cfg5 batch repeated) through the CPU oracle's "
@@ -202,11 +226,15 @@ def load_pmc_localize():
         return None
 
 
+# the PMC pass (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md) of the commit this bench line
+# measures: each profile round writes its own directory, and this names the latest
+PMC_PROFILE = os.path.join("profiles", "r04", "pmc_hbm_bytes.json")
+
+
 def load_pmc_traffic():
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_dominant.json")
+    """Per-launch HBM bytes of the dominant kernel from the latest committed PMC pass, if any."""
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, PMC_PROFILE)) as f:
             d = json.load(f)
         return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
@@ -312,6 +340,7 @@ def main():
         roofline = {"bound": "mfma", "kernel": kname,
                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_pmc_traffic(),
+                    "traffic_source": PMC_PROFILE,
                     "avg_launch_us": avg_ms * 1e3,
                     "flops_per_launch": scalar_flops,
                     "flops_basis": "scalar Cholesky of the reduced system's real rows in the chosen order "
@@ -380,6 +409,7 @@ def main():
             print(f"bench: CPU baseline on {threads} threads", file=sys.stderr, flush=True)
             out["cpu_baseline"] = cpu_baseline(g, threads, args.config)
             out["cpu_baseline"]["host_cpu"] = host
+            out["cpu_baseline"]["cgroup_cpu_quota"] = host["cgroup_cpu_quota"]
             if args.config == "cfg3":   # plus the reference's own setting (Ceres num_threads = 1) on cfg2
                 out["cpu_baseline_cfg2_1_thread"] = cpu_baseline(synth.config_graph("cfg2"), 1, "cfg2")
         print(json.dumps(out), flush=True)

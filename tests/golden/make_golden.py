@@ -152,6 +152,11 @@ def lm_trace(name, threads=8):
     }
     with open(os.path.join(HERE, f"lm_{name}.json"), "w") as f:
         json.dump(out, f, indent=1)
+    if g.n_tag > 400:
+        # the whole final state (camera, every capture and tag pose) of the large
+        # configs: the trace above pins scalars only, this pins the parameters
+        np.savez_compressed(os.path.join(HERE, f"lm_{name}_final.npz"), camera=cam, cap=cap, tag=tag,
+                            final_cost=np.array(s["final_cost"]))
 
 
 def localize_golden(n_query=4096):

@@ -8,7 +8,8 @@ ARSLAM_ELIM_AUTO -- by running its per-e-block kernels on the role-swapped
 problem (captures become the reduced system).  Either side is the same exact
 solve of the same LM system, so both must reproduce the oracle's trace
 (capture elimination) to rounding: per-iteration cost 1e-9, final cost and
-focal 1e-8, same termination, gauge-aligned tags 1e-6 m.
+focal 1e-8, same termination, every gauge-aligned capture and tag pose
+1e-6 m / 1e-7 rad (tests/gauge.py).
 """
 import json
 import os
@@ -17,20 +18,12 @@ import numpy as np
 import pytest
 
 from ar_slam_amd import synth
+from gauge import assert_poses_match
 from oracle.schur_ordering import ceres_e_blocks
 
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-
-
-def _align_rigid(P, Q):
-    pc, qc = P.mean(0), Q.mean(0)
-    H = (P - pc).T @ (Q - qc)
-    U, _, Vt = np.linalg.svd(H)
-    d = np.sign(np.linalg.det(Vt.T @ U.T))
-    R = Vt.T @ np.diag([1, 1, d]) @ U.T
-    return (R @ (P - pc).T).T + qc
 
 
 def _compare(g, ours, ref):
@@ -42,8 +35,7 @@ def _compare(g, ours, ref):
         assert abs(a - b) <= 1e-9 * abs(b)
     assert abs(s_o["final_cost"] - s_r["final_cost"]) <= 1e-8 * s_r["final_cost"]
     assert abs(cam_o[0] - cam_r[0]) <= 1e-8 * cam_r[0]
-    used = np.unique(g.obs_tag)
-    assert np.abs(_align_rigid(tag_o[used, :3], tag_r[used, :3]) - tag_r[used, :3]).max() < 1e-6
+    assert_poses_match(cap_o, tag_o, cap_r, tag_r, tags=np.unique(g.obs_tag), caps=np.unique(g.obs_cap))
 
 
 @pytest.mark.parametrize("side", ["captures", "tags", "auto"])

@@ -7,13 +7,15 @@ atomics, so agreement is to rounding, not bitwise):
   * dense Cholesky solve: 1e-10 relative residual on SPD test matrices;
   * LM traces: per-iteration cost 1e-9 relative for the first 5 iterations,
     final cost 1e-8 relative, same termination type and rule, iteration
-    count +-1, focal 1e-8 relative, gauge-aligned tag positions 1e-6 m
-    (SURVEY.md §8c proposal).
+    count +-1, focal 1e-8 relative; every capture and tag pose after one rigid
+    gauge alignment fitted on the tags: positions 1e-6 m, rotations 1e-7 rad
+    (tests/gauge.py; SURVEY.md §8c proposal).
 """
 import numpy as np
 import pytest
 
 from ar_slam_amd import synth
+from gauge import assert_poses_match, load_cfg3_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -63,16 +65,6 @@ def test_dense_llt_reports_indefinite(lm, executor):
     assert info == 71
 
 
-def _align_rigid(P, Q):
-    """Rigid (Kabsch) alignment of point sets P -> Q; returns aligned P."""
-    pc, qc = P.mean(0), Q.mean(0)
-    H = (P - pc).T @ (Q - qc)
-    U, _, Vt = np.linalg.svd(H)
-    d = np.sign(np.linalg.det(Vt.T @ U.T))
-    R = Vt.T @ np.diag([1, 1, d]) @ U.T
-    return (R @ (P - pc).T).T + qc
-
-
 def _compare_solves(g, ours, ref, n_cost_iters=5):
     cam_o, cap_o, tag_o, s_o = ours
     cam_r, cap_r, tag_r, s_r = ref
@@ -85,9 +77,8 @@ def _compare_solves(g, ours, ref, n_cost_iters=5):
         assert abs(a - b) <= 1e-9 * abs(b), (co, cr)
     assert abs(s_o["final_cost"] - s_r["final_cost"]) <= 1e-8 * s_r["final_cost"]
     assert abs(cam_o[0] - cam_r[0]) <= 1e-8 * cam_r[0]
-    used = np.unique(g.obs_tag)
-    A = _align_rigid(tag_o[used, :3], tag_r[used, :3])
-    assert np.abs(A - tag_r[used, :3]).max() < 1e-6
+    # every capture and tag pose (positions and rotations), in the oracle's gauge
+    assert_poses_match(cap_o, tag_o, cap_r, tag_r, tags=np.unique(g.obs_tag), caps=np.unique(g.obs_cap))
 
 
 @pytest.mark.parametrize("name", ["tiny", "small", "medium", "cfg2", "wide"])
@@ -189,8 +180,7 @@ def test_appended_problem_keeps_plan_and_matches_a_fresh_load(lm, oracle):
             prob.add_residual_block(g.corners[b], camera, caps[c], tags[g.obs_tag[b]])
     start = (camera.copy(), [c.copy() for c in caps], [t.copy() for t in tags])
     s2 = prob.solve()
-    assert s2["setup_kind"] == lm.SETUP_APPEND, s2["setup_kind"]
-    assert s2["setup_time_s"] < s1["setup_time_s"]
+    assert s2["setup_kind"] == lm.SETUP_APPEND, s2["setup_kind"]   # (the plan was kept: no timing check)
     # a fresh problem of the same blocks, from the same values
     fresh = lm.Problem(elimination=lm.ELIM_CAPTURES)
     cam_f, caps_f, tags_f = start[0].copy(), [c.copy() for c in start[1]], [t.copy() for t in start[2]]
@@ -293,14 +283,11 @@ def test_sparse_plan_equals_dense_plan_on_same_order(lm):
 
 
 def test_cfg3_matches_golden_oracle_trace(lm):
-    """The headline workload (10k captures / 2k tags) against the oracle's committed trace
-    (tests/golden/lm_cfg3.json, made by make_golden.py; the oracle takes minutes here)."""
-    import json
-    import os
-    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lm_cfg3.json")) as f:
-        gold = json.load(f)
+    """The headline workload (10k captures / 2k tags) against the oracle's committed trace and
+    final state: every capture and tag pose, gauge-aligned on the tags."""
+    gold, final = load_cfg3_golden()
     g = synth.config_graph("cfg3")
-    cam, _, _, s = lm.solve_graph(g)
+    cam, cap, tag, s = lm.solve_graph(g)
     assert s["termination"] == gold["termination"] and s["rule"] == gold["rule"]
     assert abs(s["num_linear_solves"] - gold["num_linear_solves"]) <= 1
     costs = [it["cost"] for it in s["iterations"]]
@@ -311,6 +298,9 @@ def test_cfg3_matches_golden_oracle_trace(lm):
     assert abs(s["final_cost"] - gold["final_cost"]) <= 1e-8 * gold["final_cost"]
     assert abs(cam[0] - gold["final_focal"]) <= 1e-8 * gold["final_focal"]
     assert abs(s["final_rms_px"] - gold["final_rms_px"]) <= 1e-8 * gold["final_rms_px"]
+    assert abs(cam[0] - final["camera"][0]) <= 1e-8 * final["camera"][0]
+    e = assert_poses_match(cap, tag, final["cap"], final["tag"])
+    print("cfg3 pose errors vs the oracle:", e)
 
 
 @pytest.mark.parametrize("name", ["medium", "cfg2"])
@@ -359,3 +349,37 @@ def test_executor_grid_size_does_not_change_the_result(lm, monkeypatch):
         c2, p2, t2, s = lm.solve_graph(g)
         assert [i["cost"] for i in s["iterations"]] == [i["cost"] for i in ref["iterations"]], grid
         assert np.array_equal(t2, tag) and np.array_equal(p2, cap) and np.array_equal(c2, cam), grid
+
+
+@pytest.mark.parametrize("side", ["captures", "tags", "auto"])
+@pytest.mark.parametrize("name", ["kvar", "k24", "wall"])
+def test_large_captures_match_oracle(lm, oracle, name, side):
+    """Captures of 8 to 120 tags (the reference adds every block of a capture, ar_slam_util.cpp:704-731,
+    and seeds solve() from the capture with the most tags, :759-771): kvar mixes captures of 8, 11,
+    16, 40 and 64 tags with one of 80, k24 has 24 per capture, wall 10 captures of 120.  Captures of
+    more than 10 tags take k_schur's second launch (its LDS sized for them); every per-capture kernel
+    takes the rows in chunks of 8 observations.  Under tag elimination the e-blocks are tags seen by
+    up to 20 captures."""
+    g = synth.config_graph(name)
+    elim = {"auto": lm.ELIM_AUTO, "captures": lm.ELIM_CAPTURES, "tags": lm.ELIM_TAGS}[side]
+    ref = oracle.solve_graph(g)
+    ours = lm.solve_graph(g, elimination=elim)
+    _compare_solves(g, ours, ref)
+    assert ours[3]["termination"] == "CONVERGENCE"
+    if side == "captures":
+        assert ours[3]["elimination_used"] == lm.ELIM_CAPTURES
+
+
+def test_capture_of_more_than_256_tags(lm, oracle):
+    """A capture seeing more distinct tags than one wave's LDS holds (kMaxSchurBlocks = 256; every
+    ArUco dictionary the reference supports has at most 250 ids) cannot be an e-block: explicit
+    capture elimination reports ARSLAM_E_UNSUPPORTED, and ARSLAM_ELIM_AUTO eliminates the tags
+    instead and matches the oracle."""
+    g = synth.make_graph(3, 20, 15, 24, k=260, depth=(5.5, 6.5), name="wall260")
+    with pytest.raises(lm.LMError) as e:
+        lm.solve_graph(g, elimination=lm.ELIM_CAPTURES)
+    assert e.value.code == -2
+    ref = oracle.solve_graph(g)
+    ours = lm.solve_graph(g, elimination=lm.ELIM_AUTO)
+    assert ours[3]["elimination_used"] == lm.ELIM_TAGS
+    _compare_solves(g, ours, ref)
