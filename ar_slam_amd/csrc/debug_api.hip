@@ -1,5 +1,6 @@
 // debug_api.hip -- component entry points (include/arslam_lm_debug.h) that run
 // one device stage in isolation so the parity tests can pin it to the oracle.
+#include <chrono>
 #include "lm_internal.h"
 #include "arslam_lm.h"
 #include "arslam_lm_debug.h"
@@ -171,8 +172,13 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
   if (!p || !info || ordering < 0 || ordering > 2) return ARSLAM_E_INVALID_ARG;
   try {
     std::memset(info, 0, sizeof(*info));
+    static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
+    auto clk = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = prof ? clk() : 0.0;
     const arslam::HostProblem h = arslam::host_problem(p, nullptr);
+    const double t1 = prof ? clk() : 0.0;
     arslam::ReducedLayout L = arslam::reduced_layout(h, ordering, skip_zero_tiles != 0, nullptr, nullptr);
+    const double t2 = prof ? clk() : 0.0;
     info->n_reduced = L.nR;
     info->n_padded = L.N;
     info->pad_rows = L.pad_rows;
@@ -184,6 +190,7 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
     if (L.nR > 0) {
       arslam::LltPlan plan;
       arslam::llt_plan_symbolic(plan, L.T, L.N, L.pattern);
+      if (prof) std::fprintf(stderr, "arslam plan: host_problem %.3f layout %.3f plan %.3f ms\n", t1 - t0, t2 - t1, clk() - t2);
       info->n_levels = plan.nlev;
       info->n_assembled_tiles = plan.n_assembled;
       info->n_factor_tiles = plan.n_tiles;

@@ -4,6 +4,7 @@
 // 720-727, 829-836, 956-963; SetParameterBlockConstant, :965, :972) and the
 // DENSE_SCHUR split (captures eliminated, tags + camera reduced).
 #include "host_structure.h"
+#include "host_threads.h"
 
 #include <algorithm>
 #include <climits>
@@ -68,20 +69,24 @@ double height_score(long ssz, long na, long nb) {
          1e-6 * std::labs(na - nb);
 }
 
+// The two sides of a separator are dissected concurrently (host_fork2) and
+// the directions of a geometric cut searched concurrently: the per-node arrays
+// (mark, lev) are shared, but a branch only writes its own nodes and reads
+// those and its separator's (the sides are not adjacent), and the parts come
+// back in the serial order (side A's, side B's, then the separator).
 struct Dissector {
   const std::vector<std::vector<int>> &adj;
   const std::vector<double> &xyz;   // optional 3-D embedding (tag positions), 3 per node
   int leaf;
   bool fast = false;
   std::vector<int> mark, lev;
-  int next_tag = 1;
-  std::vector<std::vector<int>> parts;   // elimination order
+  std::atomic<int> next_tag{1};
 
   Dissector(const std::vector<std::vector<int>> &a, const std::vector<double> &coords, int leaf_size)
       : adj(a), xyz(coords), leaf(leaf_size), mark(a.size(), 0), lev(a.size(), -1) {}
 
-  // nodes: all with mark == tag
-  void run(std::vector<int> nodes, int tag) {
+  // nodes: all with mark == tag; their parts appended to `parts` in elimination order
+  void run(std::vector<int> nodes, int tag, std::vector<std::vector<int>> &parts) {
     if (nodes.empty()) return;
     // split into connected components
     std::vector<std::vector<int>> comps;
@@ -91,7 +96,7 @@ struct Dissector {
       comps.push_back(std::move(c));
     }
     for (int u : nodes) lev[u] = -1;
-    for (auto &c : comps) dissect(c, tag);
+    for (auto &c : comps) dissect(c, tag, parts);
   }
 
   // BFS-level separator: the level that balances the two sides
@@ -124,8 +129,9 @@ struct Dissector {
   // while keeping the remaining nodes on their sides.  On the co-visibility
   // graph (edges span up to ~3 tag spacings) it is often well below either
   // one-sided boundary.  cover[u] = 1 for the chosen nodes of comp.
+  // (loc: scratch of adj.size() entries for the local numbering)
   int konig_cover(const std::vector<int> &comp, const std::vector<int> &side, int tag,
-                  std::vector<char> &cover) {
+                  std::vector<char> &cover, std::vector<int> &loc) {
     std::vector<int> left, right;
     for (int u : comp) {
       bool bd = false;
@@ -136,12 +142,12 @@ struct Dissector {
     std::vector<int> idx(0);
     // local numbering: left 0..nl-1, right nl..
     const int nl = (int)left.size(), nr = (int)right.size();
-    for (int i = 0; i < nl; ++i) lev[left[i]] = i;
-    for (int i = 0; i < nr; ++i) lev[right[i]] = nl + i;
+    for (int i = 0; i < nl; ++i) loc[left[i]] = i;
+    for (int i = 0; i < nr; ++i) loc[right[i]] = nl + i;
     std::vector<std::vector<int>> g(nl);
     for (int i = 0; i < nl; ++i)
       for (int v : adj[left[i]])
-        if (mark[v] == tag && side[v] == 2) g[i].push_back(lev[v] - nl);
+        if (mark[v] == tag && side[v] == 2) g[i].push_back(loc[v] - nl);
     std::vector<int> mate_l(nl, -1), mate_r(nr, -1), seen(nr, -1);
     // Kuhn's augmenting paths (iterative DFS), greedy initial matching
     for (int i = 0; i < nl; ++i)
@@ -185,8 +191,6 @@ struct Dissector {
     int n = 0;
     for (int i = 0; i < nl; ++i) if (!zl[i]) { cover[left[i]] = 1; ++n; }
     for (int r = 0; r < nr; ++r) if (zr[r]) { cover[right[r]] = 1; ++n; }
-    for (int u : left) lev[u] = -1;
-    for (int u : right) lev[u] = -1;
     (void)idx;
     return n;
   }
@@ -223,18 +227,23 @@ struct Dissector {
       for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b) D[3 * a + b] -= lam * v[a] * v[b];
     }
-    std::vector<int> side(adj.size(), 0);
-    std::vector<char> cover(adj.size(), 0);
-    std::vector<std::pair<double, int>> pr(m);
-    double best_score = -1;
-    std::vector<int> best_side;
     // (fast, components of up to 512 tags: half the directions and every
     // other quantile, a quarter of the König covers -- the order was most of
     // an incremental reload; a slightly larger fill, e.g. cfg2 213 tiles
     // against 205)
     const bool big = !fast || m > 512;
     const int n_dir = big ? 6 : 3, n_q = 20, q_step = big ? 1 : 2;
-    for (int k = 0; k < n_dir; ++k) {
+    // each direction's best cut (its own scratch; large components search the
+    // directions concurrently), then the first best over the directions in
+    // order: the serial search's choice
+    std::vector<double> dir_score(n_dir, -1.0);
+    std::vector<std::vector<int>> dir_side(n_dir);
+    auto search = [&](int k) {
+      std::vector<int> side(adj.size(), 0), loc(adj.size(), -1);
+      std::vector<char> cover(adj.size(), 0);
+      std::vector<std::pair<double, int>> pr(m);
+      double &best_score = dir_score[k];
+      std::vector<int> &best_side = dir_side[k];
       // cut directions in the plane of the two principal axes
       const double ang = M_PI * k / n_dir, ca = std::cos(ang), sa = std::sin(ang);
       double dir[3];
@@ -249,7 +258,7 @@ struct Dissector {
         if (cut < 1 || cut >= m) continue;
         for (int i = 0; i < m; ++i) side[pr[i].second] = i < cut ? 1 : 2;
         for (int u : comp) cover[u] = 0;
-        const int ssz = konig_cover(comp, side, tag, cover);
+        const int ssz = konig_cover(comp, side, tag, cover, loc);
         int na = 0, nbb = 0;
         for (int u : comp)
           if (!cover[u]) (side[u] == 1 ? na : nbb)++;
@@ -264,16 +273,25 @@ struct Dissector {
           for (int i = 0; i < m; ++i) best_side[i] = cover[comp[i]] ? 0 : side[comp[i]];
         }
       }
-    }
-    for (int u : comp) side[u] = 0;
+    };
+    if (m >= 256) host_parallel_for(n_dir, search);
+    else for (int k = 0; k < n_dir; ++k) search(k);
+    double best_score = -1;
+    int best_k = -1;
+    for (int k = 0; k < n_dir; ++k)
+      if (dir_score[k] >= 0 && (best_score < 0 || dir_score[k] < best_score)) {
+        best_score = dir_score[k];
+        best_k = k;
+      }
     if (best_score < 0) return false;
+    const std::vector<int> &best_side = dir_side[best_k];
     for (int i = 0; i < m; ++i) (best_side[i] == 1 ? A : best_side[i] == 2 ? B : S).push_back(comp[i]);
     return true;
   }
 
-  void dissect(std::vector<int> &comp, int tag) {
+  void dissect(std::vector<int> &comp, int tag, std::vector<std::vector<int>> &parts) {
     if ((int)comp.size() <= leaf) {
-      leaf_part(comp, tag);
+      leaf_part(comp, tag, parts);
       return;
     }
     std::vector<int> A, B, S;
@@ -291,7 +309,7 @@ struct Dissector {
       ok = level_separator(comp, tag, A, B, S);
     }
     if (!ok) {
-      leaf_part(comp, tag);
+      leaf_part(comp, tag, parts);
       return;
     }
     absorb(A, B, S, tag);
@@ -301,8 +319,9 @@ struct Dissector {
     for (int u : A) mark[u] = ta;
     for (int u : B) mark[u] = tb;
     for (int u : S) mark[u] = ts;
-    run(A, ta);
-    run(B, tb);
+    std::vector<std::vector<int>> pb;
+    host_fork2(std::min(A.size(), B.size()) >= 128, [&] { run(A, ta, parts); }, [&] { run(B, tb, pb); });
+    for (auto &q : pb) parts.push_back(std::move(q));
     parts.push_back(S);
   }
 
@@ -331,7 +350,7 @@ struct Dissector {
     X.swap(keep);
   }
 
-  void leaf_part(std::vector<int> &comp, int tag) {
+  void leaf_part(std::vector<int> &comp, int tag, std::vector<std::vector<int>> &parts) {
     // within a leaf keep BFS order (locality)
     std::vector<int> ord = bfs(comp[0], adj, mark, tag, lev);
     for (int u : ord) lev[u] = -1;
@@ -376,8 +395,9 @@ std::vector<std::vector<int>> nd_parts(int n, const std::vector<std::vector<int>
   d.fast = fast;
   std::vector<int> all(n);
   for (int i = 0; i < n; ++i) all[i] = i;
-  d.run(all, 0);
-  return d.parts;
+  std::vector<std::vector<int>> parts;
+  d.run(all, 0, parts);
+  return parts;
 }
 
 

@@ -231,13 +231,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
   // on over the chunks in the same order as over the whole capture at once
   double *rows = sm;
   double *ocost = rows + (long)8 * kObsChunk * kRowStride;   // [kObsChunk]
-  // per capture: capture gradient (6: E'r), capture column norms (6), f gradient, f column norm
-  const int pca = lane < 6 ? 1 + lane : lane < 12 ? lane - 5 : 0;
-  const int pcb = lane < 6 ? 13 : lane < 12 ? lane - 5 : lane == 12 ? 13 : 0;
-  double ps = 0.0, act = 0.0, fix = 0.0;
-  for (int q0 = 0; q0 < k; q0 += kObsChunk) {
+  // the running sums carried over the chunks, in LDS (nothing held in
+  // registers across the projection): lanes 0..13's per-capture sums, then
+  // the active and fixed cost
+  double *accs = ocost + kObsChunk;   // [16]
+  // (one chunk -- the usual capture -- as its own specialised copy: the loop
+  // around the projection cost the single-chunk code spills)
+  auto chunk = [&](int q0) __attribute__((always_inline)) {
     const int kc = min(kObsChunk, k - q0), nr = 8 * kc;
-    if (q0) __syncthreads();   // the previous chunk's LDS reads are done
     fill_rows(P, x, nullptr, c, o0, 8 * q0, nr, nrows, rows, P.jrows);
     __syncthreads();
     // Every sum below is over rows of one product of two LDS columns (ca, cb),
@@ -254,18 +255,35 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
       if (it == 0) ocost[q] = 0.5 * s;
       else obs_tg[12L * (o0 + q0 + q) + (it - 1)] = s;
     }
+    // per capture: capture gradient (6: E'r), capture column norms (6), f gradient, f column norm
     if (lane < 14) {
+      const int ca = lane < 6 ? 1 + lane : lane < 12 ? lane - 5 : 0;
+      const int cb = lane < 6 ? 13 : lane < 12 ? lane - 5 : lane == 12 ? 13 : 0;
+      double ps = q0 ? accs[lane] : 0.0;
 #pragma unroll 8
-      for (int r = 0; r < nr; ++r) ps += row_prod(rows + (long)r * kRowStride, pca, pcb);
+      for (int r = 0; r < nr; ++r) ps += row_prod(rows + (long)r * kRowStride, ca, cb);
+      accs[lane] = ps;
     }
     __syncthreads();
     if (lane == 0) {
+      double act = q0 ? accs[14] : 0.0, fix = q0 ? accs[15] : 0.0;
       for (int q = 0; q < kc; ++q) {
         if (P.obs_active[o0 + q0 + q]) act += ocost[q]; else fix += ocost[q];
       }
+      accs[14] = act;
+      accs[15] = fix;
+    }
+  };
+  if (k <= kObsChunk) {
+    chunk(0);
+  } else {
+    for (int q0 = 0; q0 < k; q0 += kObsChunk) {
+      if (q0) __syncthreads();   // the previous chunk's LDS reads are done
+      chunk(q0);
     }
   }
   if (lane < 14) {
+    const double ps = k ? accs[lane] : 0.0;
     if (lane < 12) {
       const long slot = slot_cap(P, c) + (lane % 6);
       const double v = P.slot_free[slot] ? ps : 0.0;
@@ -277,8 +295,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
     }
   }
   if (lane == 0) {
-    parts[(long)P_COST * P.nc + c] = act;
-    parts[(long)P_FIXED * P.nc + c] = fix;
+    parts[(long)P_COST * P.nc + c] = k ? accs[14] : 0.0;
+    parts[(long)P_FIXED * P.nc + c] = k ? accs[15] : 0.0;
   }
 }
 
@@ -330,17 +348,23 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
 //   [F'F - W' U^-1 W | F'r - W' U^-1 E'r],  U = E'E + D_c^2, W = E'F,
 // over the local f-side columns (f, then 6 per distinct tag of the capture),
 // stored for k_schur_gather.  One wave per capture.
+// kBig = false: the main launch (captures of at most kSchurMfmaBlocks tags,
+// the output as one MFMA product; the blocks past the captures clear S and
+// reset the executors); true: the captures of more tags (cap_list), one block
+// row of the output at a time.  Two instances, so the main one carries no
+// registers for the other's path.
+template <bool kBig>
 __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__restrict__ scale,
                                                  const double *__restrict__ diag, double radius,
                                                  double *__restrict__ zero_tiles, long n_zero, ExecReset er,
-                                                 const int *__restrict__ cap_list, int skip_big) {
+                                                 const int *__restrict__ cap_list) {
   if (gated(P.gate_step)) return;
   radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   SCHUR_STAMP_INIT;
   // (cap_list: the second launch, over the captures with more than
   // kSchurMfmaBlocks distinct tags; the main launch then skips them)
-  const int c = cap_list ? cap_list[blockIdx.x] : (int)blockIdx.x, lane = threadIdx.x;
+  const int c = kBig ? cap_list[blockIdx.x] : (int)blockIdx.x, lane = threadIdx.x;
   if (c >= P.nc + n_zero) {
     // the blocks past the tiles: the persistent executors' reset (ExecReset;
     // launch_exec_reset's work when the LM diagonal needs no update)
@@ -362,7 +386,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   if (k == 0) return;
   const int nrows = 8 * k;
   const int b0 = P.cap_blk_start[c], nblk = P.cap_blk_start[c + 1] - b0;
-  if (skip_big && nblk > kSchurMfmaBlocks) return;
+  if (!kBig && nblk > kSchurMfmaBlocks) return;   // (the second launch's)
   const int m = 1 + 6 * nblk;   // local f-side columns: f, then 6 per distinct tag
   // LDS (schur_lds_bytes): no copy of the Jacobian rows (they go from HBM
   // straight into the MFMA operand registers), so ~8 KB per wave at 8 tags:
@@ -587,7 +611,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
       for (int a = 0; a < 6; ++a) z[a] = 0.0;
     }
   };
-  const bool one_chunk = m + 1 <= kWave;
+  const bool one_chunk = !kBig;   // (m + 1 <= kWave)
   double z[6];
   if (one_chunk) make_z(lane, z);
   if (one_chunk) {
@@ -978,33 +1002,38 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   double *v = Ui + 36;                            // 8
   double *yc = v + 8;                             // 8
   const double yf = P.cam_row >= 0 ? yF[P.cam_row] : 0.0;
-  // lanes 0..20: U = E'E (upper triangle entry (ua, ub)); 21..26 (32..37 with
-  // the stored inverse): v = E'(b - F z)
-  const int va = reuse_ui ? lane - 32 : lane - 21;
-  const bool do_u = !reuse_ui && lane < 21, do_v = va >= 0 && va < 6;
-  int ua = 0, ub = 0;
-  if (do_u) upper6(lane, ua, ub);
   if (reuse_ui && lane < 36) Ui[lane] = P.cap_ui[36L * c + lane];   // (U_c + D_c^2)^{-1} as k_schur formed it
-  double s = 0.0;
-  for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
+  // lanes 0..20: U = E'E (upper triangle entry (a, b)); 21..26 (32..37 with
+  // the stored inverse): v = E'(b - F z); each lane's sum runs on over the
+  // chunks in LDS (U, v), nothing held in registers across the row loads
+  auto chunk = [&](int r0) __attribute__((always_inline)) {
     const int nr = min(kChunkRows, nrows - r0);
-    if (r0) __syncthreads();   // the previous chunk's LDS reads are done
     load_rows_q(P, scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
     __syncthreads();
-    if (do_u) {
-      for (int r = 0; r < nr; ++r) s += rows[(long)r * kRowStride + 1 + ua] * rows[(long)r * kRowStride + 1 + ub];
-    } else if (do_v) {
+    const int va = reuse_ui ? lane - 32 : lane - 21;
+    if (!reuse_ui && lane < 21) {
+      int a, b;
+      upper6(lane, a, b);
+      double s = r0 ? U[6 * a + b] : 0.0;
+      for (int r = 0; r < nr; ++r) s += rows[(long)r * kRowStride + 1 + a] * rows[(long)r * kRowStride + 1 + b];
+      U[6 * a + b] = s;
+      U[6 * b + a] = s;
+    } else if (va >= 0 && va < 6) {
+      double s = r0 ? v[va] : 0.0;
       for (int r = 0; r < nr; ++r) {
         const double *rr = rows + (long)r * kRowStride;
         s += rr[1 + va] * (rr[13] - qv[r]);   // E'(b - F z)
       }
+      v[va] = s;
     }
-  }
-  if (do_u) {
-    U[6 * ua + ub] = s;
-    U[6 * ub + ua] = s;
-  } else if (do_v) {
-    v[va] = s;
+  };
+  if (nrows <= kChunkRows) {   // (one chunk, the usual capture: its own specialised copy)
+    chunk(0);
+  } else {
+    for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
+      if (r0) __syncthreads();   // the previous chunk's LDS reads are done
+      chunk(r0);
+    }
   }
   __syncthreads();
   if (reuse_ui) {
@@ -1030,19 +1059,24 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   // model cost change share: p = Jt y (= -Jt step), sum p (r - p/2) (a capture
   // of more than one chunk loads its rows again)
   double mpart = 0.0;
-  for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
-    const int nr = min(kChunkRows, nrows - r0);
-    if (nrows > kChunkRows) {
-      __syncthreads();
-      load_rows_q(P, scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
-      __syncthreads();
-    }
+  auto model = [&](int nr) __attribute__((always_inline)) {
     for (int row = lane; row < nr; row += kWave) {
       const double *rr = rows + (long)row * kRowStride;
       double p = qv[row];
 #pragma unroll
       for (int a = 0; a < 6; ++a) p += rr[1 + a] * yc[a];
       mpart += p * (rr[13] - p / 2.0);
+    }
+  };
+  if (nrows <= kChunkRows) {
+    model(nrows);
+  } else {
+    for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
+      const int nr = min(kChunkRows, nrows - r0);
+      __syncthreads();
+      load_rows_q(P, scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
+      __syncthreads();
+      model(nr);
     }
   }
   mpart = wave_sum(mpart);
@@ -1318,7 +1352,7 @@ size_t lds_rows(int maxk) { return (size_t)8 * maxk * kRowStride * sizeof(double
 void launch_linearize(const DevProblem &P, const double *x, double *g, double *colnorm,
                       double *obs_tg, double *parts, hipStream_t s) {
   if (P.nc == 0) return;
-  const size_t lds = lds_rows(kObsChunk) + sizeof(double) * (kObsChunk + 2);
+  const size_t lds = lds_rows(kObsChunk) + sizeof(double) * (kObsChunk + 16);
   hipLaunchKernelGGL(k_linearize, dim3(P.nc), dim3(kWave), lds, s, P, x, g, colnorm, obs_tg, parts);
 }
 
@@ -1354,18 +1388,18 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
   // them, takes the captures with more
   const size_t lds = schur_lds_bytes(std::min(P.max_blk_per_cap, kSchurMfmaBlocks));
   const long reset_blocks = (r.n() + kWave - 1) / kWave;
-  hipLaunchKernelGGL(k_schur, dim3((unsigned)(P.nc + zero_tiles + reset_blocks)), dim3(kWave), lds, s, P, scale, diag,
-                     radius, S, zero_tiles, r, (const int *)nullptr, P.n_big_caps > 0 ? 1 : 0);
+  hipLaunchKernelGGL(k_schur<false>, dim3((unsigned)(P.nc + zero_tiles + reset_blocks)), dim3(kWave), lds, s, P, scale,
+                     diag, radius, S, zero_tiles, r, (const int *)nullptr);
   if (P.n_big_caps > 0) {
     const size_t lds_big = schur_lds_bytes(P.max_blk_per_cap);
     static bool attr_set = false;   // (dynamic LDS past 64 KiB)
     if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_schur), hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_schur<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)schur_lds_bytes(kMaxSchurBlocks));
       attr_set = true;
     }
-    hipLaunchKernelGGL(k_schur, dim3((unsigned)P.n_big_caps), dim3(kWave), lds_big, s, P, scale, diag, radius, S, 0L,
-                       ExecReset{}, P.big_caps, 0);
+    hipLaunchKernelGGL(k_schur<true>, dim3((unsigned)P.n_big_caps), dim3(kWave), lds_big, s, P, scale, diag, radius, S,
+                       0L, ExecReset{}, P.big_caps);
   }
   const double *pd = prep ? diag : nullptr;
   const unsigned gb = (unsigned)((P.n_items + 3) / 4) + (prep ? (unsigned)((P.N + 255) / 256) : 0u);

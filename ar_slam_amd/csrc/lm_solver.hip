@@ -232,6 +232,7 @@ struct arslam_lm {
   std::vector<double> x0;   // initial slots
   long nb_global = 0;       // observations over all ranks
   double setup_s = 0.0;     // host structure + ordering + plan + upload of the last load (or value reload)
+  double setup_phase[5] = {0, 0, 0, 0, 0};   // the last full load's phases (summary.setup_phase_s)
   double comm_bytes = 0.0;  // bytes this rank all-reduced (RCCL or the host callback) since the count was reset
   arslam::DevProblem P{};
   hipStream_t stream = nullptr;
@@ -525,6 +526,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   const arslam_soa_problem *p = side == ARSLAM_ELIM_TAGS ? &swapped : p_in;
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
   double tp[6] = {now_s(), 0, 0, 0, 0, 0};
+  double t_host = tp[0];   // (one rank: after host_problem)
   // an incremental re-load (pointer-keyed path, same options) whose free tags
   // are unchanged keeps the previous elimination order: the ordering (nested
   // dissection) is the largest part of the host setup
@@ -589,6 +591,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
       if (sl >= 3) sl -= (int)shift;
   } else {
     h = arslam::host_problem(p, nullptr);   // validates p
+    t_host = now_s();
     // (a grown pointer-keyed problem: a fresh order takes the faster separator search)
     L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
                                can_reuse ? &prev_tag_row : nullptr, prev_order_edges, reuse_order);
@@ -640,9 +643,18 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   loaded = true;
   pk_appended_only = true;
   setup_s = now_s() - t_load;
+  // summary.setup_phase_s: structure (side rule + host problem), elimination
+  // order (reduced layout; several ranks: + the split), tile plan + task graph,
+  // gather plan + upload, the rest
+  setup_phase[0] = (tp[0] - t_load) + (t_host - tp[0]);
+  setup_phase[1] = tp[1] - t_host;
+  setup_phase[2] = tp[3] - tp[2];
+  setup_phase[3] = tp[5] - tp[4];
+  setup_phase[4] = setup_s - setup_phase[0] - setup_phase[1] - setup_phase[2] - setup_phase[3];
   if (prof)
-    std::fprintf(stderr, "arslam setup: nc %d nt %d host+layout %.3f plan %.3f gather+upload %.3f ms (order %s, %d levels, %ld tiles)\n",
-                 nc, nt, 1e3 * (tp[1] - tp[0]), 1e3 * (tp[3] - tp[2]), 1e3 * (tp[5] - tp[4]),
+    std::fprintf(stderr, "arslam setup: nc %d nt %d side %.3f host+layout %.3f stream+covis %.3f plan %.3f gather+upload %.3f total %.3f ms (order %s, %d levels, %ld tiles)\n",
+                 nc, nt, 1e3 * (tp[0] - t_load), 1e3 * (tp[1] - tp[0]), 1e3 * (tp[2] - tp[1]), 1e3 * (tp[3] - tp[2]),
+                 1e3 * (tp[5] - tp[4]), 1e3 * setup_s,
                  prev_order_nc == nc ? "fresh" : "kept", plan.nlev, (long)plan.n_tiles);
 }
 
@@ -1161,6 +1173,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->n_obs = nb;
   s->n_reduced = has_f ? (int)nR : 0;
   s->setup_time_s = setup_s;
+  for (int i = 0; i < 5; ++i) s->setup_phase_s[i] = setup_phase[i];
   s->setup_kind = setup_kind;
   x = d_xa.p;
   xc = d_xb.p;
@@ -1909,6 +1922,29 @@ int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken) {
                              h->stream));
     HIP_CHECK(hipStreamSynchronize(h->stream));
     if (broken) *broken = t;
+  });
+}
+
+int arslam_lm_debug_tag_pair_tile(arslam_lm *h, const double *tag_a, const double *tag_b, int *status) {
+  if (!h || !tag_a || !tag_b || !status) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    fail_if(!h->loaded || h->nranks > 1 || h->elim_used != ARSLAM_ELIM_CAPTURES || !h->has_f, ARSLAM_E_STATE,
+            "tag_pair_tile needs a pointer-keyed problem loaded with capture elimination on one rank");
+    const auto ia = h->tag_of.find(const_cast<double *>(tag_a)), ib = h->tag_of.find(const_cast<double *>(tag_b));
+    *status = -1;
+    if (ia == h->tag_of.end() || ib == h->tag_of.end()) return;
+    const int ra = h->lay.tag_row[ia->second], rb = h->lay.tag_row[ib->second];
+    if (ra < 0 || rb < 0) return;
+    const int T = h->lay.T;
+    int st = 2;
+    for (int x : {ra, ra + 5})
+      for (int y : {rb, rb + 5}) {
+        int ti = x / 64, tj = y / 64;
+        if (ti < tj) std::swap(ti, tj);
+        const int s = h->lay.pattern[(size_t)ti * T + tj] ? 2 : (h->plan.h_tile_id[(size_t)ti * T + tj] >= 0 ? 1 : 0);
+        st = std::min(st, s);
+      }
+    *status = st;
   });
 }
 

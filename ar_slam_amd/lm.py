@@ -46,7 +46,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_set_iteration_callback", "arslam_lm_owned_captures",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
-           "arslam_lm_debug_break_dependency",
+           "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
            "arslam_debug_rank_split", "arslam_debug_gather_extend",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
@@ -129,12 +129,14 @@ class Summary(C.Structure):
                 ("split_top_work", C.c_double), ("split_max_rank_work", C.c_double),
                 ("split_total_work", C.c_double), ("t_factor_own_ms", C.c_double),
                 ("t_factor_top_ms", C.c_double),
-                ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1)), ("lm_loop", C.c_int)]
+                ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1)), ("lm_loop", C.c_int),
+                ("setup_phase_s", C.c_double * 5)]
 
     def to_dict(self):
         its = [{f: getattr(self.iters[i], f) for f, _ in Iteration._fields_}
                for i in range(self.n_iters)]
         d = {f: getattr(self, f) for f, _ in Summary._fields_ if f not in ("iters", "termination", "rule")}
+        d["setup_phase_s"] = list(self.setup_phase_s)
         d["termination"] = TERMINATION[self.termination]
         d["rule"] = RULES[self.rule]
         d["iterations"] = its
@@ -212,6 +214,7 @@ def lib():
     L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
     L.arslam_lm_set_iteration_callback.argtypes = [C.c_void_p, ITER_CB, C.c_void_p]
     L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
+    L.arslam_lm_debug_tag_pair_tile.argtypes = [C.c_void_p, _dp, _dp, C.POINTER(C.c_int)]
     _lib = L
     return L
 
@@ -267,6 +270,18 @@ def solve_soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, c
     s = Summary()
     _check(lib().arslam_lm_solve_soa(C.byref(A.s), C.byref(make_options(**opts)), C.byref(s)))
     return A.camera, A.cap, A.tag, s.to_dict()
+
+
+def warm_up(device=0):
+    """One small solve (the 'tiny' synthetic graph) on `device`: the process's one-time runtime
+    start (the library's code objects loaded on first launch, its stream, page-locked buffers),
+    which a first load would otherwise carry.  Returns its wall time (s)."""
+    import time
+    from . import synth
+    t = time.perf_counter()
+    g = synth.config_graph("tiny")
+    ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, device=device).solve()
+    return time.perf_counter() - t
 
 
 def solve_graph(g, **opts):
@@ -428,6 +443,14 @@ class Problem(_Handle):
     def reset(self):
         _check(lib().arslam_lm_reset(self._h))
         self._keep = []
+
+    def debug_tag_pair_tile(self, tag_a, tag_b):
+        """Where the loaded problem's reduced system couples tag blocks a and b: 2 an assembled
+        tile, 1 a fill tile of the factor, 0 no tile, -1 not free tags (arslam_lm_debug.h)."""
+        st = C.c_int(0)
+        _check(lib().arslam_lm_debug_tag_pair_tile(self._h, self._block(tag_a, 6), self._block(tag_b, 6),
+                                                   C.byref(st)))
+        return st.value
 
 
 # ---- component entry points (include/arslam_lm_debug.h) ----

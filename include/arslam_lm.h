@@ -165,6 +165,10 @@ typedef struct {
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
   int lm_loop;                  /* ARSLAM_LOOP_*: which loop drove the minimizer */
+  double setup_phase_s[5];      /* the last full load (ARSLAM_SETUP_LOAD): problem structure (Ceres'
+                                   e-block rule + host problem), elimination order (reduced layout; several
+                                   ranks: + the split), tile plan + task graph, Schur gather plan + upload,
+                                   the rest (stream, co-visibility bookkeeping) */
 } arslam_lm_summary;
 
 /* summary.lm_loop: the host decided every step; the device decided, kernels

@@ -208,6 +208,69 @@ def test_appended_problem_keeps_plan_and_matches_a_fresh_load(lm, oracle):
     assert abs(so["final_cost"] - s2["final_cost"]) <= 1e-8 * so["final_cost"]
 
 
+def test_appended_coupling_in_a_fill_tile_matches_a_fresh_load(lm):
+    """An appended capture that couples two known tags never seen together, where their block of
+    the reduced system lies in a fill tile of the loaded factor (arslam_lm_debug_tag_pair_tile):
+    the plan is kept (setup_kind APPEND; try_extend marks the tile assembled), and the solve gives
+    the trace a fresh load of the grown problem gives, to 1e-9.  The appended captures are
+    synthetic: a camera 2 m above the midpoint of such a pair (0.4-0.9 m apart) sees both tags."""
+    g = synth.config_graph("cfg2")
+    camera = g.camera.copy()
+    first = 700
+    caps = [g.cap[c].copy() for c in range(first)]
+    tags = [g.tag[t].copy() for t in range(g.n_tag)]
+    prob = lm.Problem(elimination=lm.ELIM_CAPTURES)
+    seen, pairs = set(), set()
+    for c in range(first):
+        ts = sorted(set(g.obs_tag[g.obs_cap == c].tolist()))
+        seen.update(ts)
+        pairs.update((a, b) for a in ts for b in ts if a < b)
+    obs = [(g.corners[b], int(g.obs_cap[b]), int(g.obs_tag[b])) for b in range(g.n_obs) if g.obs_cap[b] < first]
+    for corners, c, t in obs:
+        prob.add_residual_block(corners, camera, caps[c], tags[t])
+    s1 = prob.solve()
+    assert s1["setup_kind"] == lm.SETUP_LOAD
+    xy = g.tag_true[:, :2]
+    hist = {}
+    picked, used = [], set()
+    for a in sorted(seen):
+        for b in sorted(seen):
+            d = np.linalg.norm(xy[a] - xy[b])
+            if a >= b or (a, b) in pairs or not 0.4 <= d <= 0.9 or a in used or b in used:
+                continue
+            st = prob.debug_tag_pair_tile(tags[a], tags[b])
+            hist[st] = hist.get(st, 0) + 1
+            if st == 1 and len(picked) < 6:
+                picked.append((a, b))
+                used.update((a, b))
+    assert picked, f"no unseen tag pair in a fill tile (pair statuses {hist})"
+    rng = np.random.default_rng(5)
+    for a, b in picked:
+        mid = 0.5 * (g.tag_true[a, :3] + g.tag_true[b, :3])
+        pose = np.array([-mid[0], -mid[1], 2.0, 0.0, 0.0, 0.0])   # centre (mid, -2 m), looking along +z
+        cor = synth.project_corners(g.camera_true, np.tile(pose, (2, 1)), g.tag_true[[a, b]])
+        assert np.abs(cor[:, 0::2]).max() < 0.5 * synth.IMG_W and np.abs(cor[:, 1::2]).max() < 0.5 * synth.IMG_H
+        cor = cor + rng.normal(0.0, 0.5, cor.shape)
+        caps.append(pose + np.concatenate([rng.normal(0, 0.02, 3), rng.normal(0, 0.02, 3)]))
+        for row, t in zip(cor, (a, b)):
+            obs.append((np.ascontiguousarray(row), len(caps) - 1, t))
+            prob.add_residual_block(obs[-1][0], camera, caps[-1], tags[t])
+    start = (camera.copy(), [c.copy() for c in caps], [t.copy() for t in tags])
+    s2 = prob.solve()
+    assert s2["setup_kind"] == lm.SETUP_APPEND, s2["setup_kind"]
+    fresh = lm.Problem(elimination=lm.ELIM_CAPTURES)
+    cam_f, caps_f, tags_f = start[0].copy(), [c.copy() for c in start[1]], [t.copy() for t in start[2]]
+    for corners, c, t in obs:
+        fresh.add_residual_block(corners, cam_f, caps_f[c], tags_f[t])
+    s3 = fresh.solve()
+    assert s3["setup_kind"] == lm.SETUP_LOAD
+    print(f"appended {len(picked)} captures coupling unseen tag pairs in fill tiles (statuses {hist})")
+    assert [i["step_is_successful"] for i in s2["iterations"]] == [i["step_is_successful"] for i in s3["iterations"]]
+    for x, y in zip(s2["iterations"], s3["iterations"]):
+        assert abs(x["cost"] - y["cost"]) <= 1e-9 * y["cost"]
+    assert abs(camera[0] - cam_f[0]) <= 1e-8 * cam_f[0]
+
+
 def test_localize_constant_map(lm, oracle):
     """localizeOne: tags and camera constant (ar_slam_util.cpp:965,972), one free capture each."""
     g = synth.config_graph("medium")
