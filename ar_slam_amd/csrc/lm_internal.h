@@ -107,6 +107,12 @@ struct DevProblem {
   // multi-rank: class of each tile column (0 this rank's subtree, 1 the
   // replicated top, 2 another rank's; LltPlan::tile_class), null on one rank
   const signed char *tile_class;
+  // several ranks: the f-side slots whose values this rank holds (its own
+  // subtree's tags; the replicated top's tags, the camera and the constant
+  // tags on rank 0 only), null on one rank: the sums over f-side slots
+  // (x^2, the f-side step) count each slot on one rank, and the final tag
+  // values are gathered from these
+  const unsigned char *f_own = nullptr;
   double *jrows;             // [8 nb kRowStride] unscaled Jacobian rows + residual at the linearization point
   double *cap_ui;            // [36 nc] (U_c + D_c^2)^{-1} of the current step (k_schur -> k_backsub)
   // device-resident LM loop (lm_device.hip; null: the host loop): a kernel of
@@ -297,7 +303,10 @@ void launch_prep_reduced(const DevProblem &P, const double *diag, double radius,
                          hipStream_t s, int which = -1);
 // multi-rank: the backward solve's y before its all-reduce: this rank's
 // subtree rows kept, the top rows kept on rank 0 only, every other row 0
-void launch_mask_y(const DevProblem &P, double *yF, int rank, hipStream_t s);
+// (keep_top: the top rows kept on every rank -- every rank holds the top's y)
+void launch_mask_y(const DevProblem &P, double *yF, int rank, hipStream_t s, bool keep_top = false);
+// dst[i] = f_own[first + i] ? src[i] : 0 for i < count (several ranks: the values this rank holds)
+void launch_own_copy(const DevProblem &P, long first, long count, const double *src, double *dst, hipStream_t s);
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
                     double radius, const double *yF, double *xc, double *parts, hipStream_t s,
                     bool reuse_ui = false, bool with_cost = false);
@@ -313,6 +322,35 @@ void launch_reduce_parts(const double *parts, int nc, const double *fparts, int 
                          double *out, hipStream_t s, const int *flag = nullptr, const int *gate = nullptr,
                          double *hout = nullptr);
 void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, hipStream_t s);
+// multi-rank exchange buffers: up to 4 segments packed at offsets off[] of one buffer
+struct PackSegs {
+  int n = 0;
+  double *p[4] = {nullptr, nullptr, nullptr, nullptr};
+  long len[4] = {0, 0, 0, 0}, off[4] = {0, 0, 0, 0};
+  void add(double *ptr, long count) {
+    p[n] = ptr;
+    len[n] = count;
+    off[n] = n ? off[n - 1] + len[n - 1] : 0;
+    ++n;
+  }
+  long total() const { return n ? off[n - 1] + len[n - 1] : 0; }
+};
+void launch_pack(const PackSegs &sg, double *buf, bool unpack, hipStream_t s);
+// all-gather of up to kAgFields scalars src[idx[f]] through one SUM all-reduce of
+// ag[nranks][kAgFields] (launch_ag_put), combined in rank order by sum, or max
+// where bit f of `max` is set (launch_ag_reduce, into dst[idx[f]])
+constexpr int kAgFields = 16;
+struct AgFields {
+  int n = 0;
+  int idx[kAgFields] = {};
+  unsigned max = 0;
+  void add(int i, bool is_max) {
+    if (is_max) max |= 1u << n;
+    idx[n++] = i;
+  }
+};
+void launch_ag_put(const double *src, const AgFields &fl, double *ag, int nranks, int rank, hipStream_t s);
+void launch_ag_reduce(const double *ag, const AgFields &fl, double *dst, int nranks, hipStream_t s);
 // The camera slots of g and colnorm from the reduced partials red (P_GF, P_CF),
 // then the norms over free parameter slots: out[0..2] = max|g|, sum g^2, sum x^2
 // over capture slots, out[3..5] the same over camera + tag slots.  out[7] is

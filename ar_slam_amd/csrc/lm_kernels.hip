@@ -898,12 +898,19 @@ __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, do
   }
 }
 
-// multi-rank y before its all-reduce (launch_mask_y)
-__global__ void k_mask_y(DevProblem P, double *__restrict__ yF, int rank) {
+// multi-rank y: the rows this rank solved (own subtree; the top rows on rank 0
+// only, or on every rank with keep_top), every other row 0
+__global__ void k_mask_y(DevProblem P, double *__restrict__ yF, int rank, int keep_top) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nR) return;
   const int c = P.tile_class[i >> 6];
-  if (!(c == 0 || (c == 1 && rank == 0))) yF[i] = 0.0;
+  if (!(c == 0 || (c == 1 && (rank == 0 || keep_top)))) yF[i] = 0.0;
+}
+
+__global__ void k_own_copy(DevProblem P, long first, long count, const double *__restrict__ src,
+                           double *__restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) dst[i] = P.f_own[first + i] ? src[i] : 0.0;
 }
 
 // Cost at x (candidate evaluation) of capture c: active / fixed cost,
@@ -1125,7 +1132,8 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
     const double xo = x[slot];
     const double xn = xo + (-yv * scale[slot]);
     xc[slot] = xn;
-    if (P.slot_free[slot]) st = (xo - xn) * (xo - xn);
+    // (several ranks: each slot's step counted on the rank holding it)
+    if (P.slot_free[slot] && (!P.f_own || P.f_own[slot])) st = (xo - xn) * (xo - xn);
     bad = isfinite(yv) ? 0.0 : 1.0;
   }
   if (i < P.nf && P.fslot_row[i] < 0) {   // f-side slot i outside the reduced system: unchanged
@@ -1228,6 +1236,7 @@ constexpr int kNormBlocks = 64;
 
 __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long cap_hi,
                                                     const unsigned char *__restrict__ free_,
+                                                    const unsigned char *__restrict__ f_own,
                                                     double *__restrict__ g, double *__restrict__ colnorm,
                                                     const double *__restrict__ red,
                                                     const double *__restrict__ x,
@@ -1260,7 +1269,7 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
     const double gv = i >= 3 ? g[i] : (i == 0 ? g0 : 0.0), xv = x[i];
     v[o] = fmax(v[o], fabs(gv));
     v[o + 1] += gv * gv;
-    v[o + 2] += xv * xv;
+    if (!f_own || f_own[i]) v[o + 2] += xv * xv;   // (several ranks: the rank holding the slot)
   }
   for (int q = 0; q < 6; ++q) rs[q][t] = v[q];
   __syncthreads();
@@ -1303,6 +1312,45 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
     if (hout) hout[t] = rs[t][0];
   }
   if (t == 0) atomicExch(done, 0);
+}
+
+// ---- multi-rank exchange buffers (lm_solver.hip) ----
+// Segments copied into (unpack = 0) or out of (1) one contiguous buffer, so
+// several arrays cross the ranks in one all-reduce.
+__global__ void k_pack(PackSegs sg, double *__restrict__ buf, int unpack) {
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int q = 0; q < sg.n; ++q) {
+    if (e < sg.len[q]) {
+      if (unpack) sg.p[q][e] = buf[sg.off[q] + e];
+      else buf[sg.off[q] + e] = sg.p[q][e];
+      return;
+    }
+    e -= sg.len[q];
+  }
+}
+
+// All-gather of a few scalars through one SUM all-reduce: this rank's fields
+// (src[idx[f]]) into row `rank` of ag[nranks][kAgFields], every other row 0
+// (x + 0 is exact, so the all-reduce hands every rank every rank's values)
+__global__ void k_ag_put(const double *__restrict__ src, AgFields fl, double *__restrict__ ag, int nranks, int rank) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nranks * kAgFields) return;
+  const int r = e / kAgFields, f = e % kAgFields;
+  ag[e] = (r == rank && f < fl.n) ? src[fl.idx[f]] : 0.0;
+}
+
+// ... and their combination in rank order (sum, or max where fl.max bit f is
+// set), the same bits on every rank, written back to dst[idx[f]]
+__global__ void k_ag_reduce(const double *__restrict__ ag, AgFields fl, double *__restrict__ dst, int nranks) {
+  const int f = threadIdx.x;
+  if (f >= fl.n) return;
+  const bool mx = (fl.max >> f) & 1u;
+  double v = ag[f];
+  for (int r = 1; r < nranks; ++r) {
+    const double w = ag[r * kAgFields + f];
+    v = mx ? fmax(v, w) : v + w;
+  }
+  dst[fl.idx[f]] = v;
 }
 
 // one thread per (observation, row): residual and 15-column Jacobian row
@@ -1415,9 +1463,14 @@ void launch_prep_reduced(const DevProblem &P, const double *diag, double radius,
                      radius, S, which);
 }
 
-void launch_mask_y(const DevProblem &P, double *yF, int rank, hipStream_t s) {
+void launch_mask_y(const DevProblem &P, double *yF, int rank, hipStream_t s, bool keep_top) {
   if (P.nR == 0) return;
-  hipLaunchKernelGGL(k_mask_y, dim3((unsigned)((P.nR + 255) / 256)), dim3(256), 0, s, P, yF, rank);
+  hipLaunchKernelGGL(k_mask_y, dim3((unsigned)((P.nR + 255) / 256)), dim3(256), 0, s, P, yF, rank, keep_top ? 1 : 0);
+}
+
+void launch_own_copy(const DevProblem &P, long first, long count, const double *src, double *dst, hipStream_t s) {
+  if (count <= 0) return;
+  hipLaunchKernelGGL(k_own_copy, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, P, first, count, src, dst);
 }
 
 void launch_backsub(const DevProblem &P, const double *x, const double *scale, const double *diag,
@@ -1450,9 +1503,25 @@ void launch_reduce_parts(const double *parts, int nc, const double *fparts, int 
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
                        double *out, hipStream_t s, double *hout, const LmDiagArgs *ld) {
   // out[0..5] results, out[7] the block count (zero between launches), out[8..] the per-block partials
-  hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, g,
+  hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, P.f_own, g,
                      colnorm, red, x, out, P.gate_lin, hout, ld ? ld->scale : nullptr, ld ? ld->dmin : 0.0,
                      ld ? ld->dmax : 0.0, ld ? ld->diag : nullptr);
+}
+
+void launch_pack(const PackSegs &sg, double *buf, bool unpack, hipStream_t s) {
+  long tot = 0;
+  for (int q = 0; q < sg.n; ++q) tot += sg.len[q];
+  if (tot == 0) return;
+  hipLaunchKernelGGL(k_pack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, sg, buf, unpack ? 1 : 0);
+}
+
+void launch_ag_put(const double *src, const AgFields &fl, double *ag, int nranks, int rank, hipStream_t s) {
+  hipLaunchKernelGGL(k_ag_put, dim3((unsigned)((nranks * kAgFields + 255) / 256)), dim3(256), 0, s, src, fl, ag,
+                     nranks, rank);
+}
+
+void launch_ag_reduce(const double *ag, const AgFields &fl, double *dst, int nranks, hipStream_t s) {
+  hipLaunchKernelGGL(k_ag_reduce, dim3(1), dim3(kAgFields), 0, s, ag, fl, dst, nranks);
 }
 
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,

@@ -234,6 +234,7 @@ struct arslam_lm {
   double setup_s = 0.0;     // host structure + ordering + plan + upload of the last load (or value reload)
   double setup_phase[5] = {0, 0, 0, 0, 0};   // the last full load's phases (summary.setup_phase_s)
   double comm_bytes = 0.0;  // bytes this rank all-reduced (RCCL or the host callback) since the count was reset
+  long comm_calls = 0;      // ... and the collectives that carried them
   arslam::DevProblem P{};
   hipStream_t stream = nullptr;
   int device = 0;
@@ -243,6 +244,8 @@ struct arslam_lm {
   int *u_cap_start = nullptr, *u_obs_tag = nullptr, *u_obs_lblk = nullptr, *u_cap_blk_start = nullptr,
       *u_blk_tag = nullptr, *u_tag_start = nullptr, *u_tag_obs = nullptr, *u_tag_row = nullptr,
       *u_row_slot = nullptr, *u_fslot_row = nullptr, *u_dest_start = nullptr, *u_big_caps = nullptr;
+  unsigned char *u_f_own = nullptr;
+  std::vector<unsigned char> f_own;   // several ranks: DevProblem::f_own
   std::vector<int> big_caps;   // captures with more than kSchurMfmaBlocks distinct tags (k_schur's second launch)
   unsigned char *u_obs_active = nullptr, *u_slot_free = nullptr;
   double *u_corners = nullptr, *u_x0 = nullptr;
@@ -353,6 +356,7 @@ struct arslam_lm {
     if (nranks <= 1 || count == 0) return;
     const size_t bytes = count * (dtype == ARSLAM_DT_F64 ? sizeof(double) : 1);
     comm_bytes += (double)bytes;
+    ++comm_calls;
     if (comm_cb) {
       comm_stage.resize(bytes);
       HIP_CHECK(hipMemcpyAsync(comm_stage.data(), buf, bytes, hipMemcpyDeviceToHost, stream));
@@ -459,6 +463,15 @@ struct arslam_lm {
   // linearize split at the host read: enqueue (results copied to h_lin), collect after a sync
   void linearize_launch();
   void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
+  // several ranks: the linearization's capture-slot norms are combined at the
+  // next exchange of scalars (the step's, or exchange_norms before a sync
+  // that has no step), not by collectives of their own
+  bool norms_pending = false;
+  DevBuf<double> d_lx, d_ag;   // the linearization's packed exchange; the all-gathered scalars
+  void exchange_scalars(arslam::AgFields fl);   // (+ the pending norms), into d_red
+  void exchange_norms() {
+    if (norms_pending) exchange_scalars(arslam::AgFields{});
+  }
   PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [16..21] slot norms
   // host LM loop: the Jacobi scale of this solve is set, so each later
   // linearization also forms the LM diagonal (k_slot_norms) and the step's
@@ -694,6 +707,21 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   upload.add(&u_tag_row, L.tag_row.data(), L.tag_row.size());
   upload.add(&u_row_slot, row_slot.data(), row_slot.size());
   upload.add(&u_fslot_row, fslot_row.data(), fslot_row.size());
+  // several ranks: the f-side slots this rank holds -- its own subtree's tag
+  // rows; the top's rows, the camera and the tags outside the reduced system
+  // on rank 0 (every rank holds the top, one counts it); capture slots all
+  f_own.clear();
+  if (nranks > 1) {
+    f_own.assign(n, 0);
+    for (long sl = 3; sl < 3 + 6L * nc; ++sl) f_own[sl] = 1;
+    for (long sl = 0; sl < n; ++sl) {
+      if (sl >= 3 && sl < 3 + 6L * nc) continue;
+      const int r = fslot_row[sl < 3 ? sl : sl - 6L * nc];
+      const int cls = r >= 0 && has_f ? plan.h_col_class[r / arslam::kTile] : 1;
+      f_own[sl] = cls == 0 || (cls == 1 && rank == 0);
+    }
+    upload.add(&u_f_own, f_own.data(), f_own.size());
+  }
   big_caps.clear();
   for (int c = 0; c < nc; ++c)
     if (h.cap_blk_start[c + 1] - h.cap_blk_start[c] > arslam::kSchurMfmaBlocks) big_caps.push_back(c);
@@ -750,6 +778,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.tag_row = u_tag_row; P.row_slot = u_row_slot;
   P.tile_id = plan.tile_id; P.T = plan.T;
   P.tile_class = nranks > 1 && has_f ? plan.tile_class : nullptr;
+  P.f_own = nranks > 1 ? u_f_own : nullptr;
   P.cap_off = u_cap_off; P.slab = d_slab.p; P.dest_row = u_dest_row; P.dest_start = u_dest_start;
   P.contrib = u_contrib; P.n_dest = n_dest; P.jrows = d_jrows.p; P.cap_ui = d_cap_ui.p;
   P.gather_items = u_gather_items; P.gather_splits = u_gather_splits; P.gather_part = d_gather_part.p;
@@ -790,9 +819,11 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   if ((lay.cam_row >= 0) != (h.slot_free[0] != 0)) return false;
   for (int t = 0; t < nt; ++t)
     if ((lay.tag_row[t] >= 0) != (h.slot_free[3 + 6L * h.nc + 6L * t] != 0)) return false;
-  // every capture's tiles pairwise in the loaded factor's tiles
+  // every capture's tiles pairwise in the loaded factor's tiles (lay.pattern
+  // is the filled pattern: llt_plan_build fills it in place; a new coupling in
+  // a fill tile is gathered into it -- k_schur clears every tile of the factor
+  // each step and the updates read-modify-write their targets)
   const int T = lay.T;
-  std::vector<std::pair<int, int>> grown;   // fill tiles that become assembled
   std::vector<int> ts;
   // (only the captures of the appended residual blocks: the others' tile
   // pairs were in the pattern already)
@@ -817,17 +848,13 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
     }
     for (size_t a = 0; a < ts.size(); ++a)
       for (size_t b = 0; b < ts.size(); ++b)
-        if (ts[a] >= ts[b] && !lay.pattern[(size_t)ts[a] * T + ts[b]]) {
-          if (plan.h_tile_id[(size_t)ts[a] * T + ts[b]] < 0) return false;
-          grown.emplace_back(ts[a], ts[b]);
-        }
+        if (ts[a] >= ts[b] && plan.h_tile_id[(size_t)ts[a] * T + ts[b]] < 0) return false;
   }
   // the co-visibility graph the order was computed for, outgrown by a tenth: reload with a fresh order
   for (int c = 0; c < h.nc; ++c)
     if (touched[c]) covis_add(h, lay, c);
   if (covis_nt && 10 * covis_edges > 11 * prev_order_edges) return false;
   if (4L * h.nc > 5L * prev_order_nc) return false;   // (a quarter more captures: a fresh order)
-  for (const auto &g : grown) lay.pattern[(size_t)g.first * T + g.second] = 1;
   // only new captures got residual blocks: their contributions extend the gather plan
   const int extend_from = first_touched >= nc ? nc : -1;
   // the tag slots move with the capture count
@@ -886,22 +913,51 @@ void arslam_lm::linearize_launch() {
   arslam::launch_lin_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream,
                             direct ? h_lin.p : nullptr);
   if (nranks > 1) {
+    // the tag slots' gradient and column norms and the cost / f partials, one
+    // packed all-reduce (the tags' observations span the ranks)
     const long t0 = 3 + 6L * nc;
-    allreduce(d_g.p + t0, n - t0, ARSLAM_OP_SUM);
-    allreduce(d_colnorm.p + t0, n - t0, ARSLAM_OP_SUM);
-    allreduce(d_red.p, 4, ARSLAM_OP_SUM);   // cost, fixed, g_f, col_f
+    arslam::PackSegs sg;
+    sg.add(d_g.p + t0, n - t0);
+    sg.add(d_colnorm.p + t0, n - t0);
+    sg.add(d_red.p, 4);   // cost, fixed, g_f, col_f
+    d_lx.alloc(sg.total());
+    arslam::launch_pack(sg, d_lx.p, false, stream);
+    allreduce(d_lx.p, sg.total(), ARSLAM_OP_SUM);
+    arslam::launch_pack(sg, d_lx.p, true, stream);
   }
   const arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, opt.min_lm_diagonal, opt.max_lm_diagonal, d_diag.p};
   arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, direct ? h_lin.p + 16 : nullptr,
                             diag_in_lin ? &ld : nullptr);
-  if (nranks > 1) {
-    // capture slots are disjoint across ranks, tag/camera slots replicated:
-    // norms[0..2] cover captures (max, sum, sum), norms[3..5] the rest
-    allreduce(d_norms_p, 1, ARSLAM_OP_MAX);
-    allreduce(d_norms_p + 1, 2, ARSLAM_OP_SUM);
-  }
+  // several ranks: capture slots are disjoint across ranks, tag/camera slots
+  // replicated: norms[0..2] (captures: max, sum, sum) are combined with the
+  // next exchange of scalars (norms_pending), norms[3..5] are final
+  norms_pending = nranks > 1;
   timers[PH_LIN].stop(stream);
-  if (!direct) HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 22 * sizeof(double), hipMemcpyDeviceToHost, stream));
+  if (!direct) HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, stream));
+}
+
+// Several ranks: the scalars of fl (indices into d_red) and, if a
+// linearization's norms are pending, its capture-slot norms, all-gathered in
+// one SUM all-reduce and combined in rank order (k_ag_put / k_ag_reduce: the
+// same bits on every rank); the norms then go to h_lin like the rest of it.
+void arslam_lm::exchange_scalars(arslam::AgFields fl) {
+  const bool with_norms = norms_pending;
+  if (with_norms) {
+    const int nb0 = (int)(d_norms_p - d_red.p);
+    fl.add(nb0, true);        // max |g| over capture slots
+    fl.add(nb0 + 1, false);   // sum g^2
+    fl.add(nb0 + 2, false);   // sum x^2
+    fl.add(nb0 + 5, false);   // sum x^2 over the camera and tag slots this rank holds
+  }
+  if (fl.n == 0) return;
+  d_ag.alloc((size_t)nranks * arslam::kAgFields);
+  arslam::launch_ag_put(d_red.p, fl, d_ag.p, nranks, rank, stream);
+  allreduce(d_ag.p, (size_t)nranks * arslam::kAgFields, ARSLAM_OP_SUM);
+  arslam::launch_ag_reduce(d_ag.p, fl, d_red.p, nranks, stream);
+  if (with_norms) {
+    HIP_CHECK(hipMemcpyAsync(h_lin.p + 16, d_norms_p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    norms_pending = false;
+  }
 }
 
 // (after a stream sync that covers linearize_launch)
@@ -921,6 +977,7 @@ void arslam_lm::linearize_collect(double *x_cost, double *fixed_cost, double *gm
 void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
                           double *xnorm) {
   linearize_launch();
+  exchange_norms();
   spin_sync();
   linearize_collect(x_cost, fixed_cost, gmax, gnorm, xnorm);
 }
@@ -928,6 +985,15 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
 void arslam_lm::write_back(const double *d_src) {
   h_x.alloc(n);   // page-locked: the parameter download is one DMA, no staging
   HIP_CHECK(hipMemcpyAsync(h_x.p, d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+  if (nranks > 1 && nt) {
+    // each tag from the rank holding it (the others hold stale values of
+    // other ranks' subtree tags): one all-reduce of the held values, zeros elsewhere
+    const long t0 = 3 + 6L * nc;
+    d_lx.alloc(n - t0);
+    arslam::launch_own_copy(P, t0, n - t0, d_src + t0, d_lx.p, stream);
+    allreduce(d_lx.p, n - t0, ARSLAM_OP_SUM);
+    HIP_CHECK(hipMemcpyAsync(h_x.p + t0, d_lx.p, (n - t0) * sizeof(double), hipMemcpyDeviceToHost, stream));
+  }
   spin_sync();
   const double *h = h_x.p;
   std::memcpy(soa.camera, h, 3 * sizeof(double));
@@ -1170,6 +1236,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   dom_ms = dom_flops = 0.0;
   dom_launches = 0;
   comm_bytes = 0.0;
+  comm_calls = 0;
+  norms_pending = false;
   s->n_obs = nb;
   s->n_reduced = has_f ? (int)nR : 0;
   s->setup_time_s = setup_s;
@@ -1199,6 +1267,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     HIP_CHECK(hipStreamSynchronize(stream));
     any_iter_cb = m > 0.0;
     comm_bytes = 0.0;   // (the per-step exchange count starts here)
+    comm_calls = 0;
   }
 
   // ---- iteration 0 ----
@@ -1321,7 +1390,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     // the stop rules that do not read the pending linearization: decided now
     // (after reading it), so no step is computed past them
     const bool stop_rule = it.iteration >= o.max_num_iterations || radius <= o.min_trust_region_radius;
-    if (lin_pending && stop_rule) spin_sync();
+    if (lin_pending && stop_rule) {
+      exchange_norms();
+      spin_sync();
+    }
     const bool deferred = lin_pending && !stop_rule;
     if (!deferred && finalize()) break;
 
@@ -1439,11 +1511,13 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       else
         arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
       if (nranks > 1) {
-        // y of the top columns (identical on every rank) and of each rank's
-        // own subtrees: summed with every other row zero -- exact, so every
-        // rank holds the same full y and the f-side update stays replicated
-        arslam::launch_mask_y(P, d_yF.p, rank, stream);
-        allreduce(d_yF.p, nR, ARSLAM_OP_SUM);
+        // y of the top columns (identical on every rank) and of this rank's
+        // own subtrees; no exchange: a rank's captures see only those tags
+        // (a capture's tags lie on one root path of the elimination tree), so
+        // each rank updates the tags it holds and keeps the others' stale,
+        // and the sums over f-side slots count each slot on its holder
+        // (DevProblem::f_own); the final tags are gathered in write_back
+        arslam::launch_mask_y(P, d_yF.p, rank, stream, true);
       }
       timers[PH_SOLVE].stop(stream);
     }
@@ -1459,12 +1533,17 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p, nullptr,
                                 nranks == 1 ? h_step.p : nullptr);
     if (nranks > 1) {
-      // model change, capture step^2, candidate cost, fixed; flags by max
-      allreduce(d_red.p + arslam::P_COST, 2, ARSLAM_OP_SUM);
-      allreduce(d_red.p + arslam::P_MODEL, 2, ARSLAM_OP_SUM);
-      allreduce(d_red.p + arslam::P_YBAD, 2, ARSLAM_OP_MAX);
-      // f-side non-finite step, indefinite, executor fault: every rank takes the same branch
-      allreduce(d_red.p + arslam::NPART + 1, 3, ARSLAM_OP_MAX);
+      // candidate cost, fixed, model change, capture step^2 by sum; the
+      // non-finite flags, the f-side non-finite step, indefinite and executor
+      // fault by max (every rank takes the same branch); with a pending
+      // linearization's norms: one collective
+      arslam::AgFields fl;
+      for (int f : {(int)arslam::P_COST, (int)arslam::P_FIXED, (int)arslam::P_MODEL, (int)arslam::P_STEP2,
+                    (int)arslam::NPART})   // (NPART: the f-side step^2, of the slots this rank holds)
+        fl.add(f, false);
+      for (int f : {(int)arslam::P_YBAD, (int)arslam::P_CBAD, arslam::NPART + 1, arslam::NPART + 2, arslam::NPART + 3})
+        fl.add(f, true);
+      exchange_scalars(fl);
     }
     timers[PH_COST].stop(stream);
     if (nranks > 1)
@@ -1565,6 +1644,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->factor_update_flops = plan.total_upd_flops;
   s->factor_scalar_flops = scalar_flops;
   s->comm_bytes = comm_bytes;
+  s->comm_calls = comm_calls;
   s->elimination_used = elim_used;
   s->ceres_e_captures = ceres_e_cap;
   s->ceres_e_tags = ceres_e_tag;
@@ -1941,8 +2021,9 @@ int arslam_lm_debug_tag_pair_tile(arslam_lm *h, const double *tag_a, const doubl
       for (int y : {rb, rb + 5}) {
         int ti = x / 64, tj = y / 64;
         if (ti < tj) std::swap(ti, tj);
-        const int s = h->lay.pattern[(size_t)ti * T + tj] ? 2 : (h->plan.h_tile_id[(size_t)ti * T + tj] >= 0 ? 1 : 0);
-        st = std::min(st, s);
+        // (the tiles assembled at the load are numbered first, the fill after them)
+        const int id = h->plan.h_tile_id[(size_t)ti * T + tj];
+        st = std::min(st, id < 0 ? 0 : (id < h->plan.n_assembled ? 2 : 1));
       }
     *status = st;
   });

@@ -130,7 +130,7 @@ class Summary(C.Structure):
                 ("split_total_work", C.c_double), ("t_factor_own_ms", C.c_double),
                 ("t_factor_top_ms", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1)), ("lm_loop", C.c_int),
-                ("setup_phase_s", C.c_double * 5)]
+                ("setup_phase_s", C.c_double * 5), ("comm_calls", C.c_long)]
 
     def to_dict(self):
         its = [{f: getattr(self.iters[i], f) for f, _ in Iteration._fields_}

@@ -169,6 +169,7 @@ typedef struct {
                                    e-block rule + host problem), elimination order (reduced layout; several
                                    ranks: + the split), tile plan + task graph, Schur gather plan + upload,
                                    the rest (stream, co-visibility bookkeeping) */
+  long comm_calls;              /* multi-rank: collectives this rank made during the solve */
 } arslam_lm_summary;
 
 /* summary.lm_loop: the host decided every step; the device decided, kernels

@@ -78,10 +78,11 @@ int arslam_lm_debug_force_indefinite(arslam_lm *h, unsigned long long step_mask)
 int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken);
 /* tag_pair_tile: on a pointer-keyed problem loaded with capture elimination
  * on one rank, where the coupling of tag blocks a and b (and the pair's
- * mirror) falls in the reduced system: *status = 2 an assembled tile, 1 a
- * fill tile of the loaded factor (an appended capture coupling them keeps the
- * plan, its tile becomes assembled), 0 no tile of the factor (an append
- * reloads), -1 a or b is not a free tag of the loaded problem. */
+ * mirror) falls in the reduced system: *status = 2 a tile assembled at the
+ * load, 1 a fill tile of the loaded factor (an appended capture coupling them
+ * keeps the plan: the gather writes into the fill tile), 0 no tile of the
+ * factor (an append reloads), -1 a or b is not a free tag of the loaded
+ * problem. */
 int arslam_lm_debug_tag_pair_tile(arslam_lm *h, const double *tag_a, const double *tag_b, int *status);
 
 /* Ceres 2.0's DENSE_SCHUR e-block set for problem p (ComputeStableSchurOrdering,

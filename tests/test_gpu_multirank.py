@@ -56,9 +56,10 @@ def _worker(rank, world, port, name, q, abort_rank=-1):
         q.put((rank, rp.camera.copy(), (own, rp.cap[own].copy()), rp.tag.copy(),
                [it["cost"] for it in s["iterations"]], s["termination"], s["rule"], s["final_cost"],
                s["comm_bytes"] / max(s["num_linear_solves"], 1),
-               [it["trust_region_radius"] for it in s["iterations"]], s["n_top_tiles"]))
+               [it["trust_region_radius"] for it in s["iterations"]], s["n_top_tiles"],
+               (s["comm_calls"], s["num_linear_solves"])))
     except Exception as e:   # noqa: BLE001 -- surface the failure in the parent
-        q.put((rank, None, None, None, None, repr(e), None, None, None, None, None))
+        q.put((rank, None, None, None, None, repr(e), None, None, None, None, None, None))
     finally:
         dist.destroy_process_group()
 
@@ -141,7 +142,7 @@ def test_sharded_cfg3_matches_golden_trace(world):
         gold = json.load(f)
     res = _run_ranks("cfg3", world)
     _same_on_every_rank(res)
-    rank, cam, _, tag, costs, term, rule, final, xbytes, radius, top_tiles = res[0]
+    rank, cam, _, tag, costs, term, rule, final, xbytes, radius, top_tiles, (calls, solves) = res[0]
     assert (term, rule) == (gold["termination"], gold["rule"])
     assert abs(len(costs) - len(gold["cost"])) <= 1
     for a, b in list(zip(costs, gold["cost"]))[:5]:
@@ -156,6 +157,10 @@ def test_sharded_cfg3_matches_golden_trace(world):
     print(f"cfg3 x{world} ranks: {xbytes / 1e6:.1f} MB all-reduced per rank per LM iteration "
           f"({top_tiles} top tiles)")
     assert xbytes <= top_tiles * 32768 + 1e6 and xbytes < 20e6
+    # collectives per LM iteration: the top tiles, the step's scalars (+ the pending linearization's
+    # norms), the accepted step's linearization; + iteration 0's two and the final tag gather
+    print(f"cfg3 x{world}: {calls} collectives over {solves} LM iterations")
+    assert calls <= 3 * solves + 3, (calls, solves)
 
 
 def test_iteration_callback_decision_is_agreed_across_ranks():

@@ -213,7 +213,8 @@ def test_appended_coupling_in_a_fill_tile_matches_a_fresh_load(lm):
     the reduced system lies in a fill tile of the loaded factor (arslam_lm_debug_tag_pair_tile):
     the plan is kept (setup_kind APPEND; try_extend marks the tile assembled), and the solve gives
     the trace a fresh load of the grown problem gives, to 1e-9.  The appended captures are
-    synthetic: a camera 2 m above the midpoint of such a pair (0.4-0.9 m apart) sees both tags."""
+    synthetic: a camera above the midpoint of such a pair (the nearest such pairs, up to 3 m apart;
+    2-3.3 m up) sees both tags."""
     g = synth.config_graph("cfg2")
     camera = g.camera.copy()
     first = 700
@@ -231,23 +232,27 @@ def test_appended_coupling_in_a_fill_tile_matches_a_fresh_load(lm):
     s1 = prob.solve()
     assert s1["setup_kind"] == lm.SETUP_LOAD
     xy = g.tag_true[:, :2]
-    hist = {}
-    picked, used = [], set()
+    hist, fill = {}, []
     for a in sorted(seen):
         for b in sorted(seen):
             d = np.linalg.norm(xy[a] - xy[b])
-            if a >= b or (a, b) in pairs or not 0.4 <= d <= 0.9 or a in used or b in used:
+            if a >= b or (a, b) in pairs or d > 3.0:
                 continue
             st = prob.debug_tag_pair_tile(tags[a], tags[b])
             hist[st] = hist.get(st, 0) + 1
-            if st == 1 and len(picked) < 6:
-                picked.append((a, b))
-                used.update((a, b))
+            if st == 1:
+                fill.append((d, a, b))
+    picked, used = [], set()
+    for d, a, b in sorted(fill):
+        if a not in used and b not in used and len(picked) < 6:
+            picked.append((a, b))
+            used.update((a, b))
     assert picked, f"no unseen tag pair in a fill tile (pair statuses {hist})"
     rng = np.random.default_rng(5)
     for a, b in picked:
         mid = 0.5 * (g.tag_true[a, :3] + g.tag_true[b, :3])
-        pose = np.array([-mid[0], -mid[1], 2.0, 0.0, 0.0, 0.0])   # centre (mid, -2 m), looking along +z
+        h = max(2.0, 1.1 * np.linalg.norm(xy[a] - xy[b]))
+        pose = np.array([-mid[0], -mid[1], h, 0.0, 0.0, 0.0])   # centre (mid, -h), looking along +z
         cor = synth.project_corners(g.camera_true, np.tile(pose, (2, 1)), g.tag_true[[a, b]])
         assert np.abs(cor[:, 0::2]).max() < 0.5 * synth.IMG_W and np.abs(cor[:, 1::2]).max() < 0.5 * synth.IMG_H
         cor = cor + rng.normal(0.0, 0.5, cor.shape)
