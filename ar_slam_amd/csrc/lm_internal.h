@@ -12,6 +12,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <stdexcept>
 #include <vector>
 
 #include "host_structure.h"
@@ -336,15 +337,20 @@ struct PackSegs {
   long total() const { return n ? off[n - 1] + len[n - 1] : 0; }
 };
 void launch_pack(const PackSegs &sg, double *buf, bool unpack, hipStream_t s);
+// tail[0..m) = g[idx], tail[m..2m) = cn[idx], tail[2m..2m+2) = red[P_GF], red[P_CF] (unpack: the reverse):
+// the top tags' linearization sums riding in front of the top tiles' all-reduce
+void launch_top_tail(const int *idx, int m, double *g, double *cn, double *red, double *tail, bool unpack,
+                     hipStream_t s);
 // all-gather of up to kAgFields scalars src[idx[f]] through one SUM all-reduce of
 // ag[nranks][kAgFields] (launch_ag_put), combined in rank order by sum, or max
 // where bit f of `max` is set (launch_ag_reduce, into dst[idx[f]])
-constexpr int kAgFields = 16;
+constexpr int kAgFields = 32;
 struct AgFields {
   int n = 0;
   int idx[kAgFields] = {};
   unsigned max = 0;
   void add(int i, bool is_max) {
+    if (n >= kAgFields) throw std::logic_error("AgFields: more than kAgFields scalars");
     if (is_max) max |= 1u << n;
     idx[n++] = i;
   }

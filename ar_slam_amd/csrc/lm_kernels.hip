@@ -1264,12 +1264,13 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
       const double cn = i >= 3 ? colnorm[i] : (i == 0 ? cn0 : 0.0);
       diag[i] = fmin(fmax(scale[i] * scale[i] * cn, dmin), dmax);
     }
-    if (!free_[i]) continue;
+    // (several ranks: each slot counted on the rank holding it, DevProblem::f_own)
+    if (!free_[i] || (f_own && !f_own[i])) continue;
     const int o = (i >= cap_lo && i < cap_hi) ? 0 : 3;
     const double gv = i >= 3 ? g[i] : (i == 0 ? g0 : 0.0), xv = x[i];
     v[o] = fmax(v[o], fabs(gv));
     v[o + 1] += gv * gv;
-    if (!f_own || f_own[i]) v[o + 2] += xv * xv;   // (several ranks: the rank holding the slot)
+    v[o + 2] += xv * xv;
   }
   for (int q = 0; q < 6; ++q) rs[q][t] = v[q];
   __syncthreads();
@@ -1327,6 +1328,15 @@ __global__ void k_pack(PackSegs sg, double *__restrict__ buf, int unpack) {
     }
     e -= sg.len[q];
   }
+}
+
+__global__ void k_top_tail(const int *__restrict__ idx, int m, double *__restrict__ g, double *__restrict__ cn,
+                           double *__restrict__ red, double *__restrict__ tail, int unpack) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2 * m + 2) return;
+  double *v = e < m ? g + idx[e] : e < 2 * m ? cn + idx[e - m] : red + (e == 2 * m ? P_GF : P_CF);
+  if (unpack) *v = tail[e];
+  else tail[e] = *v;
 }
 
 // All-gather of a few scalars through one SUM all-reduce: this rank's fields
@@ -1513,6 +1523,12 @@ void launch_pack(const PackSegs &sg, double *buf, bool unpack, hipStream_t s) {
   for (int q = 0; q < sg.n; ++q) tot += sg.len[q];
   if (tot == 0) return;
   hipLaunchKernelGGL(k_pack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, sg, buf, unpack ? 1 : 0);
+}
+
+void launch_top_tail(const int *idx, int m, double *g, double *cn, double *red, double *tail, bool unpack,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_top_tail, dim3((unsigned)((2 * m + 2 + 255) / 256)), dim3(256), 0, s, idx, m, g, cn, red, tail,
+                     unpack ? 1 : 0);
 }
 
 void launch_ag_put(const double *src, const AgFields &fl, double *ag, int nranks, int rank, hipStream_t s) {

@@ -255,6 +255,14 @@ struct arslam_lm {
   arslam::SchurContrib *u_contrib = nullptr;
   DevBuf<double> d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_S, d_z, d_yF;
+  // the reduced system's tiles: Sp = d_S.p + s_pre.  Several ranks: the top
+  // tags' linearization sums (top_tail_len doubles) ride in the prefix, just in
+  // front of the top tiles, in the step's one bulk all-reduce
+  double *Sp = nullptr;
+  long s_pre = 0;
+  int *u_top_slots = nullptr;
+  int n_top_slots = 0;
+  long top_tail_len() const { return 2L * n_top_slots + 2; }
   double *d_norms_p = nullptr;   // inside d_red
   DevBuf<int> d_flag;
   DevBuf<double> d_slab, d_jrows, d_cap_ui;
@@ -463,11 +471,17 @@ struct arslam_lm {
   // linearize split at the host read: enqueue (results copied to h_lin), collect after a sync
   void linearize_launch();
   void linearize_collect(double *x_cost, double *fixed_cost, double *gmax, double *gnorm, double *xnorm);
-  // several ranks: the linearization's capture-slot norms are combined at the
-  // next exchange of scalars (the step's, or exchange_norms before a sync
-  // that has no step), not by collectives of their own
-  bool norms_pending = false;
-  DevBuf<double> d_lx, d_ag;   // the linearization's packed exchange; the all-gathered scalars
+  // Several ranks: a linearization's sums over the ranks are not collectives
+  // of their own.  Its tag slots' gradient and column norms and the camera's
+  // f partials (lin_xpending) ride in front of the top tiles in the next
+  // step's bulk all-reduce (or one packed all-reduce, complete_pending_lin,
+  // when no step follows); its cost and norms (norms_pending) ride with the
+  // step's scalars (exchange_scalars; exchange_norms when no step follows).
+  bool lin_xpending = false, norms_pending = false;
+  DevBuf<double> d_lx, d_ag;   // the packed exchange; the all-gathered scalars
+  static constexpr int kLinSave = 16 + 8 + 6 * 64;   // d_red[kLinSave..+1]: the linearization's cost, fixed
+  void complete_pending_lin();
+  void lin_norms();   // k_slot_norms once the linearization's sums are final
   void exchange_scalars(arslam::AgFields fl);   // (+ the pending norms), into d_red
   void exchange_norms() {
     if (norms_pending) exchange_scalars(arslam::AgFields{});
@@ -707,6 +721,15 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   upload.add(&u_tag_row, L.tag_row.data(), L.tag_row.size());
   upload.add(&u_row_slot, row_slot.data(), row_slot.size());
   upload.add(&u_fslot_row, fslot_row.data(), fslot_row.size());
+  // several ranks: the top tags' slots (their linearization sums ride with the top tiles)
+  std::vector<int> top_slots;
+  if (nranks > 1 && has_f)
+    for (long sl = 3 + 6L * nc; sl < n; ++sl) {
+      const int r = fslot_row[sl - 6L * nc];
+      if (r >= 0 && plan.h_col_class[r / arslam::kTile] == 1) top_slots.push_back((int)sl);
+    }
+  n_top_slots = (int)top_slots.size();
+  if (n_top_slots) upload.add(&u_top_slots, top_slots.data(), top_slots.size());
   // several ranks: the f-side slots this rank holds -- its own subtree's tag
   // rows; the top's rows, the camera and the tags outside the reduced system
   // on rank 0 (every rank holds the top, one counts it); capture slots all
@@ -746,18 +769,22 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   // stays zero when there are no reduced rows (k_update_f is then not launched)
   if (!has_f) HIP_CHECK(hipMemsetAsync(d_fparts.p, 0, d_fparts.n * sizeof(double), stream));
   const double *red_prev = d_red.p;
-  d_red.alloc(16 + 8 + 6 * 64);   // LM scalars | slot norms: results, block count, k_slot_norms block partials
+  d_red.alloc(kLinSave + 8);   // LM scalars | slot norms: results, block count, k_slot_norms block partials | saved
   d_norms_p = d_red.p + 16;       // (one D2H carries both after a linearization)
   if (d_red.p != red_prev) HIP_CHECK(hipMemsetAsync(d_norms_p + 7, 0, sizeof(double), stream));   // the count
   d_flag.alloc(1);
   if (has_f) {
     d_slab.alloc(std::max(sg.cap_off[nc], 1L));
     d_gather_part.alloc(36L * std::max(sg.n_pslots, 1));
-    d_S.alloc((size_t)plan.n_tiles * 4096);   // (cleared by k_schur's extra blocks every step)
+    s_pre = nranks > 1 ? round_up(top_tail_len(), 512) : 0;
+    d_S.alloc((size_t)s_pre + (size_t)plan.n_tiles * 4096);   // (cleared by k_schur's extra blocks every step)
+    Sp = d_S.p + s_pre;
     d_z.alloc(N);
     d_yF.alloc(N);
   } else {
     d_S.release();
+    Sp = nullptr;
+    s_pre = 0;
     d_z.release();
     d_yF.alloc(1);
   }
@@ -913,27 +940,43 @@ void arslam_lm::linearize_launch() {
   arslam::launch_lin_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream,
                             direct ? h_lin.p : nullptr);
   if (nranks > 1) {
-    // the tag slots' gradient and column norms and the cost / f partials, one
-    // packed all-reduce (the tags' observations span the ranks)
-    const long t0 = 3 + 6L * nc;
-    arslam::PackSegs sg;
-    sg.add(d_g.p + t0, n - t0);
-    sg.add(d_colnorm.p + t0, n - t0);
-    sg.add(d_red.p, 4);   // cost, fixed, g_f, col_f
-    d_lx.alloc(sg.total());
-    arslam::launch_pack(sg, d_lx.p, false, stream);
-    allreduce(d_lx.p, sg.total(), ARSLAM_OP_SUM);
-    arslam::launch_pack(sg, d_lx.p, true, stream);
+    // this rank's partial sums: the cost and fixed cost saved (the step's
+    // reductions reuse d_red) for the scalar exchange; the LM diagonal from
+    // them is final for the capture slots and this rank's own subtree tags
+    // (all their observations are this rank's), the rest follows the
+    // exchange (lin_norms)
+    HIP_CHECK(hipMemcpyAsync(d_red.p + kLinSave, d_red.p, 2 * sizeof(double), hipMemcpyDeviceToDevice, stream));
+    lin_xpending = true;
   }
   const arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, opt.min_lm_diagonal, opt.max_lm_diagonal, d_diag.p};
   arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, direct ? h_lin.p + 16 : nullptr,
                             diag_in_lin ? &ld : nullptr);
-  // several ranks: capture slots are disjoint across ranks, tag/camera slots
-  // replicated: norms[0..2] (captures: max, sum, sum) are combined with the
-  // next exchange of scalars (norms_pending), norms[3..5] are final
-  norms_pending = nranks > 1;
   timers[PH_LIN].stop(stream);
-  if (!direct) HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, stream));
+}
+
+// (several ranks) the norms and the LM diagonal again, from the exchanged sums
+void arslam_lm::lin_norms() {
+  const arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, opt.min_lm_diagonal, opt.max_lm_diagonal, d_diag.p};
+  arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, nullptr, diag_in_lin ? &ld : nullptr);
+  lin_xpending = false;
+  norms_pending = true;   // capture slots and the held f-side slots: combined with the next scalars
+}
+
+// (several ranks) a pending linearization's sums when no step carries them:
+// every tag slot's gradient and column norm and the camera's f partials, one
+// packed all-reduce (the tags' observations span the ranks)
+void arslam_lm::complete_pending_lin() {
+  if (!lin_xpending) return;
+  const long t0 = 3 + 6L * nc;
+  arslam::PackSegs sg;
+  sg.add(d_g.p + t0, n - t0);
+  sg.add(d_colnorm.p + t0, n - t0);
+  sg.add(d_red.p + arslam::P_GF, 2);   // g_f, col_f
+  d_lx.alloc(sg.total());
+  arslam::launch_pack(sg, d_lx.p, false, stream);
+  allreduce(d_lx.p, sg.total(), ARSLAM_OP_SUM);
+  arslam::launch_pack(sg, d_lx.p, true, stream);
+  lin_norms();
 }
 
 // Several ranks: the scalars of fl (indices into d_red) and, if a
@@ -943,11 +986,11 @@ void arslam_lm::linearize_launch() {
 void arslam_lm::exchange_scalars(arslam::AgFields fl) {
   const bool with_norms = norms_pending;
   if (with_norms) {
+    // the norms over the slots each rank holds (captures; its f-side slots)
     const int nb0 = (int)(d_norms_p - d_red.p);
-    fl.add(nb0, true);        // max |g| over capture slots
-    fl.add(nb0 + 1, false);   // sum g^2
-    fl.add(nb0 + 2, false);   // sum x^2
-    fl.add(nb0 + 5, false);   // sum x^2 over the camera and tag slots this rank holds
+    for (int q = 0; q < 6; ++q) fl.add(nb0 + q, q % 3 == 0);   // max |g|, sum g^2, sum x^2 (captures, then f-side)
+    fl.add(kLinSave, false);       // the linearization's cost
+    fl.add(kLinSave + 1, false);   // ... and fixed cost
   }
   if (fl.n == 0) return;
   d_ag.alloc((size_t)nranks * arslam::kAgFields);
@@ -956,6 +999,7 @@ void arslam_lm::exchange_scalars(arslam::AgFields fl) {
   arslam::launch_ag_reduce(d_ag.p, fl, d_red.p, nranks, stream);
   if (with_norms) {
     HIP_CHECK(hipMemcpyAsync(h_lin.p + 16, d_norms_p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p + kLinSave, 2 * sizeof(double), hipMemcpyDeviceToHost, stream));
     norms_pending = false;
   }
 }
@@ -977,6 +1021,7 @@ void arslam_lm::linearize_collect(double *x_cost, double *fixed_cost, double *gm
 void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, double *gnorm,
                           double *xnorm) {
   linearize_launch();
+  complete_pending_lin();
   exchange_norms();
   spin_sync();
   linearize_collect(x_cost, fixed_cost, gmax, gnorm, xnorm);
@@ -1089,16 +1134,16 @@ void arslam_lm::enqueue_iteration(int part, const arslam::LmDevConsts &c) {
     ld.gate = &st->gate_step;
     ld.keep_diag = &st->keep_diag;
     arslam::launch_exec_reset(plan, d_flag.p, stream, &ld);
-    arslam::launch_schur(Q, x, d_scale.p, d_diag.p, 0.0, d_S.p, stream, true, plan.n_tiles);
+    arslam::launch_schur(Q, x, d_scale.p, d_diag.p, 0.0, Sp, stream, true, plan.n_tiles);
     if (dbg_indefinite_mask)   // (test hook)
-      arslam::launch_lm_debug_indefinite(Q, d_S.p, P.cam_row >= 0 ? P.cam_row : nR - 1, dbg_indefinite_mask, st,
+      arslam::launch_lm_debug_indefinite(Q, Sp, P.cam_row >= 0 ? P.cam_row : nR - 1, dbg_indefinite_mask, st,
                                          stream);
   }
   if (part < 0 || part == 1)
-    arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, -1,
+    arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, -1,
                                  &st->gate_step);
   if (part < 0 || part == 2) {
-    arslam::launch_dense_back_solve_dag(plan, d_S.p, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false,
+    arslam::launch_dense_back_solve_dag(plan, Sp, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false,
                                         &st->gate_step);
     arslam::launch_update_f(Q, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
     arslam::launch_backsub(Q, x, d_scale.p, d_diag.p, 0.0, d_yF.p, xc, d_parts.p, stream, has_f, true);
@@ -1237,7 +1282,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   dom_launches = 0;
   comm_bytes = 0.0;
   comm_calls = 0;
-  norms_pending = false;
+  norms_pending = lin_xpending = false;
   s->n_obs = nb;
   s->n_reduced = has_f ? (int)nR : 0;
   s->setup_time_s = setup_s;
@@ -1391,6 +1436,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     // (after reading it), so no step is computed past them
     const bool stop_rule = it.iteration >= o.max_num_iterations || radius <= o.min_trust_region_radius;
     if (lin_pending && stop_rule) {
+      complete_pending_lin();
       exchange_norms();
       spin_sync();
     }
@@ -1417,18 +1463,22 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       HIP_CHECK(hipMemsetAsync(d_flag.p, 0, sizeof(int), stream));
     }
     reuse_diag = true;
+    // several ranks: a pending linearization's sums ride with the top tiles
+    // (below), unless this step has no such exchange
+    static const bool dag_trace_env = std::getenv("ARSLAM_DAG_TRACE") != nullptr;
+    if (lin_xpending && !(has_f && opt.factor_executor == 1 && !dag_trace_env)) complete_pending_lin();
     if (has_f) {
       timers[PH_SCHUR].start(stream);
       // one rank: the gather writes the final S (D_f^2 and the padding rows
       // included).  Several: this rank's captures' share; the D_f^2 of the
       // rank's own subtree rows now, of the top rows after their exchange
       // (below).  k_schur's extra blocks clear S's tiles first.
-      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, d_S.p, stream, nranks == 1, plan.n_tiles,
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, Sp, stream, nranks == 1, plan.n_tiles,
                            reset_in_schur ? &er : nullptr);
       const bool force_indefinite = dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull;
       const long hook_row = P.cam_row >= 0 ? P.cam_row : nR - 1;   // (a top row with several ranks)
-      if (nranks > 1) arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream, 0);
-      else if (force_indefinite) arslam::debug_set_reduced_diag(P, d_S.p, hook_row, -1.0, stream);   // test hook
+      if (nranks > 1) arslam::launch_prep_reduced(P, d_diag.p, radius, Sp, stream, 0);
+      else if (force_indefinite) arslam::debug_set_reduced_diag(P, Sp, hook_row, -1.0, stream);   // test hook
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
       timing_begin();
@@ -1441,7 +1491,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           DevBuf<unsigned long long> tr;
           tr.alloc(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemsetAsync(tr.p, 0, tr.n * 8, stream));
-          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, tr.p, false);
+          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, tr.p, false);
           std::vector<unsigned long long> h(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemcpyAsync(h.data(), tr.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
           HIP_CHECK(hipStreamSynchronize(stream));
@@ -1464,16 +1514,24 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           // are summed over the ranks -- the step's one bulk exchange -- and
           // every rank factors the top columns (phase 1) on identical inputs
           timers[PH_FAC0].start(stream);
-          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 0);
+          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 0);
           timers[PH_FAC0].stop(stream);
-          allreduce(d_S.p, (size_t)plan.n_top_tiles * 4096, ARSLAM_OP_SUM);
-          arslam::launch_prep_reduced(P, d_diag.p, radius, d_S.p, stream, 1);
-          if (force_indefinite) arslam::debug_set_reduced_diag(P, d_S.p, hook_row, -1.0, stream);   // test hook
+          // (+ a pending linearization's top-tag sums and camera partials, in
+          // front of the top tiles: the step's collectives stay two)
+          const long tail = lin_xpending ? top_tail_len() : 0;
+          if (tail) arslam::launch_top_tail(u_top_slots, n_top_slots, d_g.p, d_colnorm.p, d_red.p, Sp - tail, false, stream);
+          allreduce(Sp - tail, (size_t)tail + (size_t)plan.n_top_tiles * 4096, ARSLAM_OP_SUM);
+          if (tail) {
+            arslam::launch_top_tail(u_top_slots, n_top_slots, d_g.p, d_colnorm.p, d_red.p, Sp - tail, true, stream);
+            lin_norms();   // the LM diagonal of the top rows, then their D^2
+          }
+          arslam::launch_prep_reduced(P, d_diag.p, radius, Sp, stream, 1);
+          if (force_indefinite) arslam::debug_set_reduced_diag(P, Sp, hook_row, -1.0, stream);   // test hook
           timers[PH_FAC1].start(stream);
-          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 1);
+          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 1);
           timers[PH_FAC1].stop(stream);
         } else {
-          arslam::launch_dense_llt_dag(plan, d_S.p, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false);
+          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false);
         }
         if (rec) {
           HIP_CHECK(hipEventRecord(upd_timing.ev[2 * upd_timing.used + 1], stream));
@@ -1483,7 +1541,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
         static const char *hash_path = std::getenv("ARSLAM_FACTOR_HASH");   // debug: per-tile factor hashes
         if (hash_path) {
           std::vector<unsigned long long> h((size_t)plan.n_tiles * 4096), ld((size_t)plan.T * 4096);
-          HIP_CHECK(hipMemcpyAsync(h.data(), d_S.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
+          HIP_CHECK(hipMemcpyAsync(h.data(), Sp, h.size() * 8, hipMemcpyDeviceToHost, stream));
           HIP_CHECK(hipMemcpyAsync(ld.data(), plan.ldiag, ld.size() * 8, hipMemcpyDeviceToHost, stream));
           HIP_CHECK(hipStreamSynchronize(stream));
           if (FILE *f = std::fopen(hash_path, "ab")) {
@@ -1502,14 +1560,14 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           }
         }
       } else {
-        arslam::launch_dense_llt(plan, d_S.p, d_flag.p, stream, opt.kernel_timing ? &upd_timing : nullptr);
+        arslam::launch_dense_llt(plan, Sp, d_flag.p, stream, opt.kernel_timing ? &upd_timing : nullptr);
       }
       timers[PH_CHOL].stop(stream);
       timers[PH_SOLVE].start(stream);
       if (opt.factor_executor == 1)
-        arslam::launch_dense_back_solve_dag(plan, d_S.p, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false);
+        arslam::launch_dense_back_solve_dag(plan, Sp, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false);
       else
-        arslam::launch_dense_back_solve(plan, d_S.p, nR, d_z.p, d_yF.p, d_flag.p, stream);
+        arslam::launch_dense_back_solve(plan, Sp, nR, d_z.p, d_yF.p, d_flag.p, stream);
       if (nranks > 1) {
         // y of the top columns (identical on every rank) and of this rank's
         // own subtrees; no exchange: a rank's captures see only those tags
