@@ -699,39 +699,76 @@ RankSplit rank_split(const HostProblem &h, const ReducedLayout &L, int nranks) {
   for (int k = 0; k < T; ++k)
     if (parent[k] >= 0) W[parent[k]] += W[k];
   for (int k = 0; k < T; ++k) out.total_work += w[k];
-  // Grow the replicated top from the root: repeatedly move the heaviest
-  // subtree root of the frontier into the top (descending a separator chain
-  // one column at a time), and keep the state with the least estimated
-  // makespan = top work (every rank) + the heaviest rank's subtrees (largest
-  // first onto the least loaded rank).
+  // the observations of the captures each column would own (the lowest
+  // column of their tags), summed over subtrees, and the tiles of each column
+  std::vector<double> cob(T, 0.0), tiles(T, 0.0);
+  double top_only_obs = 0.0;
+  for (int c = 0; c < nc; ++c) {
+    int low = T;
+    for (int a = h.cap_blk_start[c]; a < h.cap_blk_start[c + 1]; ++a) {
+      const int r0 = L.tag_row[h.blk_tag[a]];
+      if (r0 >= 0) low = std::min(low, r0 / kTileRows);
+    }
+    const double ob = h.cap_start[c + 1] - h.cap_start[c];
+    if (low < T) cob[low] += ob; else top_only_obs += ob;
+  }
+  std::vector<double> COB = cob;
+  for (int k = 0; k < T; ++k)
+    if (parent[k] >= 0) COB[parent[k]] += COB[k];
+  for (int k = 0; k < T; ++k)
+    for (int i = k; i < T; ++i) tiles[k] += P[(long)i * T + k] || i == k;
+  // Grow the replicated top from the root (the heaviest subtree root of the
+  // frontier into the top, descending a separator chain one column at a
+  // time) and deal the frontier's subtrees to A <= nranks active ranks; keep
+  // the (top, A) of the least modelled step time.  The factorization is
+  // bound by its critical chain (every leaf-to-root path crosses the top),
+  // about the same for every split, so the model is
+  // what the split changes: the per-capture work of the busiest rank (its
+  // observations, ~3 ns each on cfg3: linearize, Schur, back-substitution)
+  // and the exchange of the top tiles (2 (N-1)/N x 32 KB per tile at
+  // ~100 GB/s).  A deeper split adds top tiles faster than it removes
+  // per-capture work, so ranks may stay idle in phase 0 (they then own only
+  // captures that see top tags alone).  Tile-task work breaks ties.
+  const double kObsUs = 0.003, kTileUs = 32768.0 / 100e3 * 2.0 * (nranks - 1) / nranks;
+  int active_forced = 0;
+  if (const char *e = std::getenv("ARSLAM_SPLIT_ACTIVE")) active_forced = std::atoi(e);   // debug: fix A
   std::vector<char> top(T, 0);
   std::vector<int> frontier;
   for (int k = 0; k < T; ++k)
     if (parent[k] < 0) frontier.push_back(k);
-  double best = -1.0, topw = 0.0;
+  double best = -1.0, topw = 0.0, top_tiles = 0.0;
   std::vector<char> best_top;
   std::vector<int> best_front, best_asg;
   for (int iter = 0; iter <= T; ++iter) {
-    if ((int)frontier.size() >= nranks) {
-      std::vector<int> ord = frontier;
-      std::sort(ord.begin(), ord.end(), [&](int a, int b) { return W[a] != W[b] ? W[a] > W[b] : a > b; });
-      std::vector<double> bins(nranks, 0.0);
+    std::vector<int> ord = frontier;
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return COB[a] != COB[b] ? COB[a] > COB[b] : a > b; });
+    for (int A = 1; A <= std::min<int>(nranks, (int)ord.size()); ++A) {
+      if (active_forced > 0 && A != std::min<int>(active_forced, (int)ord.size())) continue;
+      // subtrees largest-first onto the least loaded of the A active ranks
+      // (observations), then the top-only captures onto the least loaded rank
+      std::vector<double> bins(nranks, 0.0), wbin(nranks, 0.0);
       std::vector<int> asg(ord.size());
       for (size_t q = 0; q < ord.size(); ++q) {
         int r = 0;
-        for (int x = 1; x < nranks; ++x)
+        for (int x = 1; x < A; ++x)
           if (bins[x] < bins[r]) r = x;
         asg[q] = r;
-        bins[r] += W[ord[q]];
+        bins[r] += COB[ord[q]];
+        wbin[r] += W[ord[q]];
       }
-      const double mx = *std::max_element(bins.begin(), bins.end());
-      if (best < 0 || topw + mx < best * (1.0 - 1e-12)) {
-        best = topw + mx;
+      std::vector<double> ob = bins;
+      *std::min_element(ob.begin(), ob.end()) += top_only_obs;
+      const double mo = *std::max_element(ob.begin(), ob.end());
+      const double mw = *std::max_element(wbin.begin(), wbin.end());
+      const double est = kObsUs * mo + kTileUs * top_tiles + 1e-9 * (topw + mw);
+      if (best < 0 || est < best * (1.0 - 1e-12)) {
+        best = est;
         best_top = top;
         best_front = ord;
         best_asg = asg;
         out.top_work = topw;
-        out.max_rank_work = mx;
+        out.max_rank_work = mw;
+        out.n_active = A;
       }
     }
     int v = -1;
@@ -740,15 +777,9 @@ RankSplit rank_split(const HostProblem &h, const ReducedLayout &L, int nranks) {
     if (v < 0 || ch[v].empty()) break;
     top[v] = 1;
     topw += w[v];
+    top_tiles += tiles[v];
     frontier.erase(std::find(frontier.begin(), frontier.end(), v));
     frontier.insert(frontier.end(), ch[v].begin(), ch[v].end());
-  }
-  if (best < 0) {   // fewer subtrees than ranks: some ranks own none
-    best_top = top;
-    best_front = frontier;
-    best_asg.assign(frontier.size(), 0);
-    for (size_t q = 0; q < frontier.size(); ++q) best_asg[q] = (int)q % nranks;
-    out.top_work = topw;
   }
   std::vector<int> root_rank(T, -1);
   for (size_t q = 0; q < best_front.size(); ++q) root_rank[best_front[q]] = best_asg[q];

@@ -72,6 +72,10 @@ struct DevProblem {
   // launch); null when there are none
   const int *big_caps = nullptr;
   int n_big_caps = 0;
+  // captures with more than kObsChunk observations (the chunked launches of
+  // k_linearize, k_cost and k_backsub); null when there are none
+  const int *chunk_caps = nullptr;
+  int n_chunk_caps = 0;
   // 1: the e-blocks (the "capture" slots, CSR cap_start) are the problem's tags
   // and the f-blocks (the "tag" slots) its captures -- ARSLAM_ELIM_TAGS: the
   // residual is then evaluated with the two pose arguments exchanged and the
@@ -255,6 +259,7 @@ struct RankSplit {
   std::vector<int> col_owner;   // [T] owning rank, -1 = top (replicated)
   std::vector<int> cap_owner;   // [nc]
   int n_top_cols = 0;
+  int n_active = 0;             // ranks owning subtrees (the others own top-only captures)
   double top_work = 0.0, max_rank_work = 0.0, total_work = 0.0;   // tile-task counts
   std::vector<int> col_class(int rank) const {   // llt_plan_symbolic's classes
     std::vector<int> c(col_owner.size());

@@ -60,7 +60,7 @@ __device__ __forceinline__ double lm_d2(const double *diag, long slot, double ra
 // (entry (row, j) at gout + 8 o0 kRowStride + j nrows + row): the Schur and
 // back-substitution passes at the same point reload them instead of
 // re-evaluating the projection.
-__device__ void fill_rows(const DevProblem &P, const double *x, const double *scale, int c,
+__device__ __forceinline__ void fill_rows(const DevProblem &P, const double *x, const double *scale, int c,
                           int o0, int row0, int nr, int nrows, double *rows, double *gout = nullptr) {
   const double *cam = x;
   const double *cap = x + slot_cap(P, c);
@@ -114,7 +114,7 @@ __device__ void fill_rows(const DevProblem &P, const double *x, const double *sc
 //   qv[row] = F_row . y_F = J_f y_f + J_t . y_F[tag rows]
 // formed from the row the lane just scaled (its tag row and y_F loads go out
 // beside the Jacobian loads instead of after a barrier).
-__device__ void load_rows_q(const DevProblem &P, const double *scale, const double *yF, double yf, int c, int o0,
+__device__ __forceinline__ void load_rows_q(const DevProblem &P, const double *scale, const double *yF, double yf, int c, int o0,
                             int row0, int nr, int nrows, double *rows, double *qv) {
   const double *sc = scale + slot_cap(P, c);
   for (int lr = threadIdx.x; lr < nr; lr += kWave) {
@@ -212,10 +212,25 @@ __device__ __forceinline__ double row_prod(const double *rr, int ca, int cb) {
   return rr[ca] * rr[cb];
 }
 
+// The per-capture kernels k_linearize, k_cost and k_backsub come in two
+// instances: kChunked = false, the main launch over every capture, which
+// takes the captures of at most kObsChunk observations (one wave of rows, the
+// code the usual capture runs) and skips the others when there are some;
+// true, a second launch over those (DevProblem::chunk_caps), their rows
+// through LDS 64 at a time.  The rare large capture's loops then cost the
+// usual one no registers or branches.
+template <bool kChunked>
+__device__ __forceinline__ int chunk_capture(const DevProblem &P, int &k) {
+  const int c = kChunked ? P.chunk_caps[blockIdx.x] : (int)blockIdx.x;
+  k = P.cap_start[c + 1] - P.cap_start[c];
+  return (!kChunked && k > kObsChunk) ? -1 : c;   // (-1: the chunked launch's)
+}
+
 // (4 waves per SIMD instead of the 3 its 143 VGPRs allow: a 28-byte spill,
 // 84 -> 71 us on cfg3; 5 waves spills 148 bytes and is slower)
 // Linearize at x: per-observation tag gradient/column norms, per-capture
 // gradient/column norms, cost and camera partials.  Unscaled Jacobian.
+template <bool kChunked>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_linearize(DevProblem P, const double *__restrict__ x,
                                                      double *__restrict__ g,
                                                      double *__restrict__ colnorm,
@@ -223,8 +238,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
                                                      double *__restrict__ parts) {
   if (gated(P.gate_lin)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int c = blockIdx.x, lane = threadIdx.x;
+  const int c = kChunked ? P.chunk_caps[blockIdx.x] : (int)blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
+  if (!kChunked && k > kObsChunk) return;   // (the chunked launch's)
   const int nrows = 8 * k;
   // The rows go through LDS in chunks of kObsChunk observations (one wave's
   // 64 rows), so any number of observations per capture fits; every sum runs
@@ -274,7 +290,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
       accs[15] = fix;
     }
   };
-  if (k <= kObsChunk) {
+  if (!kChunked) {   // (at most one chunk)
     chunk(0);
   } else {
     for (int q0 = 0; q0 < k; q0 += kObsChunk) {
@@ -916,6 +932,9 @@ __global__ void k_own_copy(DevProblem P, long first, long count, const double *_
 // Cost at x (candidate evaluation) of capture c: active / fixed cost,
 // finiteness.  cap: the capture's 6 parameters (x's slot, or the candidate
 // k_backsub just formed, held in LDS); camera and tags from x.
+// (kChunked: a capture of more than kObsChunk observations, its rows 64 at a
+// time; else at most one wave of rows)
+template <bool kChunked>
 __device__ __forceinline__ void capture_cost(const DevProblem &P, const double *__restrict__ x, const double *cap,
                                              int c, double *__restrict__ parts) {
   __shared__ double sq[kWave];
@@ -926,7 +945,7 @@ __device__ __forceinline__ void capture_cost(const DevProblem &P, const double *
   const double *cam = x;
   const AngleAxis ac = aa_prepare(cap + 3);
   double bad = 0.0, act = 0.0, fix = 0.0;
-  for (int base = 0; base < nrows; base += kWave) {
+  for (int base = 0; base < (kChunked ? nrows : 1); base += kWave) {
     const int row = base + lane;
     double r2 = 0.0;
     if (row < nrows) {
@@ -950,11 +969,15 @@ __device__ __forceinline__ void capture_cost(const DevProblem &P, const double *
       ocost[lane] = 0.5 * s;
     }
     __syncthreads();
-    if (lane == 0)
+    if (kChunked && lane == 0)
       for (int q = base / 8; q < min(k, base / 8 + kObsChunk); ++q) {
         if (P.obs_active[o0 + q]) act += ocost[q - base / 8]; else fix += ocost[q - base / 8];
       }
   }
+  if (!kChunked && lane == 0)
+    for (int q = 0; q < k; ++q) {
+      if (P.obs_active[o0 + q]) act += ocost[q]; else fix += ocost[q];
+    }
   bad = wave_max(bad);
   if (lane == 0) {
     parts[(long)P_COST * P.nc + c] = act;
@@ -963,14 +986,18 @@ __device__ __forceinline__ void capture_cost(const DevProblem &P, const double *
   }
 }
 
+template <bool kChunked>
 __global__ __launch_bounds__(kWave) void k_cost(DevProblem P, const double *__restrict__ x,
                                                 double *__restrict__ parts) {
-  const int c = blockIdx.x;
-  capture_cost(P, x, x + slot_cap(P, c), c, parts);
+  int k;
+  const int c = chunk_capture<kChunked>(P, k);
+  if (c < 0) return;
+  capture_cost<kChunked>(P, x, x + slot_cap(P, c), c, parts);
 }
 
 // Back substitution for capture c, candidate update of its slots and its
 // share of the model cost change.
+template <bool kChunked>
 __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *__restrict__ x,
                                                    const double *__restrict__ scale,
                                                    const double *__restrict__ diag, double radius,
@@ -980,8 +1007,10 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   if (gated(P.gate_step)) return;
   radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int c = blockIdx.x, lane = threadIdx.x;
-  const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
+  int k;
+  const int c = chunk_capture<kChunked>(P, k), lane = threadIdx.x;
+  if (c < 0) return;
+  const int o0 = P.cap_start[c];
   const long sc = slot_cap(P, c);
   if (k == 0) {
     if (lane < 6) xc[sc + lane] = x[sc + lane];
@@ -1034,7 +1063,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
       v[va] = s;
     }
   };
-  if (nrows <= kChunkRows) {   // (one chunk, the usual capture: its own specialised copy)
+  if (!kChunked) {   // (at most one chunk)
     chunk(0);
   } else {
     for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
@@ -1075,7 +1104,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
       mpart += p * (rr[13] - p / 2.0);
     }
   };
-  if (nrows <= kChunkRows) {
+  if (!kChunked) {
     model(nrows);
   } else {
     for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
@@ -1110,7 +1139,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   // by k_update_f, launched before this kernel
   if (with_cost) {
     __syncthreads();
-    capture_cost(P, xc, capc, c, parts);
+    capture_cost<kChunked>(P, xc, capc, c, parts);
   }
 }
 
@@ -1411,7 +1440,9 @@ void launch_linearize(const DevProblem &P, const double *x, double *g, double *c
                       double *obs_tg, double *parts, hipStream_t s) {
   if (P.nc == 0) return;
   const size_t lds = lds_rows(kObsChunk) + sizeof(double) * (kObsChunk + 16);
-  hipLaunchKernelGGL(k_linearize, dim3(P.nc), dim3(kWave), lds, s, P, x, g, colnorm, obs_tg, parts);
+  hipLaunchKernelGGL(k_linearize<false>, dim3(P.nc), dim3(kWave), lds, s, P, x, g, colnorm, obs_tg, parts);
+  if (P.n_chunk_caps)
+    hipLaunchKernelGGL(k_linearize<true>, dim3(P.n_chunk_caps), dim3(kWave), lds, s, P, x, g, colnorm, obs_tg, parts);
 }
 
 void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
@@ -1488,8 +1519,11 @@ void launch_backsub(const DevProblem &P, const double *x, const double *scale, c
                     bool reuse_ui, bool with_cost) {
   if (P.nc == 0) return;
   const size_t lds = lds_rows(kObsChunk) + sizeof(double) * (8L * kObsChunk + 36 + 36 + 16);
-  hipLaunchKernelGGL(k_backsub, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts,
+  hipLaunchKernelGGL(k_backsub<false>, dim3(P.nc), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc, parts,
                      reuse_ui ? 1 : 0, with_cost ? 1 : 0);
+  if (P.n_chunk_caps)
+    hipLaunchKernelGGL(k_backsub<true>, dim3(P.n_chunk_caps), dim3(kWave), lds, s, P, x, scale, diag, radius, yF, xc,
+                       parts, reuse_ui ? 1 : 0, with_cost ? 1 : 0);
 }
 
 void launch_update_f(const DevProblem &P, const double *x, const double *scale, const double *yF,
@@ -1501,7 +1535,8 @@ void launch_update_f(const DevProblem &P, const double *x, const double *scale, 
 
 void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_t s) {
   if (P.nc == 0) return;
-  hipLaunchKernelGGL(k_cost, dim3(P.nc), dim3(kWave), 0, s, P, x, parts);
+  hipLaunchKernelGGL(k_cost<false>, dim3(P.nc), dim3(kWave), 0, s, P, x, parts);
+  if (P.n_chunk_caps) hipLaunchKernelGGL(k_cost<true>, dim3(P.n_chunk_caps), dim3(kWave), 0, s, P, x, parts);
 }
 
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,

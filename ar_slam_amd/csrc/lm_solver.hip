@@ -247,6 +247,8 @@ struct arslam_lm {
   unsigned char *u_f_own = nullptr;
   std::vector<unsigned char> f_own;   // several ranks: DevProblem::f_own
   std::vector<int> big_caps;   // captures with more than kSchurMfmaBlocks distinct tags (k_schur's second launch)
+  std::vector<int> chunk_caps;   // captures with more than kObsChunk observations (the chunked launches)
+  int *u_chunk_caps = nullptr;
   unsigned char *u_obs_active = nullptr, *u_slot_free = nullptr;
   double *u_corners = nullptr, *u_x0 = nullptr;
   long *u_cap_off = nullptr;
@@ -749,6 +751,10 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   for (int c = 0; c < nc; ++c)
     if (h.cap_blk_start[c + 1] - h.cap_blk_start[c] > arslam::kSchurMfmaBlocks) big_caps.push_back(c);
   if (!big_caps.empty()) upload.add(&u_big_caps, big_caps.data(), big_caps.size());
+  chunk_caps.clear();
+  for (int c = 0; c < nc; ++c)
+    if (h.cap_start[c + 1] - h.cap_start[c] > arslam::kObsChunk) chunk_caps.push_back(c);
+  if (!chunk_caps.empty()) upload.add(&u_chunk_caps, chunk_caps.data(), chunk_caps.size());
   if (has_f) {
     upload.add(&u_cap_off, sg.cap_off.data(), nc + 1);
     upload.add(&u_dest_row, reinterpret_cast<const int2 *>(sg.dest_row.data()), n_dest);
@@ -795,6 +801,8 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.max_blk_per_cap = h.maxblk;
   P.big_caps = big_caps.empty() ? nullptr : u_big_caps;
   P.n_big_caps = (int)big_caps.size();
+  P.chunk_caps = chunk_caps.empty() ? nullptr : u_chunk_caps;
+  P.n_chunk_caps = (int)chunk_caps.size();
   P.swap_roles = elim_used == ARSLAM_ELIM_TAGS ? 1 : 0;
   P.nf = 3 + 6 * nt;
   P.fslot_row = u_fslot_row;

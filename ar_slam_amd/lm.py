@@ -214,7 +214,8 @@ def lib():
     L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
     L.arslam_lm_set_iteration_callback.argtypes = [C.c_void_p, ITER_CB, C.c_void_p]
     L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
-    L.arslam_lm_debug_tag_pair_tile.argtypes = [C.c_void_p, _dp, _dp, C.POINTER(C.c_int)]
+    if hasattr(L, "arslam_lm_debug_tag_pair_tile"):   # (absent from older variant builds under A/B)
+        L.arslam_lm_debug_tag_pair_tile.argtypes = [C.c_void_p, _dp, _dp, C.POINTER(C.c_int)]
     _lib = L
     return L
 

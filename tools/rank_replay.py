@@ -73,7 +73,7 @@ def replay(name, world, solves=4):
     rows = []
     for rank in range(world):
         if world == 1:
-            rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, device=0)
+            rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, device=0, phase_timing=1)
         else:
             z = np.load(os.path.join(REC, f"replay_{name}_{world}_r{rank}.npz"))
             recs = [z[f"arr_{i}"] for i in range(len(z.files))]
@@ -84,7 +84,7 @@ def replay(name, world, solves=4):
                 pos[0] += 1
 
             rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners,
-                                    comm=(rank, world, allreduce), device=0)
+                                    comm=(rank, world, allreduce), device=0, phase_timing=1)
         acc = {k: 0.0 for k in KEYS}
         n_it = 0
         s = None
@@ -100,6 +100,7 @@ def replay(name, world, solves=4):
         row = {k: acc[k] / n_it for k in KEYS}
         row.update(rank=rank, iters=s["num_linear_solves"], owned=s["n_owned_captures"],
                    comm_mb_per_it=s["comm_bytes"] / s["num_linear_solves"] / 1e6, top_tiles=s["n_top_tiles"],
+                   comm_calls_per_it=s["comm_calls"] / s["num_linear_solves"],
                    costs=[it["cost"] for it in s["iterations"]])
         rows.append(row)
         print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in row.items() if k != "costs"}),
@@ -132,19 +133,21 @@ def model(name, worlds, gbps=100.0, lat_us=25.0):
             top = rows[0]["t_factor_top_ms"]
         solve = one["t_solve_ms"]
         mb = rows[0]["comm_mb_per_it"] if world > 1 else 0.0
-        # ring all-reduce: 2 (N-1)/N of the bytes over the link, ~7 calls per iteration
-        exch = (2.0 * (world - 1) / world * mb * 1e6 / (gbps * 1e9) * 1e3 + 7 * lat_us * 1e-3) if world > 1 else 0.0
+        calls = rows[0].get("comm_calls_per_it", 7.0) if world > 1 else 0.0   # (the solver's own count)
+        # ring all-reduce: 2 (N-1)/N of the bytes over the link, plus a latency per collective
+        exch = (2.0 * (world - 1) / world * mb * 1e6 / (gbps * 1e9) * 1e3 + calls * lat_us * 1e-3) if world > 1 else 0.0
         step = shard + top + solve + exch
         out.append({"n_gpus": world, "sharded_incl_own_factor_ms": shard, "own_factor_ms": own,
                     "top_or_full_factor_ms": top, "bsolve_ms": solve, "exchange_mb": mb,
-                    "exchange_ms_est": exch, "step_ms": step})
+                    "exchange_ms_est": exch, "collectives_per_iteration": calls, "step_ms": step})
     base = out[0]["step_ms"]
     for o in out:
         o["speedup_vs_1"] = base / o["step_ms"]
         print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in o.items()}))
     with open(os.path.join(OUT, f"replay_{name}_model.json"), "w") as f:
         json.dump({"assumptions": f"exchange = ring all-reduce at {gbps} GB/s algorithm bandwidth + {lat_us} us "
-                                  "per call x 7 calls per LM iteration; Schur assembly and both factorization "
+                                  "per collective (the solver's own count per LM iteration, summary.comm_calls); "
+                                  "Schur assembly and both factorization "
                                   "phases measured per rank alone on one MI355X (tools/rank_replay.py); "
                                   "linearize/back-substitution/cost from the one-rank run scaled by owned captures",
                    "rows": out}, f, indent=1)
