@@ -247,6 +247,7 @@ extern "C" int arslam_debug_rank_split(const arslam_soa_problem *p, int nranks, 
     info->top_work = split.top_work;
     info->max_rank_work = split.max_rank_work;
     info->total_work = split.total_work;
+    info->n_active = split.n_active;
     for (int c = 0; c < h.nc; ++c) {
       if (cap_owner) cap_owner[c] = split.cap_owner[c];
       info->n_owned_captures += split.cap_owner[c] == rank;

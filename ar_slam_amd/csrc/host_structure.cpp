@@ -58,7 +58,10 @@ int peripheral(int start, const std::vector<std::vector<int>> &adj, const std::v
   return best;
 }
 
-double nd_beta() { return 0.6; }
+double nd_beta() {
+  static const double b = std::getenv("ARSLAM_ND_BETA") ? std::atof(std::getenv("ARSLAM_ND_BETA")) : 0.6;   // debug sweeps
+  return b;
+}
 
 // Elimination-tree height, in tile columns, of a dissection step: the
 // separator's tiles plus the larger child's height, which grows about as
@@ -734,7 +737,8 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
       for (int a = 0; a < 3; ++a) xyz[3L * t + a] = h.x0[3 + 6L * nc + 6L * t + a];
     // leaves of up to 32 tags (192 rows = 3 whole tiles): a smaller dissection
     // would not shorten the elimination tree, only add padding and parts
-    parts = nd_parts(nt, adj, 32, xyz, fast_order);
+    static const int leaf = std::getenv("ARSLAM_ND_LEAF") ? std::atoi(std::getenv("ARSLAM_ND_LEAF")) : 32;   // debug sweeps
+    parts = nd_parts(nt, adj, leaf, xyz, fast_order);
   } else {
     std::vector<int> order;
     if (ordering == 1 && nt > 1) order = rcm_order(nt, adj);

@@ -528,7 +528,8 @@ class SplitInfo(C.Structure):
     _fields_ = [("tiles_per_side", C.c_int), ("n_top_cols", C.c_int), ("n_own_cols", C.c_int),
                 ("n_top_tiles", C.c_long), ("n_tiles", C.c_long), ("n_dag_tasks", C.c_long),
                 ("phase_split", C.c_long), ("dag_valid", C.c_int), ("n_owned_captures", C.c_int),
-                ("top_work", C.c_double), ("max_rank_work", C.c_double), ("total_work", C.c_double)]
+                ("top_work", C.c_double), ("max_rank_work", C.c_double), ("total_work", C.c_double),
+                ("n_active", C.c_int)]
 
 
 def debug_rank_split(camera, cap, tag, obs_cap, obs_tag, corners, nranks, rank):

@@ -106,6 +106,7 @@ typedef struct {
   int dag_valid;            /* 1: ticket order valid and the randomised interleavings finish */
   int n_owned_captures;
   double top_work, max_rank_work, total_work;   /* tile-task counts (RankSplit) */
+  int n_active;             /* ranks owning subtrees (the others own top-only captures) */
 } arslam_split_info;
 int arslam_debug_rank_split(const arslam_soa_problem *p, int nranks, int rank, arslam_split_info *info,
                             int *cap_owner);

@@ -175,6 +175,12 @@ def test_rank_split_partitions_the_factorization(L, name, worlds):
     if name == "cfg3":
         info, _ = L.debug_rank_split(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, 2, 0)
         assert info["n_top_tiles"] <= 100 and info["n_top_tiles"] * 32768 < 4e6
+        # the modelled split keeps the top small as N grows: ranks beyond the
+        # useful subtree count stay idle in phase 0 instead of growing the exchange
+        for world in (4, 8):
+            info, owners = L.debug_rank_split(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, world, 0)
+            assert info["n_top_tiles"] <= 100, (world, info)
+            assert 2 <= info["n_active"] <= world
 
 
 @pytest.mark.parametrize("name,cuts", [("small", [1, 17, 40]), ("cfg2", [300, 700, 999])])
