@@ -257,6 +257,9 @@ def main():
     ap.add_argument("--skip-zero-tiles", type=int, default=1)
     ap.add_argument("--ordering", type=int, default=2, help="0 natural, 1 RCM, 2 nested dissection")
     ap.add_argument("--executor", type=int, default=1, help="0 level launches, 1 persistent task graph")
+    ap.add_argument("--no-runtime-warmup", action="store_true",
+                    help="no small solve before the setup (profiling passes: rocprof's per-kernel averages then hold "
+                         "only this workload's launches; the setup then includes the runtime start)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -299,7 +302,7 @@ def main():
     # solve first and reported on its own (runtime_init_s): a SLAM node pays it
     # once, every problem after it pays the setup below
     torch.cuda.synchronize()
-    runtime_init_s = lm.warm_up(local_rank)
+    runtime_init_s = None if args.no_runtime_warmup else lm.warm_up(local_rank)
     torch.cuda.synchronize()
     t_setup = time.perf_counter()
     rp = lm.ResidentProblem(**part, comm=comm, phase_timing=0, **opts)
