@@ -236,8 +236,10 @@ def load_pmc_traffic():
     try:
         with open(os.path.join(ROOT, PMC_PROFILE)) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        if "hbm_bytes_per_launch" in d:
+            return d["hbm_bytes_per_launch"]
+        return d["kernels"]["k_factor_dag"]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError, TypeError):
         return None
 
 

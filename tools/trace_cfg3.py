@@ -6,6 +6,6 @@ sys.path.insert(0, ".")
 from ar_slam_amd import lm, synth  # noqa: E402
 
 g = synth.config_graph(sys.argv[1] if len(sys.argv) > 1 else "cfg3")
-lm.warm_up()
+
 cam, cap, tag, s = lm.solve_graph(g)
 print("final cost", s["final_cost"], "iterations", len(s["iterations"]))
