@@ -1085,6 +1085,16 @@ __device__ __forceinline__ void gemm64_nt(const double *sA, const double *sB, in
   }
 }
 
+// The first panel beside which the fused solve's steps may run (4: never).
+// cfg3 k_factor_dag: 3 -> 660.8, 4 -> 665.1, 2 -> 676.1, 1 -> 683.8 us
+// (interleaved, one box): waves 1-3 working beside the earlier panels slow
+// wave 0's diagonal blocks (the same steps alone on the chip cost nothing,
+// tools/pipe_bench.hip).
+#ifndef ARSLAM_PIPE_FROM
+#define ARSLAM_PIPE_FROM 3
+#endif
+constexpr int kPipeFrom = ARSLAM_PIPE_FROM;
+
 struct DagArgs {
   double *S;
   int T;
@@ -1154,7 +1164,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
   __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 12 + 16 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
-  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation,
+  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [12..15] fused solve steps done,
   // [6] its fetch requested, [8..10] the POTRF pipeline's flags, [11] thirds of that tile loaded,
   // [16..17] the continuation's A_kk halves in D, [20..21] its early waits seen met by waves 2-3
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
@@ -1328,12 +1338,22 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // a third each, beside the next panel: on the late elimination-tree chain
       // the tile's last update lands a few microseconds into the POTRF
       // (cfg3 k_factor_dag 758 -> 736 us).
-      if (tid == 0) sh[6] = 0;
+      if (tid == 0) {
+        sh[6] = 0;
+        sh[12] = sh[13] = sh[14] = sh[15] = 0;   // the fused solve's column steps done per row block
+      }
       // sh[11]: thirds of the tile loaded into X (3: all; set to 0 by the
       // pipeline's start).  Each wave decides for its own third: a wave that
       // reaches a panel late must not take another wave's completed third for
       // the whole tile.
       bool third_done = false;
+      // The fused solve's first steps beside the last panel: once the whole
+      // tile is in X, waves 1-3 apply the solve's column steps 0-2 while wave 0
+      // factors the last diagonal block (wave 1 takes row blocks 0 and 3, waves
+      // 2-3 one each), so only step 3 remains after the factorization (the
+      // same products in the same order).  Beside the earlier panels they slow
+      // the factorization more than they save (kPipeFrom).
+      int sdone = 0;
       const bool ok = blocked_potrf64_async(D, inv, LTd, sh + 1, sh + 8, tid, colx, [&](int p, int wv, int ln) {
         auto fetch_third = [&]() {
         auto poll = [&]() {
@@ -1406,6 +1426,22 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
             ap_met = met && apf;
           }
         }
+        if (kPipeFrom <= 3 && pf_src && p >= kPipeFrom && sdone < p && lds_get(sh + 11) >= 3) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          for (int st = sdone; st < p; ++st) {
+            if (wv == 1) {
+              trsm_step(X, D, LTd, 0, st, ln);
+              trsm_step(X, D, LTd, 3, st, ln);
+            } else {
+              trsm_step(X, D, LTd, wv - 1, st, ln);
+            }
+          }
+          sdone = p;
+          if (ln == 0) {
+            if (wv == 1) sh[12] = sh[15] = sdone;
+            else sh[12 + wv - 1] = sdone;
+          }
+        }
       }, X, fold_in);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1455,17 +1491,17 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
           ap_ok = true;
         }
         __syncthreads();
-        // blocked_trsm64, its steps inline (row block w per wave)
-        trsm_step(X, D, LTd, w, 0, lane);
-        trsm_step(X, D, LTd, w, 1, lane);
+        // blocked_trsm64, its steps inline (row block w per wave), from the
+        // first step not applied beside the last panel
+        const int s0 = pref ? sh[12 + w] : 0;
+        for (int st = s0; st < 2; ++st) trsm_step(X, D, LTd, w, st, lane);
         // claim the continuation target before the tile is published: its
         // drawer waits for this tile, so it cannot have claimed it yet.  (The
         // CAS goes out here and is answered beside the last two steps.)
         const bool want = c >= 0 && tid == 0 && a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap;
         int cas_old = 1;
         if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
-        trsm_step(X, D, LTd, w, 2, lane);
-        trsm_step(X, D, LTd, w, 3, lane);
+        for (int st = max(s0, 2); st < 4; ++st) trsm_step(X, D, LTd, w, st, lane);
         __syncthreads();
         // wave 1 stores the solved tile, waves 2-3 move the continuation's
         // A_kk into D (free: L_kk's last reader was the solve)

@@ -2,7 +2,7 @@
 default library, name "base") runs in its own process, interleaved over rounds; per run it
 prints the mean k_factor_dag launch (HIP events), LM iterations/s over timed cfg solves, the
 final cost and a digest of the solved parameters (bit-identity across variants).
-usage: python tools/ab.py cfg3 rounds name1 name2 ...      (child: --child cfg lib steps)"""
+usage: python tools/ab.py cfg3 rounds name1 name2 ...   (a name env:VAR=VALUE: the default library under that switch)      (child: --child cfg lib steps)"""
 import hashlib
 import json
 import os
@@ -38,7 +38,10 @@ def main():
     for r in range(rounds):
         for n in names:
             env = dict(os.environ)
-            if n != "base":
+            if n.startswith("env:"):   # the default library under an environment switch: env:NAME=VALUE
+                k, v = n[4:].split("=", 1)
+                env[k] = v
+            elif n != "base":
                 env["ARSLAM_LIB"] = os.path.join(ROOT, "ar_slam_amd", f"var_{n}.so")
             out = subprocess.run([sys.executable, __file__, "--child", cfg, "8"], env=env, capture_output=True,
                                  text=True, timeout=300)
