@@ -387,12 +387,21 @@ struct arslam_lm {
   static inline bool dag_traced = false;   // debug trace: one per process
   static inline int dag_trace_seen = 0;
 
+  int cus_device = -1, cus = 0;   // (the attribute query costs ~1 ms: once per device, not per load)
   void ensure_stream() {
-    if (opt.device >= 0) HIP_CHECK(hipSetDevice(opt.device));
+    // (hipSetDevice costs ~1 ms even to the current device: the incremental
+    // cfg2 flow's 179 full loads spent 0.21 s in it)
     HIP_CHECK(hipGetDevice(&device));
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
-      dag_workgroups = 2 * cus;   // two 73 KB-LDS workgroups per CU
+    if (opt.device >= 0 && opt.device != device) {
+      HIP_CHECK(hipSetDevice(opt.device));
+      device = opt.device;
+    }
+    if (cus_device != device) {
+      cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
+      cus_device = device;
+    }
+    if (cus > 0) dag_workgroups = 2 * cus;   // two 73 KB-LDS workgroups per CU
     if (const char *g = std::getenv("ARSLAM_DAG_GRID")) dag_workgroups = std::max(1, std::atoi(g));   // debug
     if (!stream) HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &t : timers) t.init();
@@ -634,6 +643,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   }
   tp[1] = now_s();
   ensure_stream();
+  const double t_stream = now_s();
   soa = *p;   // (several ranks: the whole problem; write_back maps this rank's captures)
   nc = h.nc;
   nt = h.nt;
@@ -681,8 +691,8 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   setup_phase[3] = tp[5] - tp[4];
   setup_phase[4] = setup_s - setup_phase[0] - setup_phase[1] - setup_phase[2] - setup_phase[3];
   if (prof)
-    std::fprintf(stderr, "arslam setup: nc %d nt %d side %.3f host+layout %.3f stream+covis %.3f plan %.3f gather+upload %.3f total %.3f ms (order %s, %d levels, %ld tiles)\n",
-                 nc, nt, 1e3 * (tp[0] - t_load), 1e3 * (tp[1] - tp[0]), 1e3 * (tp[2] - tp[1]), 1e3 * (tp[3] - tp[2]),
+    std::fprintf(stderr, "arslam setup: nc %d nt %d side %.3f host+layout %.3f stream %.3f covis %.3f plan %.3f gather+upload %.3f total %.3f ms (order %s, %d levels, %ld tiles)\n",
+                 nc, nt, 1e3 * (tp[0] - t_load), 1e3 * (tp[1] - tp[0]), 1e3 * (t_stream - tp[1]), 1e3 * (tp[2] - t_stream), 1e3 * (tp[3] - tp[2]),
                  1e3 * (tp[5] - tp[4]), 1e3 * setup_s,
                  prev_order_nc == nc ? "fresh" : "kept", plan.nlev, (long)plan.n_tiles);
 }

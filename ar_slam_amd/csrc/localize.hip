@@ -528,7 +528,9 @@ struct arslam_localizer {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
       throw arslam::ApiError(ARSLAM_E_NO_DEVICE, "no HIP device");
-    if (opt.device >= 0) hip_check(hipSetDevice(opt.device), "hipSetDevice");
+    int cur = -1;   // (hipSetDevice costs ~1 ms even to the current device)
+    hip_check(hipGetDevice(&cur), "hipGetDevice");
+    if (opt.device >= 0 && opt.device != cur) hip_check(hipSetDevice(opt.device), "hipSetDevice");
     if (!stream) {
       hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
       hip_check(hipEventCreate(&ev0), "hipEventCreate");
