@@ -1094,6 +1094,10 @@ __device__ __forceinline__ void gemm64_nt(const double *sA, const double *sB, in
 #define ARSLAM_PIPE_FROM 3
 #endif
 constexpr int kPipeFrom = ARSLAM_PIPE_FROM;
+#ifndef ARSLAM_PIPE_W2
+#define ARSLAM_PIPE_W2 1
+#endif
+constexpr int kPipeW2 = ARSLAM_PIPE_W2;   // the wave (1-3) that also takes row block 3
 
 struct DagArgs {
   double *S;
@@ -1349,8 +1353,8 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       bool third_done = false;
       // The fused solve's first steps beside the last panel: once the whole
       // tile is in X, waves 1-3 apply the solve's column steps 0-2 while wave 0
-      // factors the last diagonal block (wave 1 takes row blocks 0 and 3, waves
-      // 2-3 one each), so only step 3 remains after the factorization (the
+      // factors the last diagonal block (wave w takes row block w - 1, and wave
+      // kPipeW2 row block 3 as well), so only step 3 remains after the factorization (the
       // same products in the same order).  Beside the earlier panels they slow
       // the factorization more than they save (kPipeFrom).
       int sdone = 0;
@@ -1429,17 +1433,13 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         if (kPipeFrom <= 3 && pf_src && p >= kPipeFrom && sdone < p && lds_get(sh + 11) >= 3) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
           for (int st = sdone; st < p; ++st) {
-            if (wv == 1) {
-              trsm_step(X, D, LTd, 0, st, ln);
-              trsm_step(X, D, LTd, 3, st, ln);
-            } else {
-              trsm_step(X, D, LTd, wv - 1, st, ln);
-            }
+            trsm_step(X, D, LTd, wv - 1, st, ln);
+            if (wv == kPipeW2) trsm_step(X, D, LTd, 3, st, ln);
           }
           sdone = p;
           if (ln == 0) {
-            if (wv == 1) sh[12] = sh[15] = sdone;
-            else sh[12 + wv - 1] = sdone;
+            sh[12 + wv - 1] = sdone;
+            if (wv == kPipeW2) sh[15] = sdone;
           }
         }
       }, X, fold_in);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
