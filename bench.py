@@ -228,7 +228,7 @@ def load_pmc_localize():
 
 # the PMC pass (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md) of the commit this bench line
 # measures: each profile round writes its own directory, and this names the latest
-PMC_PROFILE = os.path.join("profiles", "r04", "pmc_hbm_bytes.json")
+PMC_PROFILE = os.path.join("profiles", "r04b", "pmc_hbm_bytes.json")
 
 
 def load_pmc_traffic():
