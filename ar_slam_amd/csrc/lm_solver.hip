@@ -387,12 +387,10 @@ struct arslam_lm {
   static inline bool dag_traced = false;   // debug trace: one per process
   static inline int dag_trace_seen = 0;
 
-  int cus_device = -1, cus = 0;   // (the attribute query costs ~1 ms: once per device, not per load)
+  int cus_device = -1, cus = 0;   // the CU count, queried once per device
   void ensure_stream() {
-    // (hipSetDevice costs ~1 ms even to the current device: the incremental
-    // cfg2 flow's 179 full loads spent 0.21 s in it)
     HIP_CHECK(hipGetDevice(&device));
-    if (opt.device >= 0 && opt.device != device) {
+    if (opt.device >= 0 && opt.device != device) {   // (set only when it differs)
       HIP_CHECK(hipSetDevice(opt.device));
       device = opt.device;
     }
