@@ -528,7 +528,7 @@ struct arslam_localizer {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
       throw arslam::ApiError(ARSLAM_E_NO_DEVICE, "no HIP device");
-    int cur = -1;   // (hipSetDevice costs ~1 ms even to the current device)
+    int cur = -1;   // (set only when it differs)
     hip_check(hipGetDevice(&cur), "hipGetDevice");
     if (opt.device >= 0 && opt.device != cur) hip_check(hipSetDevice(opt.device), "hipSetDevice");
     if (!stream) {
