@@ -138,6 +138,13 @@ __device__ inline double *reduced_elem(double *S, const DevProblem &P, long r, l
   return S + (long)P.tile_id[(r >> 6) * P.T + (c >> 6)] * 4096 + (r & 63) * 64 + (c & 63);
 }
 
+// k_slot_norms' blocks (each one's six partials are reduced by the last to finish)
+#ifndef ARSLAM_NORM_BLOCKS
+#define ARSLAM_NORM_BLOCKS 64
+#endif
+constexpr int kNormBlocks = ARSLAM_NORM_BLOCKS;
+static_assert(kNormBlocks <= 256 && (kNormBlocks & (kNormBlocks - 1)) == 0, "k_slot_norms: one 256-thread tree");
+
 // Fields of a ticket's record (LltPlan::dag_rec, 32 ints).  -1 where absent.
 enum DagRecField {
   kRecType = 0, kRecY, kRecZ, kRecW,           // the task (type, y, z, w)

@@ -1261,7 +1261,6 @@ __global__ __launch_bounds__(1024) void k_lin_reduce(DevProblem P, const double 
 // Norms over free parameter slots, split into capture slots (out[0..2]) and
 // camera + tag slots (out[3..5]): max |g|, sum g^2, sum x^2.  The split lets
 // the capture-sharded path reduce only the disjoint capture part across ranks.
-constexpr int kNormBlocks = 64;
 
 __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long cap_hi,
                                                     const unsigned char *__restrict__ free_,

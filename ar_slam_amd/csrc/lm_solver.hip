@@ -399,7 +399,11 @@ struct arslam_lm {
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
       cus_device = device;
     }
-    if (cus > 0) dag_workgroups = 2 * cus;   // two 73 KB-LDS workgroups per CU
+    // 1.75 persistent workgroups per CU (73 KB of LDS each: two fit): 448 on
+    // the MI355X's 256 CUs.  cfg3 k_factor_dag 663.1 -> 655.7 us and
+    // 597.6 -> 593.0 us against 512 (same-box A/B, tools/ab.py): fewer
+    // co-resident update workgroups beside the chain's POTRF tasks
+    if (cus > 0) dag_workgroups = 7 * cus / 4;
     if (const char *g = std::getenv("ARSLAM_DAG_GRID")) dag_workgroups = std::max(1, std::atoi(g));   // debug
     if (!stream) HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &t : timers) t.init();
@@ -488,7 +492,7 @@ struct arslam_lm {
   // step's scalars (exchange_scalars; exchange_norms when no step follows).
   bool lin_xpending = false, norms_pending = false;
   DevBuf<double> d_lx, d_ag;   // the packed exchange; the all-gathered scalars
-  static constexpr int kLinSave = 16 + 8 + 6 * 64;   // d_red[kLinSave..+1]: the linearization's cost, fixed
+  static constexpr int kLinSave = 16 + 8 + 6 * arslam::kNormBlocks;   // d_red[kLinSave..+1]: the linearization's cost, fixed
   void complete_pending_lin();
   void lin_norms();   // k_slot_norms once the linearization's sums are final
   void exchange_scalars(arslam::AgFields fl);   // (+ the pending norms), into d_red
