@@ -44,7 +44,7 @@ constexpr int kSplitMin = 6;   // k-lists longer than this are split
 // applies it -- has a smaller ticket; so the ticketed persistent kernel
 // cannot deadlock.
 // Ticket order of the task graph by list scheduling: a simulation of
-// kSimWorkers workgroups that, whenever one is free, start the ready task
+// kSimWorkersDefault workgroups that, whenever one is free, start the ready task
 // with the longest remaining path to the end of the factorization (its
 // bottom level).  Tickets follow the simulated start order, so the order is
 // topological (a task starts after all of its producers finished) and tasks
@@ -57,7 +57,12 @@ constexpr int kSplitMin = 6;   // k-lists longer than this are split
 // readiness, workgroups block on them, and chain tasks are drawn late.  A
 // narrower simulation orders the chain earlier (cfg3 k_factor_dag 735 -> 716
 // us at 192-256; 160 is worse, 810 us; tools/env_bench.sh).
-constexpr int kSimWorkers = 224;
+constexpr int kSimWorkersDefault = 224;
+int sim_workers() {   // (ARSLAM_SIM_WORKERS: debug sweeps)
+  static const int w = std::getenv("ARSLAM_SIM_WORKERS") ? std::max(1, std::atoi(std::getenv("ARSLAM_SIM_WORKERS")))
+                                                         : kSimWorkersDefault;
+  return w;
+}
 // A POTRF node may also carry the TRSM of the column's first off-diagonal
 // tile (sub = its compact tile id): 'late' waits are those of that TRSM,
 // polled after L_kk is published.
@@ -175,9 +180,9 @@ static std::vector<int> dag_list_schedule(const std::vector<DagNode> &nodes, lon
   int busy = 0;
   double now = 0.0;
   std::vector<double> through(blevel_out ? n : 0);
-  const int sim_workers = kSimWorkers;
+  const int n_workers = sim_workers();
   while ((int)order.size() < n || !events.empty()) {
-    while (busy < sim_workers && !heap.empty()) {
+    while (busy < n_workers && !heap.empty()) {
       std::pop_heap(heap.begin(), heap.end(), cmp);
       const int v = heap.back();
       heap.pop_back();
