@@ -764,7 +764,10 @@ constexpr long kSpinCap = 1L << 16;
 // polls): cfg3 k_factor_dag 796 -> 757 us with the update tasks polling
 // every 16 units, flat from 16 to 32, worse at 64 (tools/variant_bench.sh).
 // The chain tasks (POTRF, TRSM) and the backward solve keep polling fast.
-constexpr int kPollSleep = 16;     // update tasks
+#ifndef ARSLAM_POLL_SLEEP
+#define ARSLAM_POLL_SLEEP 16
+#endif
+constexpr int kPollSleep = ARSLAM_POLL_SLEEP;   // update tasks
 constexpr int kChainSleep = 1;     // POTRF / TRSM tasks
 constexpr int kBsolveSleep = 1;    // k_bsolve_dag (its waits are all on the chain)
 
