@@ -1987,7 +1987,13 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
   DagArgs a{S, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_rec, P.dag_ks_tiles, P.upd_ks, P.dag_claimed,
             P.dag_waits, P.dag_counters, (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_part, P.upd_cnt, flag, t_begin, t_end,
             P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagCounterExtra - 1 : 0), progress, trace, gate};
-  const int grid = (int)std::min<long>(n_workgroups, t_end - t_begin);
+  // A small task graph runs on fewer workgroups (a quarter of its tasks, at
+  // least 64): its time is the elimination tree's chain, which runs faster
+  // beside fewer co-resident update workgroups (cfg2, 580 tasks: 219.6 us on
+  // 128 workgroups against 228.4 on 448; the incremental cfg2 flow's
+  // minimizer 1.83 -> 1.79 ms per Solve).  cfg3 (12,625 tasks) keeps the full grid.
+  const long ntk = t_end - t_begin;
+  const int grid = (int)std::min<long>(n_workgroups, std::max<long>(std::min<long>(64, ntk), ntk / 4));
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
 
