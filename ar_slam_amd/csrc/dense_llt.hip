@@ -768,7 +768,10 @@ constexpr long kSpinCap = 1L << 16;
 #define ARSLAM_POLL_SLEEP 16
 #endif
 constexpr int kPollSleep = ARSLAM_POLL_SLEEP;   // update tasks
-constexpr int kChainSleep = 1;     // POTRF / TRSM tasks
+#ifndef ARSLAM_CHAIN_SLEEP
+#define ARSLAM_CHAIN_SLEEP 1
+#endif
+constexpr int kChainSleep = ARSLAM_CHAIN_SLEEP;   // POTRF / TRSM tasks
 constexpr int kBsolveSleep = 1;    // k_bsolve_dag (its waits are all on the chain)
 
 // Poll a dependency counter with an atomic read-modify-write (+0): counters
