@@ -53,13 +53,39 @@ def build(force=False, verbose=False):
         return _build_locked(verbose)
 
 
+def build_id():
+    """What a built library is made of, embedded in it (arslam_lm_version): the git commit of the
+    tree (+dirty when the sources differ from it; "nogit" outside a checkout) and a digest of every
+    source, header and extra flag, so any measurement or fault can be attributed to its build."""
+    import hashlib
+    h = hashlib.sha256(os.environ.get("ARSLAM_EXTRA_FLAGS", "").encode())
+    files = [os.path.join(CSRC, f) for f in SOURCES] + [os.path.join(HOST, f) for f in HOST_SOURCES] + \
+        sorted(os.path.join(d, f) for d in (CSRC, HOST, os.path.join(ROOT, "include"))
+               for f in os.listdir(d) if f.endswith((".h", ".hpp")))
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.relpath(f, ROOT).encode() + b"\0" + fh.read())
+    commit = "nogit"
+    try:
+        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                text=True, timeout=10).stdout.strip() or "nogit"
+        if commit != "nogit":
+            rel = [os.path.relpath(f, ROOT) for f in files]
+            dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--"] + rel, capture_output=True,
+                                   text=True, timeout=10).stdout.strip()
+            commit += "+dirty" if dirty else ""
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return f"{commit} src {h.hexdigest()[:12]}"
+
+
 def _build_locked(verbose):
     extra = os.environ.get("ARSLAM_EXTRA_FLAGS", "")
     objdir = os.path.join(HERE, "_obj" + ("_" + "".join(c for c in extra if c.isalnum()) if extra else ""))
     os.makedirs(objdir, exist_ok=True)
     flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
-             "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC] + \
-        os.environ.get("ARSLAM_EXTRA_FLAGS", "").split()
+             "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+             f'-DARSLAM_BUILD_ID="{build_id()}"'] + os.environ.get("ARSLAM_EXTRA_FLAGS", "").split()
     objs = []
     procs = []
     for src in SOURCES:

@@ -167,6 +167,22 @@ extern "C" int arslam_debug_dense_llt_ex(long n, double *A, const double *b, dou
   return ARSLAM_OK;
 }
 
+namespace {
+// The protocol simulation over grids and policies (arslam::dag_simulate):
+// 1 if deadlock-free in every run, else -(grid * 16 + policy) of the first
+// deadlock.  Grids: small ones, the executor's 448 (1.75 per CU on 256 CUs)
+// and 512, and the small-graph rule of launch_dense_llt_dag.
+int simulate_all(const arslam::LltPlan &plan) {
+  const long n = plan.n_dag_tasks;
+  const int small = (int)std::min<long>(448, std::max<long>(std::min<long>(64, n), n / 4));
+  for (int wk : {1, 2, 7, 64, small, 448, 512})
+    for (int pol = 0; pol < arslam::kDagSimPolicies; ++pol)
+      for (unsigned seed = 1; seed <= (pol == 0 || pol == 3 ? 3u : 1u); ++seed)
+        if (!arslam::dag_simulate(plan, wk, seed, pol)) return -(wk * 16 + pol);
+  return 1;
+}
+}  // namespace
+
 extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                                          arslam_plan_info *info, int *tag_row) {
   if (!p || !info || ordering < 0 || ordering > 2) return ARSLAM_E_INVALID_ARG;
@@ -223,10 +239,45 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
           std::fclose(f);
         }
       }
-      for (int wk : {1, 2, 7, 64, 512})
-        for (unsigned seed = 1; seed <= 3 && info->dag_valid; ++seed)
-          if (!arslam::dag_simulate(plan, wk, seed)) info->dag_valid = -wk;
+      if (info->dag_valid) info->dag_valid = simulate_all(plan);
     }
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}
+
+namespace {
+arslam::LltPlan one_rank_plan(const arslam_soa_problem *p) {
+  const arslam::HostProblem h = arslam::host_problem(p, nullptr);
+  arslam::ReducedLayout L = arslam::reduced_layout(h, 2, true, nullptr, nullptr);
+  if (L.nR <= 0) throw arslam::ApiError(ARSLAM_E_INVALID_ARG, "no reduced system");
+  arslam::LltPlan plan;
+  arslam::llt_plan_symbolic(plan, L.T, L.N, L.pattern);
+  return plan;
+}
+}  // namespace
+
+extern "C" int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_workers, unsigned seed, int policy,
+                                         int *ok) {
+  if (!p || !ok || n_workers < 1 || policy < 0) return ARSLAM_E_INVALID_ARG;
+  try {
+    *ok = arslam::dag_simulate(one_rank_plan(p), n_workers, seed, policy) ? 1 : 0;
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}
+
+extern "C" int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[8], char *buf, int len) {
+  if (!p || !rec || !buf || len <= 0) return ARSLAM_E_INVALID_ARG;
+  try {
+    const std::string s = arslam::dag_fault_detail(one_rank_plan(p), rec);
+    std::snprintf(buf, (size_t)len, "%s", s.c_str());
     return ARSLAM_OK;
   } catch (const arslam::ApiError &e) {
     return e.code;
@@ -265,9 +316,7 @@ extern "C" int arslam_debug_rank_split(const arslam_soa_problem *p, int nranks, 
       info->n_dag_tasks = plan.n_dag_tasks;
       info->phase_split = plan.phase_split;
       info->dag_valid = arslam::dag_check(plan) ? 1 : 0;
-      for (int wk : {1, 2, 7, 64, 512})
-        for (unsigned seed = 1; seed <= 3 && info->dag_valid; ++seed)
-          if (!arslam::dag_simulate(plan, wk, seed)) info->dag_valid = -wk;
+      if (info->dag_valid) info->dag_valid = simulate_all(plan);
     }
     return ARSLAM_OK;
   } catch (const arslam::ApiError &e) {

@@ -1045,7 +1045,10 @@ __device__ __forceinline__ void store_tile_wt(double *__restrict__ g, const doub
 // broken graph drains in one spin cap instead of one per task.  Lane q polls
 // wait q (64 at a time), so a task's counters are read in one round trip, not
 // one after another.
-__device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag, int lane, bool chain) {
+// On a timeout *unmet = {counter, value seen, value awaited} of the first
+// wait still unmet (uniform over the wave), for the fault record.
+__device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag, int lane, bool chain,
+                         int3 *unmet) {
   for (int base = w0; base < w1; base += 64) {
     const int w = base + lane;
     const bool mine = w < w1;
@@ -1054,14 +1057,36 @@ __device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *
     for (;;) {
       // (every lane re-polls each round: no loop-carried per-lane state)
       const int got = mine ? ld_acquire_relaxed(counters + cv.x) : 0;
-      if (__builtin_amdgcn_ballot_w64(mine && got < cv.y) == 0) break;
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(mine && got < cv.y);
+      if (m == 0) break;
       if (chain) __builtin_amdgcn_s_sleep(kChainSleep);
       else __builtin_amdgcn_s_sleep(kPollSleep);
-      if (++spins > kSpinCap) return false;
-      if ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0) return false;
+      const bool give_up = ++spins > kSpinCap ||
+                           ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0);
+      if (give_up) {
+        const int l = __builtin_ctzll(m);
+        *unmet = make_int3(__builtin_amdgcn_readlane(cv.x, l), __builtin_amdgcn_readlane(got, l),
+                           __builtin_amdgcn_readlane(cv.y, l));
+        return false;
+      }
     }
   }
   return true;
+}
+
+// A wait of ticket t gave up (one thread): raise the launch's fault flag
+// (-(kind * 1000000 + t)); the workgroup whose code wins it also fills the
+// fault record (kDagFault*), which the host reads to name the stuck counter,
+// its producers and how far the launch had drawn.  Plain agent-scope atomic
+// stores: the record is read after the launch.
+__device__ void dag_fault(int *flag, int *counters, int n_tiles, const int *ticket, int kind, int t, int3 unmet) {
+  if (atomicCAS(flag, 0, -(kind * 1000000 + t)) != 0) return;
+  int *f = counters + 2 * n_tiles + kDagOffFault;
+  const int v[kDagFaultSlots] = {t, kind, unmet.x, unmet.y, unmet.z,
+                                 ld_acquire_relaxed(const_cast<int *>(ticket)),
+                                 ld_acquire_relaxed(counters + 2 * n_tiles + kDagOffInflight), (int)blockIdx.x};
+#pragma unroll
+  for (int i = 0; i < kDagFaultSlots; ++i) __hip_atomic_store(f + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // all threads: drain this workgroup's write-through stores before thread 0
@@ -1185,7 +1210,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // EARLY waits are all drawn; its late waits may name undrawn tickets, so at
   // most half the grid may hold claimed targets: the other workgroups can
   // always draw the lowest unfinished ticket, whose producers are all done.
-  int *inflight = a.counters + 2 * a.n_tiles + 1;
+  int *inflight = a.counters + 2 * a.n_tiles + kDagOffInflight;
   const int cont_cap = (int)(gridDim.x / 2);
   // Per-CU "POTRF running" flags (performance only: a wrong or stale flag
   // costs a bounded pause, never a result).  The 64x64 POTRF is a chain of
@@ -1196,7 +1221,7 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
   // (at most ~55 us) while the flag is up: cfg3 k_factor_dag 689 -> ~675 us.
   // A flag held across the POTRF task's late wait made it 2x slower (the
   // wait can need an update the flag holds).
-  int *cu_flag = inflight + 1;
+  int *cu_flag = a.counters + 2 * a.n_tiles + kDagOffCuFlags;
   int cu_key = 0;
   {
     unsigned hw, xcc;
@@ -1245,9 +1270,10 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
     if (w == 0) {
       // (sub.y: the end of the early waits; the late ones are a fused TRSM's,
       // or a folded TRSM's L_kk)
-      const bool ok = premet || dag_wait(a.counters, a.waits, r[kRecWait0], sub.y, a.flag, lane, task.x != 2);
+      int3 unmet;
+      const bool ok = premet || dag_wait(a.counters, a.waits, r[kRecWait0], sub.y, a.flag, lane, task.x != 2, &unmet);
       if (lane == 0) {
-        if (!ok) atomicCAS(a.flag, 0, -(1000000 + t));   // stuck ticket, for diagnosis
+        if (!ok) dag_fault(a.flag, a.counters, a.n_tiles, ticket, 1, t, unmet);   // stuck ticket, for diagnosis
         // a drawn continuation target: run it only if its predecessor did not claim it
         sh[2] = (cont || r[kRecMaxdep] < 0 || atomicCAS(a.claimed + t, 0, 1) == 0) ? 1 : 0;
       }
@@ -1472,8 +1498,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         const bool pref = sh[11] >= 3;   // (written inside the POTRF, barriers since)
         if (!pref) {
           if (w == 0) {
-            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, r[kRecWait1], a.flag, lane, true);
-            if (!ok2 && lane == 0) atomicCAS(a.flag, 0, -(3000000 + t));
+            int3 unmet;
+            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, r[kRecWait1], a.flag, lane, true, &unmet);
+            if (!ok2 && lane == 0) dag_fault(a.flag, a.counters, a.n_tiles, ticket, 3, t, unmet);
           }
           __syncthreads();
         }
@@ -1657,15 +1684,14 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         // in level order: wait until the target's earlier levels were applied
         if (tid == 0) {
           long spins = 0;
-          bool ok = true;
-          while (ld_acquire_relaxed(applied + task.w) < task.z) {
+          int seen;
+          while ((seen = ld_acquire_relaxed(applied + task.w)) < task.z) {
             __builtin_amdgcn_s_sleep(kPollSleep);
             if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(a.flag) < 0)) {
-              ok = false;
+              dag_fault(a.flag, a.counters, a.n_tiles, ticket, 2, t, make_int3(a.n_tiles + task.w, seen, task.z));
               break;
             }
           }
-          if (!ok) atomicCAS(a.flag, 0, -(2000000 + t));
         }
         __syncthreads();
 #pragma unroll
@@ -1989,7 +2015,7 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
   }
   DagArgs a{S, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_rec, P.dag_ks_tiles, P.upd_ks, P.dag_claimed,
             P.dag_waits, P.dag_counters, (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_part, P.upd_cnt, flag, t_begin, t_end,
-            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagCounterExtra - 1 : 0), progress, trace, gate};
+            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagOffTicket1 : kDagOffTicket0), progress, trace, gate};
   // A small task graph runs on fewer workgroups (a quarter of its tasks, at
   // least 64): its time is the elimination tree's chain, which runs faster
   // beside fewer co-resident update workgroups (cfg2, 580 tasks: 219.6 us on

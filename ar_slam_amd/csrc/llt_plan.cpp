@@ -837,89 +837,172 @@ bool dag_check(const LltPlan &plan) {
   return true;
 }
 
-// Randomised interleaving of n_workers concurrent workers running the
-// persistent executor's protocol (draw ticket, static waits, run, split
-// arrival, level-ordered application).  Returns false on a deadlock.
-bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed) {
+// Interleavings of n_workers concurrent workgroups running the persistent
+// executor's protocol (k_factor_dag) step by step.  Returns false on a
+// deadlock: a reachable state in which no workgroup can move.
+//   draw      the next ticket, or the continuation target the workgroup claimed;
+//   early     the task's early waits met (a POTRF's own; every wait of the
+//             other types).  A drawn continuation target then runs only if no
+//             predecessor claimed it; a POTRF publishes L_kk (ready[kk]);
+//   late      a POTRF with a fused TRSM: the TRSM's waits, then the solved
+//             tile (ready[sub]) is published;
+//   apply     an update item: split arrival, then the level-ordered application.
+// A finished POTRF claims its continuation target when every early producer
+// of the target other than its claimers has been drawn (maxdep) and fewer than
+// n_workers / 2 claimed targets are in flight, and runs it next.
+// Policies (which movable workgroup moves next):
+//   0  random (seed);
+//   1  draws first, then the workgroup holding the youngest ticket (every free
+//      workgroup takes a task as early as it can, the oldest task waits
+//      longest: the most workgroups held by blocked tasks);
+//   2  draws first, then the oldest ticket;
+//   3  draws first, then random.
+// policy | kDagSimNoCap (tests only) drops the in-flight cap on claimed
+// targets, which the protocol needs: the simulation must then find deadlocks.
+bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy) {
+  const bool no_cap = (policy & kDagSimNoCap) != 0;
+  policy &= kDagSimNoCap - 1;
   const long nt = plan.n_tiles, n = plan.n_dag_tasks;
   std::vector<int> cnt(2 * nt + 1, 0), arrived(plan.h_split.size(), 0);
   const bool has_cont = !plan.h_dag_cont.empty();
   auto maxdep = [&](long t) { return has_cont ? plan.h_dag_maxdep[t] : -1; };
   std::vector<char> claimed(n, 0);
-  // the persistent kernel's protocol (k_factor_dag): phases 0 pick, 1 wait,
-  // 2 apply-wait.  A finished POTRF claims its continuation target if every
-  // task the target waits on has been drawn, and runs it next; a drawn target
-  // runs only if its predecessor did not claim it.
-  struct W { long t = -1; int phase = 0; long next = -1; bool cont = false; };
+  enum { DRAW = 0, EARLY = 1, APPLY = 2, LATE = 3 };
+  struct W { long t = -1; int phase = DRAW; long next = -1; bool cont = false; };
   std::vector<W> ws(n_workers);
   long ticket = 0, finished = 0;
   int inflight = 0;   // claimed continuations running: at most n_workers / 2 (as k_factor_dag)
   unsigned rng = seed ? seed : 1u;
   auto rnd = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
+  auto met = [&](int q0, int q1) {
+    for (int q = q0; q < q1; ++q)
+      if (cnt[plan.h_dag_waits[q].x] < plan.h_dag_waits[q].y) return false;
+    return true;
+  };
+  auto early_end = [&](long t) { return plan.h_dag_sub[t].x >= 0 ? plan.h_dag_sub[t].y : plan.h_dag_wait_off[t + 1]; };
+  auto movable = [&](const W &w) {
+    switch (w.phase) {
+      case DRAW: return w.next >= 0 || ticket < n;
+      case EARLY: return met(plan.h_dag_wait_off[w.t], early_end(w.t));
+      case LATE: return met(plan.h_dag_sub[w.t].y, plan.h_dag_wait_off[w.t + 1]);
+      default: return cnt[nt + plan.h_dag_tasks[w.t].w] >= plan.h_dag_tasks[w.t].z;
+    }
+  };
   auto done = [&](W &w) {
     ++finished;
     const int c = has_cont ? plan.h_dag_cont[w.t] : -1;
     w.next = -1;
-    if (c >= 0 && ticket > maxdep(c) && !claimed[c] && inflight < n_workers / 2) {
+    if (c >= 0 && ticket > maxdep(c) && !claimed[c] && (no_cap || inflight < n_workers / 2)) {
       claimed[c] = 1;
       w.next = c;
       ++inflight;
     }
     if (w.cont) --inflight;
-    w.phase = 0;
+    w.phase = DRAW;
   };
-  while (finished < n) {
-    bool progressed = false;
-    const int start = (int)(rnd() % (unsigned)n_workers);
-    for (int m = 0; m < n_workers && !progressed; ++m) {
-      W &w = ws[(start + m) % n_workers];
-      if (w.phase == 0) {
-        if (w.next >= 0) {
-          w.t = w.next;
-          w.next = -1;
-          w.cont = true;
-        } else {
-          if (ticket >= n) continue;
-          w.t = ticket++;
-          w.cont = false;
-        }
-        w.phase = 1;
-        progressed = true;
-      } else if (w.phase == 1) {
-        bool ok = true;
-        for (int q = plan.h_dag_wait_off[w.t]; q < plan.h_dag_wait_off[w.t + 1] && ok; ++q)
-          ok = cnt[plan.h_dag_waits[q].x] >= plan.h_dag_waits[q].y;
-        if (!ok) continue;
-        progressed = true;
-        if (!w.cont && maxdep(w.t) >= 0) {
-          if (claimed[w.t]) {   // its predecessor runs it
-            w.phase = 0;
-            continue;
-          }
-          claimed[w.t] = 1;
-        }
-        const int4 task = plan.h_dag_tasks[w.t];
-        if (task.x == 3) { done(w); continue; }
-        if (task.x != 2) {
-          cnt[task.w] = 1;
-          if (plan.h_dag_sub[w.t].x >= 0) cnt[plan.h_dag_sub[w.t].x] = 1;
-          done(w);
-          continue;
-        }
-        const int sid = plan.h_items[task.y].w;
-        if (sid >= 0 && ++arrived[sid >> 8] < plan.h_split[sid >> 8].x) { done(w); continue; }
-        w.phase = 2;
+  auto move = [&](W &w) {
+    if (w.phase == DRAW) {
+      if (w.next >= 0) {
+        w.t = w.next;
+        w.next = -1;
+        w.cont = true;
       } else {
-        const int4 task = plan.h_dag_tasks[w.t];
-        if (cnt[nt + task.w] < task.z) continue;
-        cnt[nt + task.w]++;
-        progressed = true;
-        done(w);
+        w.t = ticket++;
+        w.cont = false;
+      }
+      w.phase = EARLY;
+      return;
+    }
+    const int4 task = plan.h_dag_tasks[w.t];
+    if (w.phase == EARLY) {
+      if (!w.cont && maxdep(w.t) >= 0) {
+        if (claimed[w.t]) {   // a predecessor runs it
+          w.phase = DRAW;
+          return;
+        }
+        claimed[w.t] = 1;
+      }
+      if (task.x == 3) return done(w);
+      if (task.x != 2) {
+        cnt[task.w] = 1;   // L_kk (POTRF) or the solved tile (TRSM)
+        if (task.x == 0 && plan.h_dag_sub[w.t].x >= 0) {
+          w.phase = LATE;
+          return;
+        }
+        return done(w);
+      }
+      const int sid = plan.h_items[task.y].w;
+      if (sid >= 0 && ++arrived[sid >> 8] < plan.h_split[sid >> 8].x) return done(w);
+      w.phase = APPLY;
+      return;
+    }
+    if (w.phase == LATE) {
+      cnt[plan.h_dag_sub[w.t].x] = 1;
+      return done(w);
+    }
+    cnt[nt + task.w]++;
+    done(w);
+  };
+  std::vector<int> cand;
+  while (finished < n) {
+    cand.clear();
+    bool draw = false;
+    for (int m = 0; m < n_workers; ++m)
+      if (movable(ws[m])) {
+        if (policy != 0 && ws[m].phase == DRAW && !draw) {   // draws first: keep only draws
+          draw = true;
+          cand.clear();
+        }
+        if (!draw || ws[m].phase == DRAW) cand.push_back(m);
+      }
+    if (cand.empty()) return false;
+    int pick = cand[0];
+    if (policy == 0 || policy == 3 || draw) {
+      pick = cand[rnd() % (unsigned)cand.size()];
+    } else {
+      for (int m : cand) {
+        const bool younger = ws[m].t > ws[pick].t;
+        if (policy == 1 ? younger : ws[m].t < ws[pick].t) pick = m;
       }
     }
-    if (!progressed) return false;
+    move(ws[pick]);
   }
   return true;
+}
+
+std::string dag_fault_detail(const LltPlan &plan, const int *rec) {
+  const long nt = plan.n_tiles, n = plan.n_dag_tasks;
+  const int t = rec[kFaultTicket], ctr = rec[kFaultCounter];
+  auto task_name = [&](long u) {
+    if (u < 0 || u >= n) return std::string("?");
+    const int4 k = plan.h_dag_tasks[u];
+    char b[96];
+    if (k.x == 0) std::snprintf(b, sizeof(b), "POTRF %d%s", k.y, plan.h_dag_sub[u].x >= 0 ? "+TRSM" : "");
+    else if (k.x == 1) std::snprintf(b, sizeof(b), "TRSM (%d,%d)", k.y, k.z);
+    else if (k.x == 2) std::snprintf(b, sizeof(b), "update item %d (level %d of tile %d)", k.y, k.z, k.w);
+    else std::snprintf(b, sizeof(b), "INV %d", k.y);
+    return std::string(b);
+  };
+  std::string s = "ticket " + std::to_string(t) + " (" + task_name(t) + ")";
+  if (ctr < 0 || ctr >= 2 * nt) return s;
+  // the tickets that advance the awaited counter
+  std::vector<long> prod;
+  for (long u = 0; u < n; ++u) {
+    const int4 k = plan.h_dag_tasks[u];
+    if (ctr < nt ? ((k.x == 0 || k.x == 1) && k.w == ctr) || plan.h_dag_sub[u].x == ctr
+                 : k.x == 2 && k.w == ctr - nt && k.z < rec[kFaultNeed])
+      prod.push_back(u);
+  }
+  s += ": " + std::string(ctr < nt ? "ready[" : "applied[") + std::to_string(ctr < nt ? ctr : ctr - nt) + "] = " +
+       std::to_string(rec[kFaultSeen]) + " < " + std::to_string(rec[kFaultNeed]) + ", advanced by";
+  for (size_t q = 0; q < prod.size() && q < 6; ++q) {
+    s += (q ? ", " : " ") + std::string("ticket ") + std::to_string(prod[q]) + " (" + task_name(prod[q]) + ")";
+    if (!plan.h_dag_maxdep.empty() && plan.h_dag_maxdep[prod[q]] >= 0) s += " [continuation target]";
+  }
+  if (prod.size() > 6) s += ", ...";
+  s += "; tickets drawn " + std::to_string(rec[kFaultDrawn]) + ", claimed continuations in flight " +
+       std::to_string(rec[kFaultInflight]) + ", workgroup " + std::to_string(rec[kFaultBlock]);
+  return s;
 }
 
 void llt_plan_upload(LltPlan &plan, hipStream_t s) {

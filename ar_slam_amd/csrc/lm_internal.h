@@ -19,9 +19,27 @@
 
 namespace arslam {
 constexpr int kCuFlags = 2048;   // k_factor_dag's per-CU flags: 8 XCCs x 256 (SE, SH, CU) ids
-// dag_counters after ready[n_tiles] | applied[n_tiles]: the phase-0 ticket,
-// the claimed-continuation count, the per-CU flags, the phase-1 ticket
-constexpr int kDagCounterExtra = 2 + kCuFlags + 1;
+// dag_counters after ready[n_tiles] | applied[n_tiles] (offsets from
+// 2 n_tiles): the phase-0 ticket, the claimed-continuation count, the per-CU
+// flags, the phase-1 ticket, and the fault record of a timed-out wait
+// (kDagFault*: written once, by the workgroup whose fault code won the flag)
+constexpr int kDagOffTicket0 = 0;
+constexpr int kDagOffInflight = 1;
+constexpr int kDagOffCuFlags = 2;
+constexpr int kDagOffTicket1 = 2 + kCuFlags;
+constexpr int kDagOffFault = 3 + kCuFlags;
+enum DagFaultField {
+  kFaultTicket = 0,   // the stuck ticket
+  kFaultKind = 1,     // 1 dependency (early) wait, 2 in-order application, 3 late wait
+  kFaultCounter = 2,  // the awaited counter: ready[c] (c < n_tiles) or applied[c - n_tiles]
+  kFaultSeen = 3,     // its value when the wait gave up
+  kFaultNeed = 4,     // the value it waited for
+  kFaultDrawn = 5,    // tickets drawn by then (the launch's ticket counter)
+  kFaultInflight = 6, // claimed continuations in flight
+  kFaultBlock = 7,    // the workgroup
+  kDagFaultSlots = 8
+};
+constexpr int kDagCounterExtra = kDagOffFault + kDagFaultSlots;
 
 constexpr int kWave = 64;
 constexpr int kTile = 64;          // reduced-system Cholesky tile
@@ -232,7 +250,8 @@ struct LltPlan {
   int2 *dag_ks_tiles = nullptr;
   std::vector<int> h_dag_rec;
   std::vector<int2> h_dag_ks_tiles;
-  // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags | phase-1 ticket])
+  // (dag_counters = [ready | applied | ticket | inflight | kCuFlags per-CU flags | phase-1 ticket |
+  //  fault record], kDagOff*)
   int2 *dag_waits = nullptr;
   int *dag_counters = nullptr;
   long n_dag_tasks = 0;
@@ -278,7 +297,15 @@ RankSplit rank_split(const HostProblem &h, const ReducedLayout &L, int nranks);
 // Ticket-order check of the task graph: executing the tasks one at a time in
 // ticket order, is every wait already satisfied when its task runs?
 bool dag_check(const LltPlan &plan);
-bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed);
+// Randomised (policy 0) or adversarial interleavings of n_workers workgroups
+// running k_factor_dag's protocol; false on a reachable deadlock (dag_simulate
+// in llt_plan.cpp lists the policies).
+bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy = 0);
+constexpr int kDagSimPolicies = 4;
+constexpr int kDagSimNoCap = 16;
+// The fault record of a timed-out executor wait (kDagFault*) in words: the
+// stuck task, the awaited counter, its producers and how far the launch drew.
+std::string dag_fault_detail(const LltPlan &plan, const int *rec);
 // Upload the host lists and allocate the plan's device buffers.
 void llt_plan_upload(LltPlan &plan, hipStream_t s);
 // llt_plan_symbolic + llt_plan_upload

@@ -66,6 +66,21 @@ std::string executor_fault_message(int code, int rank, int iteration) {
          std::to_string(iteration) + "): " + what;
 }
 
+// ... and, for a timed-out wait of k_factor_dag, what its fault record says:
+// the awaited counter, the tickets that advance it, how far the launch drew
+// (read after the step's stream sync; the record is reset with the counters)
+std::string executor_fault_message(int code, int rank, int iteration, const arslam::LltPlan &plan,
+                                   hipStream_t s) {
+  std::string m = executor_fault_message(code, rank, iteration);
+  if (code > -1000000 || code <= -4000000 || !plan.dag_counters) return m;
+  int rec[arslam::kDagFaultSlots];
+  if (hipMemcpyAsync(rec, plan.dag_counters + 2 * plan.n_tiles + arslam::kDagOffFault, sizeof(rec),
+                     hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess || rec[arslam::kFaultTicket] != (-code) % 1000000)
+    return m;
+  return m + " -- " + arslam::dag_fault_detail(plan, rec);
+}
+
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1631,7 +1646,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     // A stuck dependency wait of a persistent executor is a device fault, not
     // an indefinite system: fail loudly instead of shrinking the radius.
     if (red[arslam::NPART + 3] != 0.0)
-      throw Error(ARSLAM_E_DEVICE, executor_fault_message((int)red[arslam::NPART + 4], rank, it.iteration));
+      throw Error(ARSLAM_E_DEVICE, executor_fault_message((int)red[arslam::NPART + 4], rank, it.iteration, plan, stream));
     for (int ph = PH_SCHUR; ph < PH_N; ++ph) timers[ph].collect();
     timing_collect();
     if (deferred && finalize()) {
@@ -2109,6 +2124,11 @@ int arslam_lm_debug_tag_pair_tile(arslam_lm *h, const double *tag_a, const doubl
 
 const char *arslam_lm_last_error(void) { return g_last_error.c_str(); }
 
-const char *arslam_lm_version(void) { return "arslam_lm 0.1 (gfx950, fp64)"; }
+#ifndef ARSLAM_BUILD_ID
+#define ARSLAM_BUILD_ID "unknown"
+#endif
+// the build's commit and source digest (ar_slam_amd/build.py build_id): every
+// A/B line and bench line names the library it measured
+const char *arslam_lm_version(void) { return "arslam_lm 0.2 (gfx950, fp64) build " ARSLAM_BUILD_ID; }
 
 }  // extern "C"

@@ -48,6 +48,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
+           "arslam_debug_dag_simulate", "arslam_debug_dag_fault_detail",
            "arslam_debug_rank_split", "arslam_debug_gather_extend",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
@@ -155,6 +156,17 @@ _lib = None
 
 def library_path():
     return LIB_PATH
+
+
+def library_info():
+    """Which library this process measures: its file, the sha256 of the file (first 12 hex) and the
+    build it reports (commit + source digest, ar_slam_amd/build.py build_id)."""
+    import hashlib
+    with open(LIB_PATH, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:12]
+    v = lib().arslam_lm_version().decode()
+    return {"file": os.path.basename(LIB_PATH), "sha256": sha, "version": v.split(" build ")[0],
+            "build": v.split(" build ")[-1] if " build " in v else "unknown"}
 
 
 def lib():
@@ -513,6 +525,26 @@ def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const
     _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
                                            tag_row.ctypes.data_as(_ip)))
     return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]
+
+
+def debug_dag_simulate(g, n_workers, seed=1, policy=0):
+    """Host-only: one simulated interleaving of the persistent executor's protocol on g's one-rank
+    plan (policy 0 random, 1-3 adversarial; + 16 without the in-flight cap on claimed targets).
+    True if every task finished, False on a deadlock."""
+    A = _Soa(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
+    ok = C.c_int(-1)
+    _check(lib().arslam_debug_dag_simulate(C.byref(A.s), int(n_workers), C.c_uint(seed), int(policy), C.byref(ok)))
+    return bool(ok.value)
+
+
+def debug_dag_fault_detail(g, rec):
+    """Host-only: the text an executor fault carries for fault record rec[8] (lm_internal.h
+    DagFaultField) on g's one-rank plan."""
+    A = _Soa(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
+    r = (C.c_int * 8)(*[int(v) for v in rec])
+    buf = C.create_string_buffer(4096)
+    _check(lib().arslam_debug_dag_fault_detail(C.byref(A.s), r, buf, len(buf)))
+    return buf.value.decode()
 
 
 def debug_gather_extend(camera, cap, tag, obs_cap, obs_tag, corners, c0):

@@ -53,7 +53,10 @@ typedef struct {
   long n_split_targets;
   double update_flops;     /* algorithmic flops of the trailing updates per factorization */
   long n_dag_tasks;        /* tasks of the persistent executor's graph */
-  int dag_valid;           /* 1: run one at a time in ticket order, every wait is already met */
+  int dag_valid;           /* 1: run one at a time in ticket order, every wait is already met, and
+                              every simulated interleaving finishes (grids 1..512 and the small-graph
+                              grid, random and adversarial policies); -(grid * 16 + policy) of the
+                              first simulated deadlock */
   double factor_flops;     /* flops of the tile plan per factorization (POTRF, TRSM, updates, inverses) */
   double scalar_flops;     /* flops of the scalar Cholesky of the real rows in this order (no padding,
                               no structurally zero entries inside tiles) */
@@ -92,6 +95,20 @@ int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[4]);
 
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);
+
+/* Host only: the message an executor fault carries for the one-rank plan of p
+ * (nested dissection, sparse tiles) and a fault record rec[8] = {ticket, kind
+ * (1 dependency wait, 2 in-order application, 3 late wait), counter, value
+ * seen, value awaited, tickets drawn, claimed continuations in flight,
+ * workgroup}: the task, the counter, the tickets that advance it.  Writes at
+ * most len bytes (NUL-terminated) to buf. */
+/* Host only: one simulated interleaving of n_workers workgroups running the
+ * persistent executor's protocol on the one-rank plan of p (policy 0 random,
+ * 1-3 adversarial orders; + 16 drops the cap on claimed continuations in
+ * flight, which the protocol relies on).  *ok = 1 if every task finished, 0 on
+ * a deadlock. */
+int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_workers, unsigned seed, int policy, int *ok);
+int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[8], char *buf, int len);
 
 /* Host only: the multi-rank split arslam_lm_load_soa makes for rank `rank` of
  * `nranks` (nested dissection, sparse tiles) -- its two-phase tile plan, and

@@ -91,8 +91,9 @@ def test_invalid_problem_rejected_on_host(L):
 @pytest.mark.parametrize("name", ["medium", "cfg2", "cfg3"])
 def test_task_graph_is_deadlock_free(L, name):
     """The persistent executor's ticket order: every wait is met by earlier tickets when run one at a
-    time, and randomised interleavings of 1..512 concurrent workers never deadlock
-    (dag_check / dag_simulate behind arslam_debug_reduced_plan)."""
+    time, and interleavings of 1..512 concurrent workgroups (the executor's 448 and the small-graph
+    grid included), random and adversarial, never deadlock (dag_check / dag_simulate behind
+    arslam_debug_reduced_plan)."""
     g = synth.config_graph(name)
     for ordering in (1, 2):
         info, _ = _plan(L, g, ordering=ordering)
@@ -194,3 +195,30 @@ def test_gather_plan_extension_equals_a_fresh_plan(L, name, cuts):
         same, nd = L.debug_gather_extend(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, c0)
         assert same, (name, c0)
         assert nd > 0
+
+
+@pytest.mark.parametrize("name", ["small", "medium"])
+def test_simulation_finds_the_deadlock_without_the_claim_cap(L, name):
+    """The protocol simulation has teeth: a claimed continuation target may wait on tickets not yet
+    drawn (its late waits), so without the cap on claimed targets in flight one workgroup claims a
+    target and waits forever.  With the cap (the kernel's protocol) every policy finishes."""
+    g = synth.config_graph(name)
+    assert not L.debug_dag_simulate(g, 1, policy=1 + 16)
+    for pol in range(4):
+        assert L.debug_dag_simulate(g, 1, policy=pol)
+        assert L.debug_dag_simulate(g, 2, seed=3, policy=pol)
+
+
+def test_fault_record_names_the_stuck_counter_and_its_producers(L):
+    """The record round 4's unexplained cfg3 fault would now carry (ticket 2772 timed out in its
+    dependency wait): the message names the task, the counter, the value seen and the
+    producers of the counter, with continuation targets marked -- here ticket 2772 = TRSM (80,69),
+    waiting for L_69,69 from ticket 2205, a POTRF two predecessors may claim."""
+    g = synth.config_graph("cfg3")
+    rec = [2772, 1, 340, 0, 1, 3000, 3, 17]
+    s = L.debug_dag_fault_detail(g, rec)
+    assert s.startswith("ticket 2772 (TRSM (80,69))"), s
+    assert "ready[340] = 0 < 1" in s and "ticket 2205 (POTRF 69+TRSM) [continuation target]" in s, s
+    assert "tickets drawn 3000" in s and "in flight 3" in s, s
+    s2 = L.debug_dag_fault_detail(g, [2772, 1, 12625 * 0 + 2461 + 1620, 1, 2, 3000, 3, 17])
+    assert "applied[1620] = 1 < 2" in s2 and "ticket 1981" in s2 and "ticket 2355" in s2, s2

@@ -29,7 +29,9 @@ def child(cfg, steps):
     dom = sum(s["t_dominant_ms"] for s in ss) / max(1, sum(s["n_dominant_launches"] for s in ss))
     h = hashlib.sha256(np.ascontiguousarray(rp.camera).tobytes() + np.ascontiguousarray(rp.cap).tobytes() +
                        np.ascontiguousarray(rp.tag).tobytes()).hexdigest()[:12]
-    print(json.dumps({"factor_us": dom * 1e3, "it_s": it / el, "cost": repr(ss[-1]["final_cost"]), "digest": h}))
+    li = lm.library_info()
+    print(json.dumps({"factor_us": dom * 1e3, "it_s": it / el, "cost": repr(ss[-1]["final_cost"]), "digest": h,
+                      "lib": f"{li['file']} sha {li['sha256']}", "build": li["build"]}))
 
 
 def main():
@@ -45,13 +47,16 @@ def main():
                 env["ARSLAM_LIB"] = os.path.join(ROOT, "ar_slam_amd", f"var_{n}.so")
             out = subprocess.run([sys.executable, __file__, "--child", cfg, "8"], env=env, capture_output=True,
                                  text=True, timeout=300)
-            if out.returncode != 0:
-                print(n, "FAILED", out.stdout[-1000:], out.stderr[-600:], flush=True)
+            if out.returncode != 0:   # (the library is named even when the child failed)
+                lib = env.get("ARSLAM_LIB") or os.path.join(ROOT, "ar_slam_amd", "libarslam_lm.so")
+                so = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:12] if os.path.exists(lib) else "missing"
+                print(n, "FAILED", f"lib {os.path.basename(lib)} sha {so}", out.stdout[-1000:], out.stderr[-600:],
+                      flush=True)
                 continue
             d = json.loads(out.stdout.strip().splitlines()[-1])
             res[n].append(d)
-            print(f"round {r} {n:12s} factor {d['factor_us']:7.1f} us  {d['it_s']:7.1f} it/s  cost {d['cost']}  {d['digest']}",
-                  flush=True)
+            print(f"round {r} {n:12s} factor {d['factor_us']:7.1f} us  {d['it_s']:7.1f} it/s  cost {d['cost']}  {d['digest']}"
+                  f"  [{d['lib']}, build {d['build']}]", flush=True)
     for n in names:
         if not res[n]:
             continue
