@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.environ.get("ARSLAM_LIB") or os.path.join(HERE, "libarslam_lm.so")   # (override: variant builds)
-SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "lm_device.hip", "debug_api.hip", "llt_plan.cpp",
+SOURCES = ["lm_kernels.hip", "dense_llt.hip", "lm_solver.hip", "debug_api.hip", "llt_plan.cpp",
            "host_structure.cpp", "localize.hip"]
 HOST = os.path.join(HERE, "host")
 HOST_SOURCES = ["yaml_lite.cpp", "ar_slam_solver.cpp", "slam_capi.cpp"]   # plain C++ (g++)

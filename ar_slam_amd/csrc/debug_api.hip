@@ -5,6 +5,7 @@
 #include "arslam_lm.h"
 #include "arslam_lm_debug.h"
 
+#include <climits>
 #include <cstdlib>
 #include <cstdio>
 #include <unistd.h>
@@ -386,4 +387,124 @@ extern "C" int arslam_debug_gather_extend(const arslam_soa_problem *p, int c0, i
   } catch (...) {
     return ARSLAM_E_INVALID_ARG;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Box fingerprint (arslam_debug_box_fingerprint): the memory round trips the
+// persistent executor's hand-offs are made of, measured in-process for a few
+// milliseconds, so a bench line can be placed on the kind of box it ran on
+// (the same library ran cfg3's factorization at ~597 us on some MI355X boxes
+// and ~663 us on others).  One lane per measurement, bounded loops.
+namespace {
+__device__ __forceinline__ unsigned long long fp_rt() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;   // 100 MHz
+}
+
+// mode 0: never-matching CAS (the executor's counter poll), 1: agent-scope
+// atomic load (sc1, the tile loads), over a random pointer cycle
+__global__ void k_fp_chase(long *next, int n, int mode, unsigned long long *out, long *sink) {
+  if (threadIdx.x != 0) return;
+  long p = 0;
+  for (int i = 0; i < 32; ++i) p = __hip_atomic_load(next + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long t0 = fp_rt();
+  for (int i = 0; i < n; ++i) {
+    if (mode == 0) {
+      long v = LONG_MIN;
+      __hip_atomic_compare_exchange_strong(next + p, &v, LONG_MIN, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      p = v;
+    } else {
+      p = __hip_atomic_load(next + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  out[mode] = fp_rt() - t0;
+  sink[0] = p;
+}
+
+// a write-through (agent-scope) vector store and its acknowledgement
+// (s_waitcnt vmcnt(0)), one after another: the release of a published tile
+__global__ void k_fp_store_ack(long *buf, int n, unsigned long long *out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = fp_rt();
+  for (int i = 0; i < n; ++i) {
+    __hip_atomic_store(buf + 16L * (i & 1023), (long)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  out[2] = fp_rt() - t0;
+}
+
+// ping-pong of two workgroups through agent-scope release / acquire flags
+// (a hand-off and its answer); every wait bounded
+__global__ void k_fp_pingpong(int *flags, int n, unsigned long long *out, int *xcc) {
+  if (threadIdx.x != 0) return;
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  if (blockIdx.x < 2) xcc[blockIdx.x] = (int)(x & 7);
+  if (blockIdx.x >= 2) return;
+  int *a = flags, *b = flags + 64;
+  const bool first = blockIdx.x == 0;
+  const unsigned long long t0 = fp_rt();
+  long spins = 0;
+  for (int i = 1; i <= n && spins < (1L << 24); ++i) {
+    if (first) {
+      __hip_atomic_store(a, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      while (__hip_atomic_load(b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < i && ++spins < (1L << 24)) {}
+    } else {
+      while (__hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < i && ++spins < (1L << 24)) {}
+      __hip_atomic_store(b, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (first) out[3] = spins >= (1L << 24) ? ~0ull : fp_rt() - t0;
+}
+}  // namespace
+
+extern "C" int arslam_debug_box_fingerprint(int device, double out[6]) {
+  if (!out) return ARSLAM_E_INVALID_ARG;
+  int cur = 0;
+  DBG_CHECK(hipGetDevice(&cur));
+  if (device >= 0 && device != cur) DBG_CHECK(hipSetDevice(device));
+  const int nel = 1 << 15, n = 2000;   // 256 KB pointer cycle over cache-line-spaced slots
+  std::vector<long> h(nel, 0);
+  std::vector<int> perm(nel / 16);
+  for (int i = 0; i < (int)perm.size(); ++i) perm[i] = i;
+  unsigned s = 12345;
+  for (int i = (int)perm.size() - 1; i > 0; --i) {
+    s = s * 1103515245u + 12345u;
+    std::swap(perm[i], perm[s % (i + 1)]);
+  }
+  for (int i = 0; i < (int)perm.size(); ++i) h[16 * perm[i]] = 16L * perm[(i + 1) % perm.size()];
+  long *d = nullptr, *sink = nullptr, *st = nullptr;
+  unsigned long long *t = nullptr;
+  int *flags = nullptr, *xcc = nullptr;
+  hipStream_t stream = nullptr;
+  auto cleanup = [&]() {
+    if (stream) (void)hipStreamDestroy(stream);
+    for (void *p : {(void *)d, (void *)sink, (void *)st, (void *)t, (void *)flags, (void *)xcc})
+      if (p) (void)hipFree(p);
+    if (device >= 0 && device != cur) (void)hipSetDevice(cur);
+  };
+  hipError_t e = hipSuccess;
+  auto ok = [&](hipError_t r) { if (e == hipSuccess) e = r; return e == hipSuccess; };
+  if (ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) && ok(hipMalloc(&d, nel * sizeof(long))) &&
+      ok(hipMalloc(&sink, 64)) && ok(hipMalloc(&st, 1024 * 16 * sizeof(long))) && ok(hipMalloc(&t, 64)) &&
+      ok(hipMalloc(&flags, 1024)) && ok(hipMalloc(&xcc, 64)) &&
+      ok(hipMemcpyAsync(d, h.data(), nel * sizeof(long), hipMemcpyHostToDevice, stream)) &&
+      ok(hipMemsetAsync(flags, 0, 1024, stream)) && ok(hipMemsetAsync(t, 0, 64, stream))) {
+    hipLaunchKernelGGL(k_fp_chase, dim3(1), dim3(64), 0, stream, d, n, 0, t, sink);
+    hipLaunchKernelGGL(k_fp_chase, dim3(1), dim3(64), 0, stream, d, n, 1, t, sink);
+    hipLaunchKernelGGL(k_fp_store_ack, dim3(1), dim3(64), 0, stream, st, n, t);
+    hipLaunchKernelGGL(k_fp_pingpong, dim3(8), dim3(64), 0, stream, flags, n, t, xcc);
+    unsigned long long ht[4] = {0, 0, 0, 0};
+    int hx[2] = {-1, -1};
+    if (ok(hipGetLastError()) && ok(hipMemcpyAsync(ht, t, sizeof(ht), hipMemcpyDeviceToHost, stream)) &&
+        ok(hipMemcpyAsync(hx, xcc, sizeof(hx), hipMemcpyDeviceToHost, stream)) && ok(hipStreamSynchronize(stream))) {
+      for (int q = 0; q < 4; ++q) out[q] = ht[q] == ~0ull ? -1.0 : ht[q] * 10.0 / n;   // ns (100 MHz clock)
+      out[4] = hx[0];
+      out[5] = hx[1];
+    }
+  }
+  cleanup();
+  return hip_fail(e);
 }

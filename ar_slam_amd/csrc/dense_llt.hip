@@ -1152,7 +1152,6 @@ struct DagArgs {
   int *ticket;                // its ticket counter
   int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
   unsigned long long *trace;  // debug: [n_tasks][8] s_memrealtime at draw / waits met / end, workgroup, sub-phases
-  const int *gate;            // device LM loop: the launch returns at once while *gate != 0
 };
 
 // A ticket's 32-int record: two scalar loads in flight, one wait (the record
@@ -1195,7 +1194,6 @@ __device__ __forceinline__ unsigned long long realtime() {
   } while (0)
 
 __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
-  if (gated(a.gate)) return;
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
   __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 12 + 16 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
@@ -1829,11 +1827,11 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
                                                     int T, const double *__restrict__ Ld, long nR,
                                                     const int *__restrict__ cols, const int2 *__restrict__ gather,
                                                     const int *__restrict__ gbeg, int ncols, double *yF,
-                                                    int *counters, int *flag, const int *gate) {
+                                                    int *counters, int *flag) {
   __shared__ double red[4][T64];
   __shared__ double ys[T64];
   __shared__ int sh[2];
-  if (gated(gate) || *flag) return;
+  if (*flag) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   int *ticket = counters + T;   // (counters[0..T) are unused: y entries are their own flags)
   const double *Xinv = Ld + (long)T * T64 * T64;
@@ -1931,8 +1929,6 @@ namespace {
 // (with ld.n > 0 also the step's LM diagonal: k_lm_diag's work, one launch less)
 __global__ void k_exec_reset(int *flag, int *a, long na, int *b, long nb, int *c, long nc, int *d, long nd,
                              LmDiagArgs ld) {
-  if (gated(ld.gate)) return;
-  if (gated(ld.keep_diag)) ld.n = 0;
   const long n = na + nb + nc + nd;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < ld.nys; e += (long)gridDim.x * blockDim.x)
     ld.ysent[e] = __longlong_as_double((long long)kYSentinel);
@@ -2004,7 +2000,7 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
 }
 
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
-                          unsigned long long *trace, bool reset, int phase, const int *gate) {
+                          unsigned long long *trace, bool reset, int phase) {
   const int t_begin = phase == 1 ? (int)P.phase_split : 0;
   const int t_end = phase == 0 ? (int)P.phase_split : (int)P.n_dag_tasks;
   if (t_end <= t_begin) return;
@@ -2015,7 +2011,7 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
   }
   DagArgs a{S, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_rec, P.dag_ks_tiles, P.upd_ks, P.dag_claimed,
             P.dag_waits, P.dag_counters, (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_part, P.upd_cnt, flag, t_begin, t_end,
-            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagOffTicket1 : kDagOffTicket0), progress, trace, gate};
+            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagOffTicket1 : kDagOffTicket0), progress, trace};
   // A small task graph runs on fewer workgroups (a quarter of its tasks, at
   // least 64): its time is the elimination tree's chain, which runs faster
   // beside fewer co-resident update workgroups (cfg2, 580 tasks: 219.6 us on
@@ -2027,7 +2023,7 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
 }
 
 void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, double *yF, int *flag,
-                                 hipStream_t s, int n_workgroups, bool reset, const int *gate) {
+                                 hipStream_t s, int n_workgroups, bool reset) {
   const int ncols = (int)P.h_bcols.size();
   if (ncols == 0) return;
   if (reset) {
@@ -2039,7 +2035,7 @@ void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, dou
   }
   const int grid = std::min(n_workgroups, ncols);
   hipLaunchKernelGGL(k_bsolve_dag, dim3((unsigned)grid), dim3(256), 0, s, S, P.tile_id, P.T, P.ldiag, nR, P.bs_cols,
-                     P.bs_gather, P.bs_gbeg, ncols, yF, P.bs_counters, flag, gate);
+                     P.bs_gather, P.bs_gbeg, ncols, yF, P.bs_counters, flag);
 }
 
 void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double *z, double *yF,

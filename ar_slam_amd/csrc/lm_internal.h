@@ -138,18 +138,7 @@ struct DevProblem {
   const unsigned char *f_own = nullptr;
   double *jrows;             // [8 nb kRowStride] unscaled Jacobian rows + residual at the linearization point
   double *cap_ui;            // [36 nc] (U_c + D_c^2)^{-1} of the current step (k_schur -> k_backsub)
-  // device-resident LM loop (lm_device.hip; null: the host loop): a kernel of
-  // the linearization returns at once while *gate_lin != 0, one of the step
-  // while *gate_step != 0, and the step reads its radius from *radius_dev
-  const int *gate_lin = nullptr, *gate_step = nullptr;
-  const double *radius_dev = nullptr;
 };
-
-// the step's radius: the device LM state's when the loop runs on the device
-__device__ __forceinline__ double step_radius(const DevProblem &P, double radius) {
-  return P.radius_dev ? *P.radius_dev : radius;
-}
-__device__ __forceinline__ bool gated(const int *g) { return g && *g; }
 
 // element (r, c), r >= c, of the compact-tiled reduced system
 __device__ inline double *reduced_elem(double *S, const DevProblem &P, long r, long c) {
@@ -359,7 +348,7 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 // (flag: also out[NPART + 2] = indefinite (flag > 0), out[NPART + 3] = executor
 // fault (flag < 0), out[NPART + 4] = the raw flag)
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts,
-                         double *out, hipStream_t s, const int *flag = nullptr, const int *gate = nullptr,
+                         double *out, hipStream_t s, const int *flag = nullptr,
                          double *hout = nullptr);
 void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, hipStream_t s);
 // multi-rank exchange buffers: up to 4 segments packed at offsets off[] of one buffer
@@ -415,38 +404,6 @@ struct LaunchTiming {
   double flops = 0.0;         // algorithmic flops of the recorded launches
 };
 
-// ---- lm_device.hip: the device-resident LM loop ----
-constexpr int kLmDevMaxIters = ARSLAM_LM_MAX_ITERS;
-struct LmDevConsts {
-  double function_tolerance, parameter_tolerance, gradient_tolerance, min_relative_decrease;
-  double min_radius, max_radius;
-  int max_num_iterations, max_invalid;
-};
-// Ceres' minimizer state between iterations, in device memory (k_lm_decide /
-// k_lm_finalize).  The first block is what the host reads after each
-// iteration (done) and at the end.
-struct LmDevState {
-  int done, termination, rule, fault, fault_flag;
-  int num_successful, num_unsuccessful, num_linear_solves, n_iters;
-  // gates and switches read by the kernels of the next launches
-  int gate_step, gate_lin, keep_diag, need_lin, accept, copy_best;
-  int n_invalid;
-  double radius, decrease_factor;
-  double x_cost, fixed_cost, minimum_cost, gmax, gnorm, x_norm, prev_gmax, prev_gnorm;
-  double t0_s;                      // host seconds since the solve started, at k_lm_start
-  unsigned long long rt0, rt_iter;  // s_memrealtime at k_lm_start / the last record
-  arslam_lm_iteration it;           // the iteration being computed
-  arslam_lm_iteration iters[kLmDevMaxIters];   // records 1, 2, ... (iteration 0 is the host's)
-};
-void launch_lm_start(LmDevState *st, hipStream_t s);
-void launch_lm_decide(LmDevState *st, const double *red, const LmDevConsts &c, hipStream_t s);
-void launch_lm_finalize(LmDevState *st, const double *red, const LmDevConsts &c, hipStream_t s);
-// test hook: S's diagonal entry (row, row) to -1 when bit (solves so far) of mask is set
-void launch_lm_debug_indefinite(const DevProblem &P, double *S, long row, unsigned long long mask,
-                                const LmDevState *st, hipStream_t s);
-// dst <- src (n doubles) when *when != 0
-void launch_lm_copy(double *dst, const double *src, long n, const int *when, hipStream_t s);
-
 // ---- dense_llt.hip ----
 // Cholesky of the lower triangle of S (row-major, lda) over the plan's tiles,
 // in place.  Row nR carries the right-hand side, so on exit row nR =
@@ -460,7 +417,7 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
 // (phase: -1 every task; 0 / 1 one phase of a multi-rank plan, LltPlan)
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups,
                           int *progress = nullptr, unsigned long long *trace = nullptr, bool reset = true,
-                          int phase = -1, const int *gate = nullptr);
+                          int phase = -1);
 // the LM diagonal clamp(s^2 colnorm, dmin, dmax) over n slots (k_lm_diag)
 struct LmDiagArgs {
   long n;
@@ -469,8 +426,6 @@ struct LmDiagArgs {
   double *diag;
   double *ysent = nullptr;   // (also: the backward solve's y, nys rows, to kYSentinel)
   long nys = 0;
-  const int *gate = nullptr;       // device LM loop: the whole launch returns while *gate != 0
-  const int *keep_diag = nullptr;  // ... and the diagonal is kept while *keep_diag != 0
 };
 // k_bsolve_dag's "not solved yet" value of a y entry: a signalling-NaN bit
 // pattern no arithmetic produces (those NaNs are quiet)
@@ -503,7 +458,7 @@ void launch_dense_back_solve(const LltPlan &P, const double *S, long nR, double 
 // The same backward solve as one persistent launch (columns in root-first
 // ticket order, per-column completion counters).
 void launch_dense_back_solve_dag(const LltPlan &P, const double *S, long nR, double *yF, int *flag,
-                                 hipStream_t s, int n_workgroups, bool reset = true, const int *gate = nullptr);
+                                 hipStream_t s, int n_workgroups, bool reset = true);
 void launch_zero_tiles(const LltPlan &P, double *S, hipStream_t s);
 // copy the diagonal factors L_kk into S (tests only: S then holds the whole factor)
 void launch_scatter_diag(const LltPlan &P, double *S, hipStream_t s);

@@ -236,7 +236,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
                                                      double *__restrict__ colnorm,
                                                      double *__restrict__ obs_tg,
                                                      double *__restrict__ parts) {
-  if (gated(P.gate_lin)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int c = kChunked ? P.chunk_caps[blockIdx.x] : (int)blockIdx.x, lane = threadIdx.x;
   const int o0 = P.cap_start[c], k = P.cap_start[c + 1] - o0;
@@ -374,8 +373,6 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
                                                  const double *__restrict__ diag, double radius,
                                                  double *__restrict__ zero_tiles, long n_zero, ExecReset er,
                                                  const int *__restrict__ cap_list) {
-  if (gated(P.gate_step)) return;
-  radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   SCHUR_STAMP_INIT;
   // (cap_list: the second launch, over the captures with more than
@@ -819,8 +816,6 @@ __device__ __forceinline__ void prep_pad_row(const DevProblem &P, const double *
 
 __global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__restrict__ S,
                                                       const double *__restrict__ diag, double radius) {
-  if (gated(P.gate_step)) return;
-  radius = step_radius(P, radius);
   __shared__ double part[4][kWave];
   __shared__ SchurContrib cts[4][kWave];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -866,8 +861,6 @@ __global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__re
 // Split destinations: the pieces' partial sums, in piece order.
 __global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__restrict__ S,
                                                        const double *__restrict__ diag, double radius) {
-  if (gated(P.gate_step)) return;
-  radius = step_radius(P, radius);
   __shared__ double part[4][kWave];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int sp = blockIdx.x * 4 + w;
@@ -897,8 +890,6 @@ __global__ __launch_bounds__(256) void k_schur_combine(DevProblem P, double *__r
 // enough to stay positive (its factor row is L^{-1} b, its pivot unused).
 __global__ void k_prep_reduced(DevProblem P, const double *__restrict__ diag, double radius,
                                double *__restrict__ S, int which) {
-  if (gated(P.gate_step)) return;
-  radius = step_radius(P, radius);
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.N) return;
   if (which >= 0 && P.tile_class[i >> 6] != which) return;
@@ -1004,8 +995,6 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
                                                    const double *__restrict__ yF,
                                                    double *__restrict__ xc,
                                                    double *__restrict__ parts, int reuse_ui, int with_cost) {
-  if (gated(P.gate_step)) return;
-  radius = step_radius(P, radius);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   int k;
   const int c = chunk_capture<kChunked>(P, k), lane = threadIdx.x;
@@ -1151,7 +1140,6 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
                                                   const double *__restrict__ yF,
                                                   double *__restrict__ xc,
                                                   double *__restrict__ fparts) {
-  if (gated(P.gate_step)) return;
   __shared__ double red[2][256];
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0;
@@ -1236,9 +1224,8 @@ __device__ __forceinline__ void reduce_parts_block(int p, const double *__restri
 __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
                                                        const double *__restrict__ fparts,
                                                        int nfparts, double *__restrict__ out,
-                                                       const int *__restrict__ flag, const int *gate,
+                                                       const int *__restrict__ flag,
                                                        double *__restrict__ hout) {
-  if (gated(gate)) return;
   __shared__ double red[1024];
   reduce_parts_block(blockIdx.x, parts, nc, fparts, nfparts, out, flag, red, hout);
 }
@@ -1250,7 +1237,6 @@ __global__ __launch_bounds__(1024) void k_lin_reduce(DevProblem P, const double 
                                                      double *__restrict__ g, double *__restrict__ colnorm,
                                                      const double *__restrict__ parts, double *__restrict__ out,
                                                      double *__restrict__ hout) {
-  if (gated(P.gate_lin)) return;
   __shared__ double red[1024];
   if ((int)blockIdx.x < NPART + 2)
     reduce_parts_block(blockIdx.x, parts, P.nc, nullptr, 0, out, nullptr, red, hout);
@@ -1268,10 +1254,9 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
                                                     double *__restrict__ g, double *__restrict__ colnorm,
                                                     const double *__restrict__ red,
                                                     const double *__restrict__ x,
-                                                    double *__restrict__ out, const int *gate,
+                                                    double *__restrict__ out,
                                                     double *__restrict__ hout, const double *__restrict__ scale,
                                                     double dmin, double dmax, double *__restrict__ diag) {
-  if (gated(gate)) return;
   __shared__ double rs[6][256];
   __shared__ int last;
   const int t = threadIdx.x;
@@ -1539,16 +1524,15 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 }
 
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
-                         hipStream_t s, const int *flag, const int *gate, double *hout) {
-  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, gate,
-                     hout);
+                         hipStream_t s, const int *flag, double *hout) {
+  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, hout);
 }
 
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
                        double *out, hipStream_t s, double *hout, const LmDiagArgs *ld) {
   // out[0..5] results, out[7] the block count (zero between launches), out[8..] the per-block partials
   hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, P.f_own, g,
-                     colnorm, red, x, out, P.gate_lin, hout, ld ? ld->scale : nullptr, ld ? ld->dmin : 0.0,
+                     colnorm, red, x, out, hout, ld ? ld->scale : nullptr, ld ? ld->dmin : 0.0,
                      ld ? ld->dmax : 0.0, ld ? ld->diag : nullptr);
 }
 

@@ -328,42 +328,9 @@ struct arslam_lm {
   int rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
 
-  // ---- device-resident LM loop (lm_device.hip) ----
-  static constexpr int kLoopDepth = 2;   // iterations enqueued ahead of the one the host waits for
-  static constexpr size_t kLmHead = offsetof(arslam::LmDevState, gate_step);   // done .. n_iters
-  DevBuf<arslam::LmDevState> d_lmst;
-  int *h_lmhead = nullptr;   // pinned: per slot, the state's head after that iteration
-  hipEvent_t ev_loop[kLoopDepth] = {}, ev_dom[kLoopDepth][2] = {};
-  // the captured iteration: one graph, or (kernel_timing) three -- before the
-  // factorization, the factorization, after it -- with the timing events
-  // recorded on the stream between their launches
-  hipGraphExec_t loop_exec[3] = {};
-  // what a captured iteration baked into its kernel arguments
-  struct GraphKey {
-    long epoch = -1;
-    arslam::LmDevConsts c{};
-    int workgroups = 0, timing = 0;
-    double *x = nullptr;
-    unsigned long long indefinite = 0;
-  } loop_key;
-  long problem_epoch = 0;    // bumped by every change of the device problem's structure
-  bool device_loop_eligible() const;
-  arslam::LmDevConsts lm_consts() const;
-  // part 0: exec reset .. Schur (.. test hook), 1: k_factor_dag, 2: the rest; -1 all
-  void enqueue_iteration(int part, const arslam::LmDevConsts &c);
-  int run_device_loop(arslam_lm_summary *s, arslam::LmDevState &init);
-
   ~arslam_lm() {
     for (auto &t : timers) t.destroy();
     for (auto e : upd_events) (void)hipEventDestroy(e);
-    for (auto g : loop_exec)
-      if (g) (void)hipGraphExecDestroy(g);
-    for (int q = 0; q < kLoopDepth; ++q) {
-      if (ev_loop[q]) (void)hipEventDestroy(ev_loop[q]);
-      for (auto e : ev_dom[q])
-        if (e) (void)hipEventDestroy(e);
-    }
-    if (h_lmhead) (void)hipHostFree(h_lmhead);
     if (ev_sync) (void)hipEventDestroy(ev_sync);
     arslam::llt_plan_free(plan);
     if (comm) (void)ncclCommDestroy(comm);
@@ -397,6 +364,30 @@ struct arslam_lm {
                              op == ARSLAM_OP_SUM ? ncclSum : ncclMax, comm, stream));
   }
   void allreduce(double *buf, size_t count, int op) { allreduce_any(buf, count, ARSLAM_DT_F64, op); }
+
+  // Every rank derives the split itself (no structure is exchanged), so ranks
+  // that disagree -- a rank-dependent environment, a different problem --
+  // would issue mismatched collectives and hang.  One all-reduce (MAX of h and
+  // of -h, 52-bit hash of the owner maps) proves they agree before the first step.
+  DevBuf<double> d_split_hash;
+  void check_same_split(const arslam::RankSplit &sp) {
+    unsigned long long h = 1469598103934665603ull;
+    auto mix = [&](long v) { h = (h ^ (unsigned long long)v) * 1099511628211ull; };
+    for (int v : sp.col_owner) mix(v);
+    for (int v : sp.cap_owner) mix(v);
+    mix(sp.n_active);
+    const double hv[2] = {(double)(h >> 12), -(double)(h >> 12)};   // exact in a double
+    ensure_stream();
+    d_split_hash.alloc(2);
+    HIP_CHECK(hipMemcpyAsync(d_split_hash.p, hv, sizeof(hv), hipMemcpyHostToDevice, stream));
+    allreduce(d_split_hash.p, 2, ARSLAM_OP_MAX);
+    double got[2];
+    HIP_CHECK(hipMemcpyAsync(got, d_split_hash.p, sizeof(got), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    fail_if(got[0] != -got[1], ARSLAM_E_COMM,
+            "the ranks derived different capture / tile-column splits (same problem and options on every rank, "
+            "no rank-dependent ARSLAM_* environment)");
+  }
 
   int dag_workgroups = 512;
   static inline bool dag_traced = false;   // debug trace: one per process
@@ -445,6 +436,7 @@ struct arslam_lm {
   std::vector<int> loc_obs_cap, loc_obs_tag;
   std::vector<unsigned char> loc_cap_const;
   double split_top_work = 0.0, split_max_rank_work = 0.0, split_total_work = 0.0;
+  int split_active = 1;   // ranks owning subtrees (RankSplit::n_active)
   // co-visibility of the free tags (a bit matrix, directed edge count as
   // ReducedLayout::n_edges), kept up to date through appends: an appended
   // problem whose graph outgrew the one its elimination order was computed
@@ -605,6 +597,8 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
     split_top_work = split.top_work;
     split_max_rank_work = split.max_rank_work;
     split_total_work = split.total_work;
+    split_active = split.n_active;
+    check_same_split(split);
     for (int c = 0; c < p->n_cap; ++c)
       if (split.cap_owner[c] == rank) own_caps.push_back(c);
     // this rank's problem: its captures (ascending), their observations, every tag
@@ -845,7 +839,6 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.contrib = u_contrib; P.n_dest = n_dest; P.jrows = d_jrows.p; P.cap_ui = d_cap_ui.p;
   P.gather_items = u_gather_items; P.gather_splits = u_gather_splits; P.gather_part = d_gather_part.p;
   P.n_items = n_items; P.n_splits = n_splits;
-  ++problem_epoch;   // (captured LM iterations hold the old arrays)
   const double tu2 = prof ? now_s() : 0.0;
   // (no sync: the copy reads the arena's page-locked image, which stays
   // untouched until the next upload -- after this solve's syncs)
@@ -1133,177 +1126,6 @@ void print_row(const arslam_lm_iteration &it) {
 
 }  // namespace
 
-// ---- device-resident LM loop ----
-bool arslam_lm::device_loop_eligible() const {
-  static const bool debug_trace = std::getenv("ARSLAM_DAG_TRACE") || std::getenv("ARSLAM_FACTOR_HASH");
-  return opt.device_loop && nranks == 1 && has_f && opt.factor_executor == 1 && !iter_cb &&
-         !opt.update_state_every_iteration && !opt.minimizer_progress_to_stdout && !opt.phase_timing &&
-         !debug_trace;
-}
-
-arslam::LmDevConsts arslam_lm::lm_consts() const {
-  arslam::LmDevConsts c{};
-  c.function_tolerance = opt.function_tolerance;
-  c.parameter_tolerance = opt.parameter_tolerance;
-  c.gradient_tolerance = opt.gradient_tolerance;
-  c.min_relative_decrease = opt.min_relative_decrease;
-  c.min_radius = opt.min_trust_region_radius;
-  c.max_radius = opt.max_trust_region_radius;
-  c.max_num_iterations = opt.max_num_iterations;
-  c.max_invalid = opt.max_num_consecutive_invalid_steps;
-  return c;
-}
-
-// One LM iteration on the stream, decided on the device: the step (the host
-// loop's sequence, gated by gate_step, the radius read from the state), its
-// evaluation, the accepted candidate into x, the linearization there (gated
-// by gate_lin), the iteration's record and the best point.
-void arslam_lm::enqueue_iteration(int part, const arslam::LmDevConsts &c) {
-  arslam::LmDevState *st = d_lmst.p;
-  arslam::DevProblem Q = P;
-  Q.gate_lin = &st->gate_lin;
-  Q.gate_step = &st->gate_step;
-  Q.radius_dev = &st->radius;
-  if (part <= 0) {
-    arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, opt.min_lm_diagonal, opt.max_lm_diagonal, d_diag.p, d_yF.p, nR};
-    ld.gate = &st->gate_step;
-    ld.keep_diag = &st->keep_diag;
-    arslam::launch_exec_reset(plan, d_flag.p, stream, &ld);
-    arslam::launch_schur(Q, x, d_scale.p, d_diag.p, 0.0, Sp, stream, true, plan.n_tiles);
-    if (dbg_indefinite_mask)   // (test hook)
-      arslam::launch_lm_debug_indefinite(Q, Sp, P.cam_row >= 0 ? P.cam_row : nR - 1, dbg_indefinite_mask, st,
-                                         stream);
-  }
-  if (part < 0 || part == 1)
-    arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, -1,
-                                 &st->gate_step);
-  if (part < 0 || part == 2) {
-    arslam::launch_dense_back_solve_dag(plan, Sp, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false,
-                                        &st->gate_step);
-    arslam::launch_update_f(Q, x, d_scale.p, d_yF.p, xc, d_fparts.p, stream);
-    arslam::launch_backsub(Q, x, d_scale.p, d_diag.p, 0.0, d_yF.p, xc, d_parts.p, stream, has_f, true);
-    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p, &st->gate_step);
-    arslam::launch_lm_decide(st, d_red.p, c, stream);
-    arslam::launch_lm_copy(x, xc, n, &st->accept, stream);
-    arslam::launch_linearize(Q, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
-    arslam::launch_lin_reduce(Q, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream);
-    arslam::launch_slot_norms(Q, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream);
-    arslam::launch_lm_finalize(st, d_red.p, c, stream);
-    arslam::launch_lm_copy(d_xbest.p, x, n, &st->copy_best, stream);
-  }
-}
-
-// Iterations 1, 2, ... with the decisions on the device: kLoopDepth
-// iterations stay enqueued (one hipGraph launch each), the host waits for the
-// oldest, reads its `done` and enqueues the next; iterations enqueued past
-// the end return at their gates.  Returns the ARSLAM_LOOP_* used.
-int arslam_lm::run_device_loop(arslam_lm_summary *s, arslam::LmDevState &init) {
-  const arslam::LmDevConsts c = lm_consts();
-  d_lmst.alloc(1);
-  if (!h_lmhead) HIP_CHECK(hipHostMalloc(&h_lmhead, kLoopDepth * kLmHead, hipHostMallocDefault));
-  for (int q = 0; q < kLoopDepth; ++q) {
-    if (!ev_loop[q]) HIP_CHECK(hipEventCreateWithFlags(&ev_loop[q], hipEventDisableTiming));
-    for (auto &e : ev_dom[q])
-      if (!e) HIP_CHECK(hipEventCreate(&e));
-  }
-  HIP_CHECK(hipMemcpyAsync(d_lmst.p, &init, offsetof(arslam::LmDevState, iters), hipMemcpyHostToDevice, stream));
-  arslam::launch_lm_start(d_lmst.p, stream);
-  // the captured iteration, kept while the problem, the options and the
-  // buffers it names are unchanged
-  const int nparts = opt.kernel_timing ? 3 : 1;
-  static const bool no_graphs = std::getenv("ARSLAM_LOOP_NOGRAPH") != nullptr;   // debug A/B
-  bool graphs = !no_graphs;
-  GraphKey key;
-  key.epoch = problem_epoch;
-  key.c = c;
-  key.workgroups = dag_workgroups;
-  key.timing = opt.kernel_timing;
-  key.x = x;
-  key.indefinite = dbg_indefinite_mask;
-  const GraphKey &k = loop_key;
-  if (graphs && !(loop_exec[0] && k.epoch == key.epoch && !std::memcmp(&k.c, &key.c, sizeof(c)) &&
-        k.workgroups == key.workgroups && k.timing == key.timing && k.x == key.x && k.indefinite == key.indefinite)) {
-    for (auto &g : loop_exec) {
-      if (g) (void)hipGraphExecDestroy(g);
-      g = nullptr;
-    }
-    loop_key = GraphKey{};
-    for (int part = 0; part < nparts && graphs; ++part) {
-      hipGraph_t g = nullptr;
-      if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-        graphs = false;
-        break;
-      }
-      enqueue_iteration(nparts == 1 ? -1 : part, c);
-      const hipError_t e1 = hipStreamEndCapture(stream, &g);
-      const hipError_t e2 = e1 == hipSuccess ? hipGraphInstantiate(&loop_exec[part], g, nullptr, nullptr, 0) : e1;
-      if (g) (void)hipGraphDestroy(g);
-      if (e2 != hipSuccess) {
-        (void)hipGetLastError();
-        for (auto &ge : loop_exec) {
-          if (ge) (void)hipGraphExecDestroy(ge);
-          ge = nullptr;
-        }
-        graphs = false;
-      }
-    }
-    if (graphs) loop_key = key;
-  }
-  const int H = (int)(kLmHead / sizeof(int));
-  auto enqueue = [&](int q) {
-    for (int part = 0; part < nparts; ++part) {
-      if (nparts == 3 && part == 1) HIP_CHECK(hipEventRecord(ev_dom[q][0], stream));
-      if (graphs) HIP_CHECK(hipGraphLaunch(loop_exec[part], stream));
-      else enqueue_iteration(nparts == 1 ? -1 : part, c);
-      if (nparts == 3 && part == 1) HIP_CHECK(hipEventRecord(ev_dom[q][1], stream));
-    }
-    HIP_CHECK(hipMemcpyAsync(h_lmhead + q * H, d_lmst.p, kLmHead, hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipEventRecord(ev_loop[q], stream));
-  };
-  // every iteration computes at most one step: the minimizer ends within
-  // max_num_iterations of them; the rest is the in-flight margin
-  const int cap = opt.max_num_iterations + 2 * kLoopDepth + 2;
-  int launched = 0, completed = 0, seen_solves = 0;
-  for (; launched < kLoopDepth; ++launched) enqueue(launched);
-  for (;;) {
-    const int q = completed % kLoopDepth;
-    hipError_t e;
-    while ((e = hipEventQuery(ev_loop[q])) == hipErrorNotReady) {
-    }
-    HIP_CHECK(e);
-    const volatile int *hd = h_lmhead + q * H;
-    const int solves = hd[offsetof(arslam::LmDevState, num_linear_solves) / sizeof(int)];
-    if (opt.kernel_timing && solves > seen_solves) {   // this iteration factored: its k_factor_dag launch
-      float ms = 0.f;
-      HIP_CHECK(hipEventElapsedTime(&ms, ev_dom[q][0], ev_dom[q][1]));
-      dom_ms += ms;
-      dom_launches++;
-      dom_flops += plan.total_factor_flops;
-    }
-    seen_solves = solves;
-    ++completed;
-    if (hd[offsetof(arslam::LmDevState, done) / sizeof(int)]) break;
-    fail_if(launched >= cap, ARSLAM_E_DEVICE, "device LM loop: no termination within max_num_iterations");
-    enqueue(launched % kLoopDepth);
-    ++launched;
-  }
-  HIP_CHECK(hipStreamSynchronize(stream));   // (the iterations past the end, gated)
-  std::unique_ptr<arslam::LmDevState> hst(new arslam::LmDevState);   // (~90 KB: not on the stack)
-  arslam::LmDevState &st = *hst;
-  HIP_CHECK(hipMemcpy(&st, d_lmst.p, offsetof(arslam::LmDevState, iters), hipMemcpyDeviceToHost));
-  if (st.n_iters > 0)
-    HIP_CHECK(hipMemcpy(st.iters, d_lmst.p->iters, st.n_iters * sizeof(arslam_lm_iteration), hipMemcpyDeviceToHost));
-  if (st.fault) throw Error(ARSLAM_E_DEVICE, executor_fault_message(st.fault_flag, rank, st.it.iteration));
-  s->num_successful_steps += st.num_successful;
-  s->num_unsuccessful_steps += st.num_unsuccessful;
-  s->num_linear_solves += st.num_linear_solves;
-  for (int i = 0; i < st.n_iters && s->n_iters <= ARSLAM_LM_MAX_ITERS; ++i) s->iters[s->n_iters++] = st.iters[i];
-  s->termination = st.termination;
-  s->rule = st.rule;
-  init.minimum_cost = st.minimum_cost;
-  return graphs ? ARSLAM_LOOP_GRAPH : ARSLAM_LOOP_DEVICE;
-}
-
 void arslam_lm::solve(arslam_lm_summary *s) {
   fail_if(!loaded, ARSLAM_E_STATE, "no problem loaded");
   const arslam_lm_options &o = opt;
@@ -1445,28 +1267,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     return false;
   };
 
-  if (device_loop_eligible()) {
-    // iteration 0 as the host loop records it, then the device decides
-    if (!finalize()) {
-      arslam::LmDevState init{};
-      init.radius = radius;
-      init.decrease_factor = decrease_factor;
-      init.x_cost = x_cost;
-      init.fixed_cost = fixed_cost;
-      init.minimum_cost = minimum_cost;
-      init.gmax = gmax;
-      init.gnorm = gnorm;
-      init.x_norm = x_norm;
-      init.prev_gmax = prev_gmax;
-      init.prev_gnorm = prev_gnorm;
-      init.it = it;
-      init.t0_s = now_s() - t_start;
-      s->lm_loop = run_device_loop(s, init);
-      minimum_cost = init.minimum_cost;
-    } else {
-      s->lm_loop = ARSLAM_LOOP_DEVICE;
-    }
-  } else for (;;) {
+  for (;;) {
     // the stop rules that do not read the pending linearization: decided now
     // (after reading it), so no step is computed past them
     const bool stop_rule = it.iteration >= o.max_num_iterations || radius <= o.min_trust_region_radius;
@@ -1623,7 +1424,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     timers[PH_COST].start(stream);
     h_step.alloc(16);
     // (one rank: the scalars are also stored straight into the page-locked h_step)
-    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p, nullptr,
+    arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p,
                                 nranks == 1 ? h_step.p : nullptr);
     if (nranks > 1) {
       // candidate cost, fixed, model change, capture step^2 by sum; the
@@ -1747,6 +1548,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->split_top_work = split_top_work;
   s->split_max_rank_work = split_max_rank_work;
   s->split_total_work = split_total_work;
+  s->n_active_ranks = nranks > 1 ? split_active : 1;
 }
 
 // ===========================================================================
@@ -1810,7 +1612,6 @@ int arslam_lm_options_init(arslam_lm_options *o) {
   o->kernel_timing = 0;
   o->factor_executor = 1;
   o->phase_timing = 0;
-  o->device_loop = 0;   // (measured slower than the host loop: DESIGN.md section 6)
   return ARSLAM_OK;
 }
 

@@ -48,7 +48,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
-           "arslam_debug_dag_simulate", "arslam_debug_dag_fault_detail",
+           "arslam_debug_dag_simulate", "arslam_debug_dag_fault_detail", "arslam_debug_box_fingerprint",
            "arslam_debug_rank_split", "arslam_debug_gather_extend",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
@@ -66,7 +66,6 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int,
 SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = 0, 1, 2
 ELIM_AUTO, ELIM_CAPTURES, ELIM_TAGS = 0, 1, 2   # arslam_lm_options.elimination
 SETUP_LOAD, SETUP_VALUES, SETUP_APPEND = 0, 1, 2   # arslam_lm_summary.setup_kind
-LOOP_HOST, LOOP_DEVICE, LOOP_GRAPH = 0, 1, 2         # arslam_lm_summary.lm_loop
 _ip = C.POINTER(C.c_int)
 _up = C.POINTER(C.c_ubyte)
 
@@ -92,7 +91,7 @@ class Options(C.Structure):
                 ("update_state_every_iteration", C.c_int),
                 ("device", C.c_int), ("cholesky_skip_zero_tiles", C.c_int),
                 ("reduced_ordering", C.c_int), ("kernel_timing", C.c_int), ("factor_executor", C.c_int),
-                ("phase_timing", C.c_int), ("device_loop", C.c_int)]
+                ("phase_timing", C.c_int)]
 
 
 class Iteration(C.Structure):
@@ -130,8 +129,8 @@ class Summary(C.Structure):
                 ("split_top_work", C.c_double), ("split_max_rank_work", C.c_double),
                 ("split_total_work", C.c_double), ("t_factor_own_ms", C.c_double),
                 ("t_factor_top_ms", C.c_double),
-                ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1)), ("lm_loop", C.c_int),
-                ("setup_phase_s", C.c_double * 5), ("comm_calls", C.c_long)]
+                ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1)),
+                ("setup_phase_s", C.c_double * 5), ("comm_calls", C.c_long), ("n_active_ranks", C.c_int)]
 
     def to_dict(self):
         its = [{f: getattr(self.iters[i], f) for f, _ in Iteration._fields_}
@@ -525,6 +524,15 @@ def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const
     _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
                                            tag_row.ctypes.data_as(_ip)))
     return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]
+
+
+def box_fingerprint(device=0):
+    """The device's hand-off round trips (arslam_debug_box_fingerprint), a few ms of GPU time:
+    the kind of MI355X box a measurement ran on."""
+    out = (C.c_double * 6)()
+    _check(lib().arslam_debug_box_fingerprint(int(device), out))
+    return {"cas_poll_ns": out[0], "sc1_load_ns": out[1], "wt_store_ack_ns": out[2],
+            "pingpong_ns": out[3], "pingpong_xcc": [int(out[4]), int(out[5])]}
 
 
 def debug_dag_simulate(g, n_workers, seed=1, policy=0):

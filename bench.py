@@ -13,11 +13,18 @@ resident initial state.
                  timed solves / wall time of the K solves (max over ranks)
   ms_per_step  = ms-to-converged of one solve
 
-Multi-GPU (torchrun, one process per GPU): every rank loads the whole
-problem and the solver splits the reduced system's elimination tree below its
-top separators; each rank factors its own subtrees (and owns their captures),
-then the top columns' tiles are summed over RCCL and factored on every rank
-(the path has a real exchange step, and total work is fixed: strong scaling).
+Multi-GPU, one process per GPU: `python bench.py --gpus N` starts the N rank
+processes itself (before anything touches the GPU; 127.0.0.1 rendezvous), or
+run it under torchrun (`python -m torch.distributed.run --nnodes=1
+--nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N`),
+which sets WORLD_SIZE.  Every rank loads the whole problem and the solver
+splits the reduced system's elimination tree below its top separators; each
+rank factors its own subtrees (and owns their captures), then the top
+columns' tiles are summed over RCCL and factored on every rank (the path has
+a real exchange step, and total work is fixed: strong scaling).
+`--transport callback` runs the same exchange through the host all-reduce
+callback over gloo, every rank on the one GPU there is (a test transport: it
+checks the multi-rank path end to end on a 1-GPU box, it measures no scaling).
 
 The JSON line also carries the dominant kernel's roofline (the MFMA fp64
 trailing update of the reduced-system Cholesky, timed with HIP events around
@@ -192,7 +199,8 @@ def bench_localize(args, world, rank, side=False):
            "mean_iterations_per_query": q_iters / b.n_query,
            "roofline": {"bound": "valu", "kernel": "k_localize (two queries per wave)",
                         "achieved": achieved_valu, "peak": valu_peak, "unit": "G VALU-instructions/s",
-                        "frac": achieved_valu / valu_peak if achieved_valu else None, "traffic": None,
+                        "frac": achieved_valu / valu_peak if achieved_valu else None,
+                        "traffic": load_pmc_traffic("k_localize<2, 32>"), "traffic_source": PMC_PROFILE,
                         "avg_launch_us": avg_kernel_s * 1e6, "valu_instructions_per_launch": valu,
                         "hbm_view": {"achieved_GBps": achieved, "peak_GBps": HBM_PEAK_GBS,
                                      "frac": achieved / HBM_PEAK_GBS,
@@ -226,21 +234,95 @@ def load_pmc_localize():
         return None
 
 
-# the PMC pass (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md) of the commit this bench line
-# measures: each profile round writes its own directory, and this names the latest
-PMC_PROFILE = os.path.join("profiles", "r04b", "pmc_hbm_bytes.json")
+# the PMC passes of the commit this bench line measures (each profile round writes its own
+# directory; these name the latest): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md,
+# tools/pmc_bench.sh) and the dominant kernel's MFMA utilisation (tools/pmc_mfma.sh)
+PMC_PROFILE = os.path.join("profiles", "r05", "pmc_hbm_bytes.json")
+PMC_MFMA = os.path.join("profiles", "r05", "pmc_mfma.json")
 
 
-def load_pmc_traffic():
-    """Per-launch HBM bytes of the dominant kernel from the latest committed PMC pass, if any."""
+def _load_json(rel):
     try:
-        with open(os.path.join(ROOT, PMC_PROFILE)) as f:
-            d = json.load(f)
-        if "hbm_bytes_per_launch" in d:
-            return d["hbm_bytes_per_launch"]
-        return d["kernels"]["k_factor_dag"]["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError, TypeError):
+        with open(os.path.join(ROOT, rel)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
         return None
+
+
+def load_pmc_traffic(kernel="k_factor_dag"):
+    """Per-launch HBM bytes of a kernel from the latest committed PMC pass, if any."""
+    d = _load_json(PMC_PROFILE)
+    try:
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (KeyError, TypeError):
+        return None
+
+
+def load_pmc_mfma():
+    """k_factor_dag's MFMA busy fraction and issued fp64 MFMA flops from the latest PMC pass."""
+    d = _load_json(PMC_MFMA)
+    if not d:
+        return {}
+    return {k: d.get(k) for k in ("mfma_busy_frac", "mfma_busy_frac_at_2p4ghz", "effective_clock_ghz",
+                                  "mfma_f64_flops_per_launch", "mfma_f64_tflops", "mean_us")}
+
+
+def compulsory_factor_bytes(n_factor_tiles, n_reduced):
+    """The least HBM traffic of one factorization: every factor tile read once (as assembled) and
+    written once (as L), and each tile column's L_kk, L_kk^{-1} (64x64) and its four 16x16 block
+    inverses written once -- no operand re-reads at all."""
+    T = -(-(int(n_reduced) + 1) // 64)
+    tile = 64 * 64 * 8
+    return 2 * int(n_factor_tiles) * tile + T * (2 * tile + 4 * 16 * 18 * 8)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` without a launcher: build first (CPU only), then start N rank processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each), forward rank 0's line and
+    return the worst exit status.  This process never touches the GPU, so the children are plain
+    child processes (no exec from a process that initialised HIP)."""
+    import subprocess
+    if not args.launch_check:
+        from ar_slam_amd import build
+        build.build()
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, cwd=ROOT))
+    out = procs[0].stdout.read().decode()
+    rcs = [p.wait() for p in procs]
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def launch_check(world, rank):
+    """`--launch-check` (CPU, no GPU): the ranks meet over gloo and rank 0 prints who came -- the
+    launcher and rendezvous of the multi-rank bench without a solve (tests/test_bench_launch.py)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.zeros(world, dtype=torch.int64)
+    t[rank] = rank + 1
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "world_size": world,
+                          "ranks": [int(v) - 1 for v in t.tolist()],
+                          "env": {k: os.environ.get(k) for k in ("MASTER_ADDR", "LOCAL_WORLD_SIZE")}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -254,8 +336,12 @@ def main():
     ap.add_argument("--no-localize", action="store_true", help="skip the cfg5 batched-localize side key")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--device-loop", action="store_true",
-                    help="LM decisions on the device, iterations enqueued ahead as hipGraphs (measured slower)")
+    ap.add_argument("--transport", choices=("rccl", "callback"), default="rccl",
+                    help="multi-rank exchange: RCCL (one GPU per rank) or the host all-reduce callback over gloo "
+                         "(test transport: every rank on the one GPU there is)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="(tests) start the ranks and meet over gloo, no GPU, no solve")
+    ap.add_argument("--no-fingerprint", action="store_true", help="skip the in-process box fingerprint")
     ap.add_argument("--skip-zero-tiles", type=int, default=1)
     ap.add_argument("--ordering", type=int, default=2, help="0 natural, 1 RCM, 2 nested dissection")
     ap.add_argument("--executor", type=int, default=1, help="0 level launches, 1 persistent task graph")
@@ -264,15 +350,27 @@ def main():
                          "only this workload's launches; the setup then includes the runtime start)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: measuring {world} ranks", file=sys.stderr)
+    if args.launch_check:
+        launch_check(world, rank)
+        return
     # build (if stale) before anything touches the GPU; ranks serialize on the build lock
     from ar_slam_amd import build
     build.build()
     import torch
     import torch.distributed as dist
-    if world > 1:
+    callback = world > 1 and args.transport == "callback"
+    device = local_rank
+    if callback:   # every rank on the one GPU there is (device_count does not initialise HIP here)
+        device = local_rank % max(1, torch.cuda.device_count())
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    elif world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
@@ -287,13 +385,17 @@ def main():
     # reduced system's elimination tree: each rank owns the captures of its subtrees)
     part = dict(camera=g.camera, cap=g.cap, tag=g.tag, obs_cap=g.obs_cap, obs_tag=g.obs_tag, corners=g.corners)
     comm = None
-    if world > 1:
+    if callback:
+        def allreduce(a, op):
+            dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+        comm = (rank, world, allreduce)
+    elif world > 1:
         obj = [lm.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = (rank, world, obj[0])
-    opts = dict(device=local_rank, kernel_timing=0 if args.no_kernel_timing else 1,
+    opts = dict(device=device, kernel_timing=0 if args.no_kernel_timing else 1,
                 cholesky_skip_zero_tiles=args.skip_zero_tiles, reduced_ordering=args.ordering,
-                factor_executor=args.executor, device_loop=1 if args.device_loop else 0)
+                factor_executor=args.executor)
     # the timed solves record no per-phase events (each costs GPU time between
     # kernels); the dominant kernel's own events stay on for the roofline.
     # Construction = the cold per-problem setup a Ceres Solve's preprocessor
@@ -303,8 +405,9 @@ def main():
     # on first launch, its stream and page-locked buffers) is paid by a small
     # solve first and reported on its own (runtime_init_s): a SLAM node pays it
     # once, every problem after it pays the setup below
+    torch.cuda.set_device(device)
     torch.cuda.synchronize()
-    runtime_init_s = None if args.no_runtime_warmup else lm.warm_up(local_rank)
+    runtime_init_s = None if args.no_runtime_warmup else lm.warm_up(device)
     torch.cuda.synchronize()
     t_setup = time.perf_counter()
     rp = lm.ResidentProblem(**part, comm=comm, phase_timing=0, **opts)
@@ -326,7 +429,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if callback else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -348,10 +451,19 @@ def main():
         kname = ("k_factor_dag (reduced-system Cholesky, persistent task graph: POTRF + TRSM + "
                  "trailing updates on v_mfma_f64_16x16x4_f64)") if args.executor == 1 else \
             "k_update (reduced-system Cholesky trailing update, v_mfma_f64_16x16x4_f64)"
+        traffic = load_pmc_traffic("k_factor_dag" if args.executor == 1 else "k_update")
+        compulsory = compulsory_factor_bytes(last["n_factor_tiles"], last["n_reduced"])
+        mf = load_pmc_mfma() if args.executor == 1 else {}
         roofline = {"bound": "mfma", "kernel": kname,
                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_pmc_traffic(),
+                    "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                     "traffic_source": PMC_PROFILE,
+                    # PMC bytes / the least traffic of the factorization (every tile read and
+                    # written once): > 1 is operand re-reads and the level-ordered target updates
+                    "compulsory_bytes": compulsory,
+                    "traffic_ratio": traffic / compulsory if traffic else None,
+                    "mfma_busy_frac": mf.get("mfma_busy_frac"),
+                    "mfma_counters": dict(mf, source=PMC_MFMA) if mf else None,
                     "avg_launch_us": avg_ms * 1e3,
                     "flops_per_launch": scalar_flops,
                     "flops_basis": "scalar Cholesky of the reduced system's real rows in the chosen order "
@@ -380,7 +492,8 @@ def main():
             "config": {"workload": f"{args.config}: {g.n_cap} captures / {g.n_tag} tags / "
                                    f"{g.n_obs} observations (k=8), one full LM solve per step",
                        "n_obs": int(g.n_obs), "n_reduced": int(last["n_reduced"]),
-                       "parallelism": f"subtree split x{world} (RCCL all-reduce of the top tiles)"
+                       "parallelism": (f"subtree split x{world} ("
+                                       + ("host-callback" if callback else "RCCL") + " all-reduce of the top tiles)")
                                       if world > 1 else "single GPU"},
             "ms_to_converged": 1e3 * elapsed / args.steps,
             # the cold setup of the problem (first load: ordering, plan, upload), outside the timed
@@ -394,20 +507,26 @@ def main():
             "final_rms_px": last["final_rms_px"],
             "termination": f"{last['termination']} ({last['rule']})",
             "lm_iterations_per_solve": last["num_linear_solves"],
-            "lm_loop": {0: "host", 1: "device", 2: "device, one hipGraph per iteration"}.get(last.get("lm_loop"), "?"),
             "reduced_system": {"rows": int(last["n_reduced"]), "factor_tiles": int(last["n_factor_tiles"]),
                                "etree_levels": int(last["n_levels"]),
                                "ordering": ["natural", "RCM", "nested dissection"][args.ordering],
                                "executor": ["level launches", "persistent task graph"][args.executor],
                                "skip_zero_tiles": bool(args.skip_zero_tiles)},
             "comm_mb_per_lm_iteration": last["comm_bytes"] / max(last["num_linear_solves"], 1) / 1e6,
-            "split": {k: last[k] for k in ("n_ranks", "n_owned_captures", "n_top_tiles", "split_top_work",
-                                           "split_max_rank_work", "split_total_work")},
+            "split": dict({k: last[k] for k in ("n_ranks", "n_owned_captures", "n_top_tiles", "split_top_work",
+                                                "split_max_rank_work", "split_total_work")},
+                          active_ranks=last["n_active_ranks"]),
+            "transport": ("host all-reduce callback over gloo, ranks sharing cuda:" + str(device) +
+                          " (test transport: no scaling measurement)") if callback else
+                         ("RCCL, one GPU per rank" if world > 1 else None),
             "phase_ms_per_solve": {k: phased[f"t_{k}_ms"] for k in
                                    ("linearize", "schur", "cholesky", "solve", "backsub", "cost")},
             "roofline": roofline,
             "cpu_baseline": None,
+            "library": lm.library_info(),
         }
+        if not args.no_fingerprint:   # which kind of MI355X box this line ran on (a few ms, untimed)
+            out["box_fingerprint"] = lm.box_fingerprint(device)
         if world == 1 and not args.no_incremental and args.config == "cfg3":
             print("bench: incremental cfg2 flow", file=sys.stderr, flush=True)
             out["incremental_cfg2"] = bench_incremental("cfg2")

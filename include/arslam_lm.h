@@ -105,13 +105,6 @@ typedef struct {
   int phase_timing;                  /* 1: HIP events around each phase of the step (summary
                                         t_*_ms; host loop only); 0 (default): none (each event
                                         record costs a few microseconds of GPU time) */
-  int device_loop;                   /* 1: the LM decisions (step acceptance, radius, termination)
-                                        run on the device and the host enqueues iterations ahead,
-                                        one hipGraph launch each, whenever nothing needs the host
-                                        between iterations (one rank, no iteration callback, no
-                                        per-iteration write-back or progress table, phase_timing
-                                        = 0); 0 (default): the host decides each step, one round
-                                        trip per step -- measured faster on MI355X */
 } arslam_lm_options;
 
 /* ceres::IterationSummary subset */
@@ -164,17 +157,14 @@ typedef struct {
   double t_factor_top_ms;       /*   phase 1 (the top), summed over the solve (phase_timing = 1) */
   int n_iters;                  /* entries in iters[], iteration 0 included */
   arslam_lm_iteration iters[ARSLAM_LM_MAX_ITERS + 1];
-  int lm_loop;                  /* ARSLAM_LOOP_*: which loop drove the minimizer */
   double setup_phase_s[5];      /* the last full load (ARSLAM_SETUP_LOAD): problem structure (Ceres'
                                    e-block rule + host problem), elimination order (reduced layout; several
                                    ranks: + the split), tile plan + task graph, Schur gather plan + upload,
                                    the rest (stream, co-visibility bookkeeping) */
   long comm_calls;              /* multi-rank: collectives this rank made during the solve */
+  int n_active_ranks;           /* ranks that own subtrees of the split (the others own only captures that
+                                   see top tags alone); 1 on one rank */
 } arslam_lm_summary;
-
-/* summary.lm_loop: the host decided every step; the device decided, kernels
- * enqueued per iteration; the device decided, one hipGraph launch per iteration */
-enum { ARSLAM_LOOP_HOST = 0, ARSLAM_LOOP_DEVICE = 1, ARSLAM_LOOP_GRAPH = 2 };
 
 /* Whole problem in struct-of-arrays form (bulk / benchmark path). */
 typedef struct {

@@ -107,6 +107,13 @@ int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int ski
  * 1-3 adversarial orders; + 16 drops the cap on claimed continuations in
  * flight, which the protocol relies on).  *ok = 1 if every task finished, 0 on
  * a deadlock. */
+/* The memory round trips of the persistent executor's hand-offs on this
+ * device, measured in a few milliseconds (one lane each): out = {never-matching
+ * CAS poll (ns, dependent chain), agent-scope sc1 load (ns, dependent chain),
+ * write-through store + its acknowledgement (ns each), workgroup ping-pong
+ * through agent-scope flags (ns per round trip, -1 if it timed out), the two
+ * workgroups' XCC ids}.  device < 0: the current device. */
+int arslam_debug_box_fingerprint(int device, double out[6]);
 int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_workers, unsigned seed, int policy, int *ok);
 int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[8], char *buf, int len);
 

@@ -105,7 +105,8 @@ def _same_on_every_rank(res):
         np.testing.assert_array_equal(r[3], res[0][3])
 
 
-@pytest.mark.parametrize("name,world", [("medium", 2), ("cfg2", 2), ("cfg2", 3), ("cfg2", 4)])
+@pytest.mark.parametrize("name,world", [("medium", 2), ("cfg2", 2), ("cfg2", 3), ("cfg2", 4), ("kvar", 2),
+                                        ("k24", 2)])
 def test_sharded_gpu_solve_matches_oracle(oracle, name, world):
     if torch.cuda.device_count() < 1:
         pytest.skip("no GPU")
@@ -175,3 +176,28 @@ def test_iteration_callback_decision_is_agreed_across_ranks():
     for r in res:
         assert (r[5], r[6]) == ("USER_FAILURE", "user_callback"), r[5:7]
         assert len(r[4]) == 3 and r[4] == res[0][4]
+
+
+def test_bench_launches_its_ranks():
+    """`bench.py --gpus 2` with no launcher environment starts its two rank processes itself and emits
+    ONE line for the job: n_gpus 2, the split over 2 ranks with its active-rank count.  The exchange
+    runs through the host callback over gloo with both ranks on the one GPU of this box (the
+    driver's multi-GPU runs use RCCL, one GPU per rank)."""
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--config", "medium",
+                          "--transport", "callback", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                          "--no-incremental", "--no-localize", "--no-fingerprint"],
+                         capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["split"]["n_ranks"] == 2 and 1 <= d["split"]["active_ranks"] <= 2, d["split"]
+    assert d["value"] > 0 and d["termination"].startswith("CONVERGENCE"), d
+    assert "callback" in d["transport"], d["transport"]

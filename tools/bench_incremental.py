@@ -17,9 +17,7 @@ build.build()
 name = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
 g = synth.config_graph(name)
 # (default options, as a drop-in user gets them; ARSLAM_PHASES=1: per-phase device times)
-# (ARSLAM_DEVICE_LOOP=1: the opt-in device-resident LM loop)
-s = lm.SlamSolver(phase_timing=int(os.environ.get("ARSLAM_PHASES", "0")),
-                  device_loop=int(os.environ.get("ARSLAM_DEVICE_LOOP", "0")))
+s = lm.SlamSolver(phase_timing=int(os.environ.get("ARSLAM_PHASES", "0")))
 s.set_camera(g.camera)
 t0 = time.perf_counter()
 t_add = 0.0
