@@ -59,7 +59,10 @@ int peripheral(int start, const std::vector<std::vector<int>> &adj, const std::v
 }
 
 double nd_beta() {
-  static const double b = std::getenv("ARSLAM_ND_BETA") ? std::atof(std::getenv("ARSLAM_ND_BETA")) : 0.6;   // debug sweeps
+  // (debug sweeps; clamped to [0, 4]: a finite, non-negative weight)
+  static const double b = std::getenv("ARSLAM_ND_BETA")
+                              ? std::min(4.0, std::max(0.0, std::atof(std::getenv("ARSLAM_ND_BETA")) + 0.0))
+                              : 0.6;
   return b;
 }
 
@@ -737,7 +740,9 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
       for (int a = 0; a < 3; ++a) xyz[3L * t + a] = h.x0[3 + 6L * nc + 6L * t + a];
     // leaves of up to 32 tags (192 rows = 3 whole tiles): a smaller dissection
     // would not shorten the elimination tree, only add padding and parts
-    static const int leaf = std::getenv("ARSLAM_ND_LEAF") ? std::atoi(std::getenv("ARSLAM_ND_LEAF")) : 32;   // debug sweeps
+    // (debug sweeps; clamped to [1, 4096])
+    static const int leaf =
+        std::getenv("ARSLAM_ND_LEAF") ? std::min(4096, std::max(1, std::atoi(std::getenv("ARSLAM_ND_LEAF")))) : 32;
     parts = nd_parts(nt, adj, leaf, xyz, fast_order);
   } else {
     std::vector<int> order;

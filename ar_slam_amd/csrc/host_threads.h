@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <exception>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -49,14 +51,38 @@ inline bool host_thread_take() {
 
 inline void host_thread_give() { host_thread_pool().fetch_add(1, std::memory_order_acq_rel); }
 
+// The first exception thrown by any branch of a fork (bad_alloc on a large
+// graph, an ApiError), rethrown on the calling thread once every thread has
+// joined -- an exception must not escape a std::thread (std::terminate), so
+// it reaches the C-ABI's guard as an error code instead.
+struct HostForkError {
+  std::mutex m;
+  std::exception_ptr e;
+  template <class F>
+  void run(F &&f) {
+    try {
+      f();
+    } catch (...) {
+      std::lock_guard<std::mutex> g(m);
+      if (!e) e = std::current_exception();
+    }
+  }
+  void rethrow() {
+    if (e) std::rethrow_exception(e);
+  }
+};
+
 // fn(i) for i in [0, n): on up to n threads (the caller's included) as the
 // budget allows, each index run exactly once; blocks until all are done
 template <class F>
 void host_parallel_for(int n, F &&fn) {
   if (n <= 0) return;
   std::atomic<int> next{0};
+  HostForkError err;
   auto work = [&] {
-    for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(i);
+    err.run([&] {
+      for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(i);
+    });
   };
   std::vector<std::thread> ts;
   for (int k = 1; k < n && host_thread_take(); ++k) ts.emplace_back(work);
@@ -65,16 +91,19 @@ void host_parallel_for(int n, F &&fn) {
     t.join();
     host_thread_give();
   }
+  err.rethrow();
 }
 
 // a() and b() concurrently when a thread is free (a on the new one), else in turn
 template <class A, class B>
 void host_fork2(bool worth_it, A &&a, B &&b) {
   if (worth_it && host_thread_take()) {
-    std::thread t(a);
-    b();
+    HostForkError err;
+    std::thread t([&] { err.run(a); });
+    err.run(b);
     t.join();
     host_thread_give();
+    err.rethrow();
   } else {
     a();
     b();

@@ -59,7 +59,7 @@ constexpr int kSplitMin = 6;   // k-lists longer than this are split
 // us at 192-256; 160 is worse, 810 us; tools/env_bench.sh).
 constexpr int kSimWorkersDefault = 224;
 int sim_workers() {   // (ARSLAM_SIM_WORKERS: debug sweeps)
-  static const int w = std::getenv("ARSLAM_SIM_WORKERS") ? std::max(1, std::atoi(std::getenv("ARSLAM_SIM_WORKERS")))
+  static const int w = std::getenv("ARSLAM_SIM_WORKERS") ? std::min(4096, std::max(1, std::atoi(std::getenv("ARSLAM_SIM_WORKERS"))))
                                                          : kSimWorkersDefault;
   return w;
 }
@@ -736,7 +736,8 @@ RankSplit rank_split(const HostProblem &h, const ReducedLayout &L, int nranks) {
   // captures that see top tags alone).  Tile-task work breaks ties.
   const double kObsUs = 0.003, kTileUs = 32768.0 / 100e3 * 2.0 * (nranks - 1) / nranks;
   int active_forced = 0;
-  if (const char *e = std::getenv("ARSLAM_SPLIT_ACTIVE")) active_forced = std::atoi(e);   // debug: fix A
+  if (const char *e = std::getenv("ARSLAM_SPLIT_ACTIVE"))   // debug: fix A (clamped to [0, nranks]; 0 = the model's)
+    active_forced = std::min(nranks, std::max(0, std::atoi(e)));
   std::vector<char> top(T, 0);
   std::vector<int> frontier;
   for (int k = 0; k < T; ++k)

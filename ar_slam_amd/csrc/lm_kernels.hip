@@ -6,18 +6,26 @@
 // are exactly one wave.  Each lane evaluates its row of the reference's
 // residual (projectCorner, ar_slam_util.cpp:131-172; ArucoReprojectionError
 // :198-211) and the analytic Jacobian into LDS; the
-// wave then forms the capture's normal-equation blocks from LDS:
+// wave then forms the capture's normal-equation blocks:
 //   U_c = E'E + D_c^2 (6x6), W_c = E'F (6 x (1 + 6 n_tags)), F'F, E'r, F'r
-// and scatters its Schur contribution F'F - W'U^{-1}W (lower triangle) and
-// F'r - W'U^{-1}E'r into the dense reduced system with fp64 atomics.
+// and writes its Schur contribution F'F - W'U^{-1}W (lower block triangle)
+// and F'r - W'U^{-1}E'r to its block-packed slab slot; k_schur_gather sums
+// the slab blocks of each destination in capture order into the compact
+// tiles of the reduced system.
 //
-// Every reduction that feeds an LM decision (cost, model cost change, step
-// and gradient norms) is a fixed-order tree, so the control flow is
-// deterministic; only the S/rhs scatter order (atomics) varies run to run.
+// Every sum is fixed-order (no atomics in any of them): the Schur gather, the
+// reductions that feed an LM decision (cost, model cost change, step and
+// gradient norms) and the factorization's split updates, so a solve is
+// bit-identical run to run.
 #include "lm_internal.h"
 #include "projection.h"
 
 #include <cfloat>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "arslam_lm.h"
 #include <cmath>
 
 namespace arslam {
@@ -1448,6 +1456,25 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
                      colnorm, dmin, dmax, diag);
 }
 
+// k_schur<true>'s dynamic-LDS limit, set once per device (the attribute is
+// per device; several host threads may launch first at once): a failure is
+// an error, not a launch that later fails for its LDS size
+void set_schur_big_lds_attribute() {
+  static std::mutex m;
+  static std::vector<char> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) throw ApiError(ARSLAM_E_HIP, "hipGetDevice");
+  std::lock_guard<std::mutex> g(m);
+  if ((int)done.size() <= dev) done.resize(dev + 1, 0);
+  if (done[dev]) return;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_schur<true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)schur_lds_bytes(kMaxSchurBlocks));
+  if (e != hipSuccess)
+    throw ApiError(ARSLAM_E_HIP, std::string("hipFuncSetAttribute(k_schur, dynamic LDS): ") + hipGetErrorString(e));
+  done[dev] = 1;
+}
+
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
                   double radius, double *S, hipStream_t s, bool prep, long zero_tiles, const ExecReset *er) {
   const ExecReset r = er ? *er : ExecReset{};
@@ -1465,12 +1492,7 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
                      diag, radius, S, zero_tiles, r, (const int *)nullptr);
   if (P.n_big_caps > 0) {
     const size_t lds_big = schur_lds_bytes(P.max_blk_per_cap);
-    static bool attr_set = false;   // (dynamic LDS past 64 KiB)
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_schur<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)schur_lds_bytes(kMaxSchurBlocks));
-      attr_set = true;
-    }
+    set_schur_big_lds_attribute();   // (dynamic LDS past 64 KiB: once per device)
     hipLaunchKernelGGL(k_schur<true>, dim3((unsigned)P.n_big_caps), dim3(kWave), lds_big, s, P, scale, diag, radius, S,
                        0L, ExecReset{}, P.big_caps);
   }

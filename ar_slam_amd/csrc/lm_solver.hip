@@ -1058,14 +1058,18 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
 void arslam_lm::write_back(const double *d_src) {
   h_x.alloc(n);   // page-locked: the parameter download is one DMA, no staging
   HIP_CHECK(hipMemcpyAsync(h_x.p, d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
-  if (nranks > 1 && nt) {
-    // each tag from the rank holding it (the others hold stale values of
-    // other ranks' subtree tags): one all-reduce of the held values, zeros elsewhere
+  if (nranks > 1) {
+    // the camera and each tag from the rank holding it (the others hold stale
+    // values of other ranks' subtree tags, and of the camera when its rows are
+    // not in the replicated top -- a split with one active rank and no top):
+    // one all-reduce of the held values, zeros elsewhere
     const long t0 = 3 + 6L * nc;
-    d_lx.alloc(n - t0);
-    arslam::launch_own_copy(P, t0, n - t0, d_src + t0, d_lx.p, stream);
-    allreduce(d_lx.p, n - t0, ARSLAM_OP_SUM);
-    HIP_CHECK(hipMemcpyAsync(h_x.p + t0, d_lx.p, (n - t0) * sizeof(double), hipMemcpyDeviceToHost, stream));
+    d_lx.alloc(3 + n - t0);
+    arslam::launch_own_copy(P, 0, 3, d_src, d_lx.p, stream);
+    arslam::launch_own_copy(P, t0, n - t0, d_src + t0, d_lx.p + 3, stream);
+    allreduce(d_lx.p, 3 + n - t0, ARSLAM_OP_SUM);
+    HIP_CHECK(hipMemcpyAsync(h_x.p, d_lx.p, 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipMemcpyAsync(h_x.p + t0, d_lx.p + 3, (n - t0) * sizeof(double), hipMemcpyDeviceToHost, stream));
   }
   spin_sync();
   const double *h = h_x.p;

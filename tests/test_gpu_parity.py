@@ -212,7 +212,8 @@ def test_appended_problem_keeps_plan_and_matches_a_fresh_load(lm, oracle):
 def test_appended_coupling_in_a_fill_tile_matches_a_fresh_load(lm):
     """An appended capture that couples two known tags never seen together, where their block of
     the reduced system lies in a fill tile of the loaded factor (arslam_lm_debug_tag_pair_tile):
-    the plan is kept (setup_kind APPEND; try_extend marks the tile assembled), and the solve gives
+    the plan is kept (setup_kind APPEND: the pair's tile is a fill tile of the loaded factor, which
+    k_schur clears every step and the extended gather writes into), and the solve gives
     the trace a fresh load of the grown problem gives, to 1e-9.  The appended captures are
     synthetic: a camera above the midpoint of such a pair (the nearest such pairs, up to 3 m apart;
     2-3.3 m up) sees both tags."""
