@@ -274,7 +274,7 @@ extern "C" int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_work
   }
 }
 
-extern "C" int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[8], char *buf, int len) {
+extern "C" int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[9], char *buf, int len) {
   if (!p || !rec || !buf || len <= 0) return ARSLAM_E_INVALID_ARG;
   try {
     const std::string s = arslam::dag_fault_detail(one_rank_plan(p), rec);

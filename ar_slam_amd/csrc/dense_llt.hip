@@ -751,12 +751,26 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ S, const in
 //               target's earlier levels, so the summation order is fixed.
 // ---------------------------------------------------------------------------
 constexpr int kLtdSize = 4 * 16 * LI;   // 1152 doubles
-// Spins before a dependency wait counts as a device fault.  One spin is a
-// memory-side atomic round trip (~1 us under load) plus the task type's sleep
-// below (one s_sleep unit = 64 cycles, ~27 ns): ~0.07 s for the chain tasks and
-// the backward solve (1 unit), ~0.1 s for the update tasks (16 units) -- far
-// beyond any legitimate wait (a whole factorization is < 1 ms).
-constexpr long kSpinCap = 1L << 16;
+// How long a dependency wait may last before it counts as a device fault: 50
+// ms of the 100 MHz s_memrealtime clock (read every 16 polls), far beyond any
+// legitimate wait (a whole factorization is < 1 ms).  A time limit, not a poll
+// count: the chain tasks poll every unit and the update tasks every 16, so
+// with a count the chain task waiting downstream of a stuck update gave up
+// first and was the one reported; with the clock the earliest wait gives up
+// first, i.e. the stuck task itself (its fault record names its counter).
+constexpr unsigned long long kWaitCapTicks = 5000000ull;   // 50 ms at 100 MHz
+// the bound on the poll count as well (the clock read is 1 in 16 polls)
+constexpr long kSpinCap = 1L << 22;
+__device__ __forceinline__ unsigned long long wait_clock() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+// true once the wait that started at t0 has lasted kWaitCapTicks (checked on
+// every 16th poll) or kSpinCap polls
+__device__ __forceinline__ bool wait_expired(long spins, unsigned long long t0) {
+  return spins > kSpinCap || ((spins & 15) == 0 && wait_clock() - t0 > kWaitCapTicks);
+}
 // s_sleep units (64 cycles) between two polls of a dependency counter.  Every
 // poll is a device-scope atomic performed at the memory side; with a few
 // hundred update tasks waiting at once, polling every 64 cycles slowed the
@@ -1046,14 +1060,16 @@ __device__ __forceinline__ void store_tile_wt(double *__restrict__ g, const doub
 // wait q (64 at a time), so a task's counters are read in one round trip, not
 // one after another.
 // On a timeout *unmet = {counter, value seen, value awaited} of the first
-// wait still unmet (uniform over the wave), for the fault record.
+// wait still unmet (uniform over the wave), for the fault record; *expired:
+// this wait ran out of time (false: it gave up because another one had).
 __device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *flag, int lane, bool chain,
-                         int3 *unmet) {
+                         int3 *unmet, bool *expired) {
   for (int base = w0; base < w1; base += 64) {
     const int w = base + lane;
     const bool mine = w < w1;
     const int2 cv = mine ? waits[w] : make_int2(0, 0);
     long spins = 0;
+    const unsigned long long t0 = wait_clock();
     for (;;) {
       // (every lane re-polls each round: no loop-carried per-lane state)
       const int got = mine ? ld_acquire_relaxed(counters + cv.x) : 0;
@@ -1061,9 +1077,10 @@ __device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *
       if (m == 0) break;
       if (chain) __builtin_amdgcn_s_sleep(kChainSleep);
       else __builtin_amdgcn_s_sleep(kPollSleep);
-      const bool give_up = ++spins > kSpinCap ||
-                           ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0);
+      const bool exp = wait_expired(++spins, t0);
+      const bool give_up = exp || ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0);
       if (give_up) {
+        *expired = exp;
         const int l = __builtin_ctzll(m);
         *unmet = make_int3(__builtin_amdgcn_readlane(cv.x, l), __builtin_amdgcn_readlane(got, l),
                            __builtin_amdgcn_readlane(cv.y, l));
@@ -1079,9 +1096,14 @@ __device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *
 // fault record (kDagFault*), which the host reads to name the stuck counter,
 // its producers and how far the launch had drawn.  Plain agent-scope atomic
 // stores: the record is read after the launch.
-__device__ void dag_fault(int *flag, int *counters, int n_tiles, const int *ticket, int kind, int t, int3 unmet) {
-  if (atomicCAS(flag, 0, -(kind * 1000000 + t)) != 0) return;
+// Every wait that ran out of time (not one that gave up after another's
+// fault) also records its ticket in kFaultFirstStuck (as INT_MAX - ticket,
+// max-combined): the smallest stuck ticket, where a stuck chain starts.
+__device__ void dag_fault(int *flag, int *counters, int n_tiles, const int *ticket, int kind, int t, int3 unmet,
+                          bool expired) {
   int *f = counters + 2 * n_tiles + kDagOffFault;
+  if (expired) __hip_atomic_fetch_max(f + kFaultFirstStuck, INT_MAX - t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (atomicCAS(flag, 0, -(kind * 1000000 + t)) != 0) return;
   const int v[kDagFaultSlots] = {t, kind, unmet.x, unmet.y, unmet.z,
                                  ld_acquire_relaxed(const_cast<int *>(ticket)),
                                  ld_acquire_relaxed(counters + 2 * n_tiles + kDagOffInflight), (int)blockIdx.x};
@@ -1269,9 +1291,11 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
       // (sub.y: the end of the early waits; the late ones are a fused TRSM's,
       // or a folded TRSM's L_kk)
       int3 unmet;
-      const bool ok = premet || dag_wait(a.counters, a.waits, r[kRecWait0], sub.y, a.flag, lane, task.x != 2, &unmet);
+      bool expired = false;
+      const bool ok =
+          premet || dag_wait(a.counters, a.waits, r[kRecWait0], sub.y, a.flag, lane, task.x != 2, &unmet, &expired);
       if (lane == 0) {
-        if (!ok) dag_fault(a.flag, a.counters, a.n_tiles, ticket, 1, t, unmet);   // stuck ticket, for diagnosis
+        if (!ok) dag_fault(a.flag, a.counters, a.n_tiles, ticket, 1, t, unmet, expired);   // stuck ticket, for diagnosis
         // a drawn continuation target: run it only if its predecessor did not claim it
         sh[2] = (cont || r[kRecMaxdep] < 0 || atomicCAS(a.claimed + t, 0, 1) == 0) ? 1 : 0;
       }
@@ -1497,8 +1521,9 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         if (!pref) {
           if (w == 0) {
             int3 unmet;
-            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, r[kRecWait1], a.flag, lane, true, &unmet);
-            if (!ok2 && lane == 0) dag_fault(a.flag, a.counters, a.n_tiles, ticket, 3, t, unmet);
+            bool expired = false;
+            const bool ok2 = dag_wait(a.counters, a.waits, sub.y, r[kRecWait1], a.flag, lane, true, &unmet, &expired);
+            if (!ok2 && lane == 0) dag_fault(a.flag, a.counters, a.n_tiles, ticket, 3, t, unmet, expired);
           }
           __syncthreads();
         }
@@ -1683,10 +1708,12 @@ __global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
         if (tid == 0) {
           long spins = 0;
           int seen;
+          const unsigned long long t0 = wait_clock();
           while ((seen = ld_acquire_relaxed(applied + task.w)) < task.z) {
             __builtin_amdgcn_s_sleep(kPollSleep);
-            if (++spins > kSpinCap || (((spins & 255) == 0) && ld_acquire_relaxed(a.flag) < 0)) {
-              dag_fault(a.flag, a.counters, a.n_tiles, ticket, 2, t, make_int3(a.n_tiles + task.w, seen, task.z));
+            const bool exp = wait_expired(++spins, t0);
+            if (exp || (((spins & 255) == 0) && ld_acquire_relaxed(a.flag) < 0)) {
+              dag_fault(a.flag, a.counters, a.n_tiles, ticket, 2, t, make_int3(a.n_tiles + task.w, seen, task.z), exp);
               break;
             }
           }
@@ -1864,6 +1891,7 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
         double yv = 0.0;
         bool mine = ri + lane < nR;
         long spins = 0;
+        const unsigned long long t0 = wait_clock();
         for (;;) {
           if (mine) {
             yv = ld_wt(yF + ri + lane);
@@ -1871,7 +1899,7 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
           }
           if (__builtin_amdgcn_ballot_w64(mine) == 0) break;
           __builtin_amdgcn_s_sleep(kBsolveSleep);
-          if (++spins > kSpinCap || (((spins & 255) == 0) &&
+          if (wait_expired(++spins, t0) || (((spins & 255) == 0) &&
                                      __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) != 0)) {
             if (lane == 0) atomicCAS(flag, 0, -(4000000 + b));
             ok = false;

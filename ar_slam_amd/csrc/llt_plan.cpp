@@ -9,6 +9,7 @@
 //  3. a level schedule of the tile elimination tree: tile columns of equal
 //     height are independent and are factored in one launch, their updates
 //     applied in one launch; the backward solve walks the levels in reverse.
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1003,6 +1004,10 @@ std::string dag_fault_detail(const LltPlan &plan, const int *rec) {
   if (prod.size() > 6) s += ", ...";
   s += "; tickets drawn " + std::to_string(rec[kFaultDrawn]) + ", claimed continuations in flight " +
        std::to_string(rec[kFaultInflight]) + ", workgroup " + std::to_string(rec[kFaultBlock]);
+  if (rec[kFaultFirstStuck] > 0) {   // where the stuck chain starts (the earliest waits give up first)
+    const long first = (long)INT_MAX - rec[kFaultFirstStuck];
+    s += "; smallest ticket timed out: " + std::to_string(first) + " (" + task_name(first) + ")";
+  }
   return s;
 }
 

@@ -37,7 +37,8 @@ enum DagFaultField {
   kFaultDrawn = 5,    // tickets drawn by then (the launch's ticket counter)
   kFaultInflight = 6, // claimed continuations in flight
   kFaultBlock = 7,    // the workgroup
-  kDagFaultSlots = 8
+  kFaultFirstStuck = 8,   // INT_MAX - the smallest ticket whose wait ran out of time (0: none)
+  kDagFaultSlots = 9
 };
 constexpr int kDagCounterExtra = kDagOffFault + kDagFaultSlots;
 

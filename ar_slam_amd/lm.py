@@ -549,7 +549,7 @@ def debug_dag_fault_detail(g, rec):
     """Host-only: the text an executor fault carries for fault record rec[8] (lm_internal.h
     DagFaultField) on g's one-rank plan."""
     A = _Soa(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
-    r = (C.c_int * 8)(*[int(v) for v in rec])
+    r = (C.c_int * 9)(*([int(v) for v in rec] + [0] * (9 - len(rec))))
     buf = C.create_string_buffer(4096)
     _check(lib().arslam_debug_dag_fault_detail(C.byref(A.s), r, buf, len(buf)))
     return buf.value.decode()

@@ -96,17 +96,22 @@ int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[4]);
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);
 
-/* Host only: the message an executor fault carries for the one-rank plan of p
- * (nested dissection, sparse tiles) and a fault record rec[8] = {ticket, kind
- * (1 dependency wait, 2 in-order application, 3 late wait), counter, value
- * seen, value awaited, tickets drawn, claimed continuations in flight,
- * workgroup}: the task, the counter, the tickets that advance it.  Writes at
- * most len bytes (NUL-terminated) to buf. */
 /* Host only: one simulated interleaving of n_workers workgroups running the
  * persistent executor's protocol on the one-rank plan of p (policy 0 random,
  * 1-3 adversarial orders; + 16 drops the cap on claimed continuations in
  * flight, which the protocol relies on).  *ok = 1 if every task finished, 0 on
  * a deadlock. */
+int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_workers, unsigned seed, int policy, int *ok);
+
+/* Host only: the message an executor fault carries for the one-rank plan of p
+ * (nested dissection, sparse tiles) and a fault record rec[9] = {ticket, kind
+ * (1 dependency wait, 2 in-order application, 3 late wait), counter, value
+ * seen, value awaited, tickets drawn, claimed continuations in flight,
+ * workgroup, INT_MAX - the smallest ticket whose wait ran out of time (0:
+ * none)}: the task, the counter, the tickets that advance it.  Writes at most
+ * len bytes (NUL-terminated) to buf. */
+int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[9], char *buf, int len);
+
 /* The memory round trips of the persistent executor's hand-offs on this
  * device, measured in a few milliseconds (one lane each): out = {never-matching
  * CAS poll (ns, dependent chain), agent-scope sc1 load (ns, dependent chain),
@@ -114,8 +119,6 @@ int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int ski
  * through agent-scope flags (ns per round trip, -1 if it timed out), the two
  * workgroups' XCC ids}.  device < 0: the current device. */
 int arslam_debug_box_fingerprint(int device, double out[6]);
-int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_workers, unsigned seed, int policy, int *ok);
-int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[8], char *buf, int len);
 
 /* Host only: the multi-rank split arslam_lm_load_soa makes for rank `rank` of
  * `nranks` (nested dissection, sparse tiles) -- its two-phase tile plan, and

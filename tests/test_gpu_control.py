@@ -174,10 +174,14 @@ def test_broken_dependency_is_a_device_error(lm):
         rp.solve()
     assert e.value.code == -8
     assert "executor fault" in str(e.value) and "timed out" in str(e.value)
-    # the fault record: the stuck task, the awaited counter with the value it had, its producers
+    # the fault record: the stuck task (the earliest wait gives up first: the broken one), the
+    # awaited counter with the value it had and what advances it, how far the launch drew
     msg = str(e.value)
-    assert f"ticket {broken} (" in msg and "advanced by" in msg and "tickets drawn" in msg, msg
+    assert "dependency wait timed out -- ticket " in msg, msg
+    assert f"smallest ticket timed out: {broken} (" in msg, msg
+    assert "advanced by" in msg and "tickets drawn" in msg, msg
     assert "ready[" in msg or "applied[" in msg, msg
+    assert "< " in msg.split("]")[1], msg
     # the broken wait lasts one solve: the same handle then solves normally again
     assert [i["cost"] for i in rp.solve()["iterations"]] == [i["cost"] for i in ok["iterations"]]
     rp2 = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)

@@ -220,5 +220,8 @@ def test_fault_record_names_the_stuck_counter_and_its_producers(L):
     assert s.startswith("ticket 2772 (TRSM (80,69))"), s
     assert "ready[340] = 0 < 1" in s and "ticket 2205 (POTRF 69+TRSM) [continuation target]" in s, s
     assert "tickets drawn 3000" in s and "in flight 3" in s, s
+    assert "smallest ticket timed out" not in s, s
+    s3 = L.debug_dag_fault_detail(g, rec + [2**31 - 1 - 2205])   # a stuck chain starting at POTRF 69
+    assert s3.endswith("smallest ticket timed out: 2205 (POTRF 69+TRSM)"), s3
     s2 = L.debug_dag_fault_detail(g, [2772, 1, 12625 * 0 + 2461 + 1620, 1, 2, 3000, 3, 17])
     assert "applied[1620] = 1 < 2" in s2 and "ticket 1981" in s2 and "ticket 2355" in s2, s2
