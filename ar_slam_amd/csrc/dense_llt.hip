@@ -1104,11 +1104,12 @@ __device__ void dag_fault(int *flag, int *counters, int n_tiles, const int *tick
   int *f = counters + 2 * n_tiles + kDagOffFault;
   if (expired) __hip_atomic_fetch_max(f + kFaultFirstStuck, INT_MAX - t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (atomicCAS(flag, 0, -(kind * 1000000 + t)) != 0) return;
-  const int v[kDagFaultSlots] = {t, kind, unmet.x, unmet.y, unmet.z,
-                                 ld_acquire_relaxed(const_cast<int *>(ticket)),
-                                 ld_acquire_relaxed(counters + 2 * n_tiles + kDagOffInflight), (int)blockIdx.x};
+  const int v[kFaultFirstStuck] = {t, kind, unmet.x, unmet.y, unmet.z,
+                                   ld_acquire_relaxed(const_cast<int *>(ticket)),
+                                   ld_acquire_relaxed(counters + 2 * n_tiles + kDagOffInflight), (int)blockIdx.x};
 #pragma unroll
-  for (int i = 0; i < kDagFaultSlots; ++i) __hip_atomic_store(f + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = 0; i < kFaultFirstStuck; ++i)   // (kFaultFirstStuck itself is max-combined above)
+    __hip_atomic_store(f + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // all threads: drain this workgroup's write-through stores before thread 0
