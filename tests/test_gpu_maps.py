@@ -13,15 +13,18 @@
   from the image), fed one Detections message at a time with a
   solveIncremental after each (the ROS node's flow, :629-742).
 
-Tolerances: as tests/test_gpu_slam.py (a chain of full solves: costs and
-focal 1e-6 relative; poses as tag and camera centres after a rigid
-alignment, 1e-5 m), widened to 20x the distance between the
-oracle's own Schur and full-normal-equation runs of the same driver where
-the problem itself amplifies rounding: cfg1's first message is one capture
-of 4 tags with no fixed block, which Ceres' LM leaves at NO_CONVERGENCE
-after 50 iterations in a flat valley, where two exact arithmetics already
-differ by 2e-5 in cost and 5e-2 px in focal; the gauge (no block is held
-constant, ar_slam_util.cpp:697-700) lets every later pose drift by as much.
+Tolerances (tests/spread_tol.py): as tests/test_gpu_slam.py (a chain of full
+solves: costs and focal 1e-6 relative; poses as tag and camera centres after
+a rigid alignment, 1e-5 m), widened to 20x the distance between the oracle's
+own Schur and full-normal-equation runs of the same driver where the problem
+itself amplifies rounding, but capped at focal 1e-3 px, centres 1e-4 m, cost
+1e-6 relative.  Three values are exempt from the caps, each with its reason
+asserted (spread_tol.EXEMPT): cfg1's first message is one capture of 4 tags
+with no fixed block, which Ceres' LM leaves at NO_CONVERGENCE after 50
+iterations in a flat valley, where two exact arithmetics already differ by
+2e-5 in cost and 5e-2 px in focal, and the second message inherits that
+focal drift.  The gauge-invariant reprojection RMS of every converged cfg1
+solve (the map file and the final message) agrees to 1e-8 relative.
 """
 import os
 
@@ -29,6 +32,7 @@ import numpy as np
 import pytest
 
 from ar_slam_amd import synth
+from spread_tol import tolerance
 
 pytestmark = pytest.mark.gpu
 yaml = pytest.importorskip("yaml")
@@ -65,24 +69,29 @@ def _points(caps, tags):
     return np.concatenate([np.asarray(tags)[:, :3], -np.asarray(caps)[:, :3]])
 
 
-def _compare(s, o, alt):
+def _compare(s, o, alt, key=None, rms_rel=None):
     """Device vs oracle `o`; `alt` is the oracle run with the full normal equations.  Costs and
     focal directly; poses as tag and camera centres after a rigid alignment onto the oracle's
     (no block is held constant: the solution is defined up to a rigid motion, and the flat
-    first solve leaves the gauge wherever the rounding took it)."""
+    first solve leaves the gauge wherever the rounding took it).  Tolerances: spread_tol (the
+    oracle's two arithmetics' spread, capped; key = (flow, message) for the named exemptions);
+    rms_rel: the reprojection RMS (gauge-invariant) to that relative tolerance as well."""
     assert s.num_solves == o.n_solves == alt.n_solves
     last = s.last_summary()
     assert last["termination"] == o.last_summary["termination"]
     ref, oth = _state(o), _state(alt)
     ours = (last["final_cost"], s.camera()[0][0])
-    for what, a, b, c, base in zip(("cost", "focal"), ours, ref, oth, (1e-6, 1e-6)):
-        tol = max(base * abs(b), 20.0 * abs(c - b))
-        assert abs(a - b) <= tol, (what, a, b, tol)
+    for what, a, b, c in zip(("cost", "focal"), ours, ref, oth):
+        tol = tolerance(what, b, c, key)
+        assert abs(a - b) <= tol, (what, key, a, b, tol)
     q = _points(ref[2], ref[3])
     p_ours = _align_rigid(_points(s.capture_poses(), s.aruco_poses()), q)
     p_alt = _align_rigid(_points(oth[2], oth[3]), q)
-    tol = np.maximum(1e-5, 20.0 * np.abs(p_alt - q))
-    assert np.all(np.abs(p_ours - q) <= tol), ("centres", np.max(np.abs(p_ours - q)), np.max(np.abs(p_alt - q)))
+    tol = np.vectorize(lambda qq, aa: tolerance("centres", qq, aa, key))(q, p_alt)
+    assert np.all(np.abs(p_ours - q) <= tol), ("centres", key, np.max(np.abs(p_ours - q)), np.max(np.abs(p_alt - q)))
+    if rms_rel is not None:   # (final_rms_px = sqrt(2 cost / (4 n_obs)), synth.rms_px)
+        rms_ref = synth.rms_px(ref[0], last["n_obs"])
+        assert abs(last["final_rms_px"] - rms_ref) <= rms_rel * rms_ref, ("rms", key, last["final_rms_px"], rms_ref)
 
 
 def _write_map(g, path):
@@ -115,7 +124,7 @@ def test_map_file_solve_save_matches_oracle(lm, name, tmp_path):
         for uid, ids, corners in _messages(doc):
             x.add_detections(uid, ids, corners)
         x.solve()
-    _compare(s, o, alt)
+    _compare(s, o, alt, rms_rel=1e-8 if name == "cfg1" else None)
     assert s.last_summary()["final_rms_px"] < 1.0
     out = tmp_path / "solved.yaml"
     s.save_yaml(out)
@@ -140,12 +149,15 @@ def test_cfg1_incremental_messages_match_oracle(lm):
     o = OracleSlam(camera=doc["camera"]["params"])
     alt = OracleSlam(camera=doc["camera"]["params"], elimination=1)
     s.set_camera(doc["camera"]["params"])
-    for uid, ids, corners in _messages(doc):
+    msgs = list(_messages(doc))
+    for i, (uid, ids, corners) in enumerate(msgs):
         s.add_detections(uid, ids, corners)
         s.solve_incremental()
         for x in (o, alt):
             x.add_detections(uid, ids, corners)
             x.solve_incremental()
-        _compare(s, o, alt)
+        _compare(s, o, alt, key=("cfg1_incremental", i), rms_rel=1e-8 if i == len(msgs) - 1 else None)
+        if i == 0:   # the exemption's premise (spread_tol.EXEMPT): the flat-valley stop
+            assert o.last_summary["termination"] == "NO_CONVERGENCE"
     assert s.num_solves == 3
     assert s.last_summary()["final_rms_px"] < 1.0
