@@ -120,7 +120,13 @@ extern "C" int arslam_debug_dense_llt_ex(long n, double *A, const double *b, dou
   DBG_CHECK(hipMemcpy(d_S, tiles.data(), tiles.size() * sizeof(double), hipMemcpyHostToDevice));
   DBG_CHECK(hipMemset(d_flag, 0, sizeof(int)));
   const char *eg = std::getenv("ARSLAM_DAG_GRID");
-  const int grid = eg ? std::atoi(eg) : 512;
+  int grid = eg ? std::max(1, std::atoi(eg)) : 512;
+  {   // at most the resident workgroups (the claim cap is half the grid)
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+      grid = std::min(grid, arslam::kDagWorkgroupsPerCu * cus);
+  }
   if (executor == 1 && std::getenv("ARSLAM_DAG_PROGRESS")) {
     // debug: host-visible progress words, polled while the kernel runs
     int *prog = nullptr;

@@ -1216,7 +1216,7 @@ __device__ __forceinline__ unsigned long long realtime() {
                          __HIP_MEMORY_SCOPE_SYSTEM);                                            \
   } while (0)
 
-__global__ __launch_bounds__(256, 2) void k_factor_dag(DagArgs a) {
+__global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs a) {
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
   __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 12 + 16 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
@@ -2028,20 +2028,6 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
   }
 }
 
-// k_factor_dag workgroups that fit on the current device at once (its launch
-// bounds: 2 per CU) times the CU count, cached per device
-int dag_resident_workgroups() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 512;
-  if (!cached[dev]) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    cached[dev] = 2 * cus;
-  }
-  return cached[dev];
-}
-
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
                           unsigned long long *trace, bool reset, int phase) {
   const int t_begin = phase == 1 ? (int)P.phase_split : 0;
@@ -2061,10 +2047,10 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
   // 128 workgroups against 228.4 on 448; the incremental cfg2 flow's
   // minimizer 1.83 -> 1.79 ms per Solve).  cfg3 (12,625 tasks) keeps the full grid.
   const long ntk = t_end - t_begin;
-  int grid = (int)std::min<long>(n_workgroups, std::max<long>(std::min<long>(64, ntk), ntk / 4));
-  // never more workgroups than can be resident at once: the claim cap (half
-  // the grid) must leave resident workgroups free to draw
-  grid = std::max(1, std::min(grid, dag_resident_workgroups()));
+  // (n_workgroups: at most the resident count, kDagWorkgroupsPerCu per CU --
+  // the claim cap, half the grid, must leave resident workgroups free to draw;
+  // DESIGN §8b.  The callers clamp it: a HIP query here would sit on the hot path)
+  const int grid = (int)std::min<long>(n_workgroups, std::max<long>(std::min<long>(64, ntk), ntk / 4));
   hipLaunchKernelGGL(k_factor_dag, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
 

@@ -41,6 +41,9 @@ enum DagFaultField {
   kDagFaultSlots = 9
 };
 constexpr int kDagCounterExtra = kDagOffFault + kDagFaultSlots;
+// k_factor_dag workgroups resident per CU (its launch bounds; 73 KB of LDS
+// each): a launch never asks for more than this times the CU count
+constexpr int kDagWorkgroupsPerCu = 2;
 
 constexpr int kWave = 64;
 constexpr int kTile = 64;          // reduced-system Cholesky tile
@@ -325,6 +328,8 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
 // k_schur blocks before the gather writes S)
 // (er: the persistent executors' reset rides along in k_schur's blocks past
 // the tiles; only with P.nc > 0)
+// k_schur<true>'s dynamic-LDS attribute on the current device (once per device)
+void set_schur_big_lds_attribute();
 void launch_schur(const DevProblem &P, const double *x, const double *scale, const double *diag,
                   double radius, double *S, hipStream_t s, bool prep = false, long zero_tiles = 0,
                   const ExecReset *er = nullptr);

@@ -1456,9 +1456,10 @@ void launch_lm_diag(const DevProblem &P, const double *scale, const double *coln
                      colnorm, dmin, dmax, diag);
 }
 
-// k_schur<true>'s dynamic-LDS limit, set once per device (the attribute is
-// per device; several host threads may launch first at once): a failure is
-// an error, not a launch that later fails for its LDS size
+// k_schur<true>'s dynamic-LDS limit on the current device, once per device
+// (the attribute is per device; several host threads may reach it at once): a
+// failure is an error, not a launch that later fails for its LDS size.  Called
+// where the device is made current (ensure_stream), not per launch.
 void set_schur_big_lds_attribute() {
   static std::mutex m;
   static std::vector<char> done;
@@ -1492,7 +1493,7 @@ void launch_schur(const DevProblem &P, const double *x, const double *scale, con
                      diag, radius, S, zero_tiles, r, (const int *)nullptr);
   if (P.n_big_caps > 0) {
     const size_t lds_big = schur_lds_bytes(P.max_blk_per_cap);
-    set_schur_big_lds_attribute();   // (dynamic LDS past 64 KiB: once per device)
+    // (dynamic LDS past 64 KiB: set once per device by the caller, ensure_stream)
     hipLaunchKernelGGL(k_schur<true>, dim3((unsigned)P.n_big_caps), dim3(kWave), lds_big, s, P, scale, diag, radius, S,
                        0L, ExecReset{}, P.big_caps);
   }

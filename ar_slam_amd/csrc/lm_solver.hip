@@ -24,6 +24,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -285,7 +286,9 @@ struct arslam_lm {
   DevBuf<double> d_slab, d_jrows, d_cap_ui;
   DevBuf<double> d_gather_part;
   arslam::LltPlan plan;
-  double *x = nullptr, *xc = nullptr;
+  // x: the current point, xc: the candidate, xbest: the best point so far --
+  // three of d_xa / d_xb / d_xbest by pointer, xc never aliasing the other two
+  double *x = nullptr, *xc = nullptr, *xbest = nullptr;
   unsigned long long dbg_indefinite_mask = 0;   // arslam_lm_debug_force_indefinite
   arslam_iteration_callback iter_cb = nullptr;  // arslam_lm_set_iteration_callback
   void *iter_cb_ctx = nullptr;
@@ -394,7 +397,15 @@ struct arslam_lm {
   static inline int dag_trace_seen = 0;
 
   int cus_device = -1, cus = 0;   // the CU count, queried once per device
+  // The thread and options device the handle's stream was last made ready
+  // for: a later load from the same thread with the same options makes no HIP
+  // call here.
+  std::thread::id ready_thread{};
+  int ready_opt_device = -2;
   void ensure_stream() {
+    if (stream && ready_thread == std::this_thread::get_id() && ready_opt_device == opt.device) {
+      return;
+    }
     HIP_CHECK(hipGetDevice(&device));
     if (opt.device >= 0 && opt.device != device) {   // (set only when it differs)
       HIP_CHECK(hipSetDevice(opt.device));
@@ -404,6 +415,7 @@ struct arslam_lm {
       cus = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
       cus_device = device;
+      arslam::set_schur_big_lds_attribute();   // (k_schur's big-capture launch: once per device)
     }
     // 1.75 persistent workgroups per CU (73 KB of LDS each: two fit): 448 on
     // the MI355X's 256 CUs.  cfg3 k_factor_dag 663.1 -> 655.7 us and
@@ -411,8 +423,12 @@ struct arslam_lm {
     // co-resident update workgroups beside the chain's POTRF tasks
     if (cus > 0) dag_workgroups = 7 * cus / 4;
     if (const char *g = std::getenv("ARSLAM_DAG_GRID")) dag_workgroups = std::max(1, std::atoi(g));   // debug
+    // never more than can be resident at once (the claim cap is half the grid)
+    if (cus > 0) dag_workgroups = std::min(dag_workgroups, arslam::kDagWorkgroupsPerCu * cus);
     if (!stream) HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &t : timers) t.init();
+    ready_thread = std::this_thread::get_id();
+    ready_opt_device = opt.device;
   }
 
   void load(const arslam_soa_problem *p);
@@ -548,6 +564,10 @@ long round_up(long v, long m) { return (v + m - 1) / m * m; }
 void arslam_lm::load(const arslam_soa_problem *p_in) {
   const double t_load = now_s();
   loaded = false;
+  // (the process's first HIP call starts the runtime, 0.02-0.2 s: the first
+  // load of a process pays it here, in summary.setup_phase_s[0] -- round 4's
+  // "1.2 ms per full load" was that one start averaged over 179 loads)
+  ensure_stream();
   // the e-block side (ARSLAM_ELIM_*): Ceres' own independent set decides AUTO;
   // tag elimination runs the same kernels on the role-swapped problem
   const arslam::SchurSide cs = arslam::ceres_schur_side(p_in);
@@ -653,8 +673,6 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
                                  nullptr, 0, true);
   }
   tp[1] = now_s();
-  ensure_stream();
-  const double t_stream = now_s();
   soa = *p;   // (several ranks: the whole problem; write_back maps this rank's captures)
   nc = h.nc;
   nt = h.nt;
@@ -692,7 +710,8 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   soa = *p;
   loaded = true;
   pk_appended_only = true;
-  setup_s = now_s() - t_load;
+  const double t_end = now_s();
+  setup_s = t_end - t_load;
   // summary.setup_phase_s: structure (side rule + host problem), elimination
   // order (reduced layout; several ranks: + the split), tile plan + task graph,
   // gather plan + upload, the rest
@@ -702,9 +721,9 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   setup_phase[3] = tp[5] - tp[4];
   setup_phase[4] = setup_s - setup_phase[0] - setup_phase[1] - setup_phase[2] - setup_phase[3];
   if (prof)
-    std::fprintf(stderr, "arslam setup: nc %d nt %d side %.3f host+layout %.3f stream %.3f covis %.3f plan %.3f gather+upload %.3f total %.3f ms (order %s, %d levels, %ld tiles)\n",
-                 nc, nt, 1e3 * (tp[0] - t_load), 1e3 * (tp[1] - tp[0]), 1e3 * (t_stream - tp[1]), 1e3 * (tp[2] - t_stream), 1e3 * (tp[3] - tp[2]),
-                 1e3 * (tp[5] - tp[4]), 1e3 * setup_s,
+    std::fprintf(stderr, "arslam setup: nc %d nt %d side %.3f host+layout %.3f covis %.3f plan %.3f gather+upload %.3f tail %.3f total %.3f ms (order %s, %d levels, %ld tiles)\n",
+                 nc, nt, 1e3 * (tp[0] - t_load), 1e3 * (tp[1] - tp[0]), 1e3 * (tp[2] - tp[1]), 1e3 * (tp[3] - tp[2]),
+                 1e3 * (tp[5] - tp[4]), 1e3 * (t_end - tp[5]), 1e3 * setup_s,
                  prev_order_nc == nc ? "fresh" : "kept", plan.nlev, (long)plan.n_tiles);
 }
 
@@ -1151,8 +1170,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->setup_kind = setup_kind;
   x = d_xa.p;
   xc = d_xb.p;
+  xbest = x;   // (iteration 0's finalize makes it so)
   HIP_CHECK(hipMemcpyAsync(x, u_x0, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
-  HIP_CHECK(hipMemcpyAsync(d_xbest.p, u_x0, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
   const bool root = rank == 0;
   if (o.minimizer_progress_to_stdout && root) print_header();
   // the patched dependency of arslam_lm_debug_break_dependency lasts one solve
@@ -1232,8 +1251,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       if (it.iteration > 0) s->num_successful_steps++;
       if (x_cost < minimum_cost || it.iteration == 0) {
         minimum_cost = x_cost;
-        HIP_CHECK(hipMemcpyAsync(d_xbest.p, x, n * sizeof(double), hipMemcpyDeviceToDevice, stream));
-        if (o.update_state_every_iteration) write_back(d_xbest.p);
+        xbest = x;   // (by pointer: no copy; the step in flight writes xc)
+        if (o.update_state_every_iteration) write_back(xbest);
       }
     } else {
       s->num_unsuccessful_steps++;
@@ -1497,7 +1516,13 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     it.relative_decrease = candidate_cost >= DBL_MAX ? -DBL_MAX
                                                      : (x_cost - candidate_cost) / model_cost_change;
     if (it.relative_decrease > o.min_relative_decrease) {
-      std::swap(x, xc);
+      // the candidate becomes x; the next candidate goes to a buffer that is
+      // neither x nor the best point (the old x, unless it is the best: its
+      // successor's cost is read only at the next sync, after the next step
+      // is enqueued)
+      double *old = x;
+      x = xc;
+      xc = old != xbest ? old : (d_xa.p != x && d_xa.p != xbest) ? d_xa.p : (d_xb.p != x && d_xb.p != xbest) ? d_xb.p : d_xbest.p;
       linearize_launch();   // read at the next step's sync (finalize)
       lin_pending = true;
       it.step_is_successful = 1;
@@ -1518,7 +1543,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   }
   s->final_cost = minimum_cost + fixed_cost;
   s->minimizer_time_s = now_s() - t_start;
-  write_back(d_xbest.p);
+  write_back(xbest);
   s->total_time_s = now_s() - t_start;
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
   if (prof) std::fprintf(stderr, "arslam write_back %.3f ms\n", 1e3 * (s->total_time_s - s->minimizer_time_s));
