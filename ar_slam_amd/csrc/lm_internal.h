@@ -353,9 +353,12 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 // reduce per-capture partials [NPART][nc] (+ f-slot partials) into out[NPART]
 // (flag: also out[NPART + 2] = indefinite (flag > 0), out[NPART + 3] = executor
 // fault (flag < 0), out[NPART + 4] = the raw flag)
+// (seq_done, seq > 0: with hout, the last block to finish also stores seq into
+// hout[kHostSeq] after every block's host words -- the LM loop's host polls that
+// word instead of an event; seq_done: a zeroed device int, left zero again)
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts,
                          double *out, hipStream_t s, const int *flag = nullptr,
-                         double *hout = nullptr);
+                         double *hout = nullptr, int *seq_done = nullptr, double seq = 0.0);
 void debug_set_reduced_diag(const DevProblem &P, double *S, long row, double v, hipStream_t s);
 // multi-rank exchange buffers: up to 4 segments packed at offsets off[] of one buffer
 struct PackSegs {
@@ -397,10 +400,17 @@ void launch_ag_reduce(const double *ag, const AgFields &fl, double *dst, int nra
 // the launch's block count (must be zero before the first launch), out[8..]
 // its per-block partials.
 // (ld: also the LM diagonal clamp(s^2 colnorm) of every slot from ld->scale, into ld->diag)
+// (seq > 0: with hout, the last block stores seq into hout[kHostSeq] after the results)
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
-                       double *out, hipStream_t s, double *hout = nullptr, const LmDiagArgs *ld = nullptr);
+                       double *out, hipStream_t s, double *hout = nullptr, const LmDiagArgs *ld = nullptr,
+                       double seq = 0.0);
 // (hout, in the three launchers above: page-locked host words that also receive
-// the results, so a single-rank solve needs no device-to-host copy for them)
+// the results, so a single-rank solve needs no device-to-host copy for them;
+// each writer releases them at system scope)
+// hout[kHostSeq]: the launch's sequence number, stored last (a host-memory flag:
+// a ~8 us kernel-to-host round trip against ~13 us for an event query on
+// MI355X, tools/sync_bench.hip)
+constexpr int kHostSeq = 15;
 
 // Optional per-launch event pairs around the dominant kernel (trailing update).
 struct LaunchTiming {

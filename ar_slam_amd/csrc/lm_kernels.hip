@@ -1190,7 +1190,8 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
 __device__ __forceinline__ void reduce_parts_block(int p, const double *__restrict__ parts, int nc,
                                                    const double *__restrict__ fparts, int nfparts,
                                                    double *__restrict__ out, const int *__restrict__ flag,
-                                                   double *red, double *__restrict__ hout) {
+                                                   double *red, double *__restrict__ hout,
+                                                   int *seq_done = nullptr, double seq = 0.0) {
   const int t = threadIdx.x;
   const bool is_max = (p == P_YBAD || p == P_CBAD || p == NPART + 1);
   const double *src = p < NPART ? parts + (long)p * nc : fparts;
@@ -1227,15 +1228,24 @@ __device__ __forceinline__ void reduce_parts_block(int p, const double *__restri
       if (hout) hout[NPART + 2 + q] = v[q];
     }
   }
+  if (hout && t == 0) {
+    // this block's host words out of its XCD's L2 (the blocks span XCDs);
+    // then the last block to finish stores the sequence number
+    __threadfence_system();
+    if (seq_done && seq > 0.0 && atomicAdd(seq_done, 1) == (int)gridDim.x - 1) {
+      atomicExch(seq_done, 0);
+      __hip_atomic_store(hout + kHostSeq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict__ parts, int nc,
                                                        const double *__restrict__ fparts,
                                                        int nfparts, double *__restrict__ out,
                                                        const int *__restrict__ flag,
-                                                       double *__restrict__ hout) {
+                                                       double *__restrict__ hout, int *seq_done, double seq) {
   __shared__ double red[1024];
-  reduce_parts_block(blockIdx.x, parts, nc, fparts, nfparts, out, flag, red, hout);
+  reduce_parts_block(blockIdx.x, parts, nc, fparts, nfparts, out, flag, red, hout, seq_done, seq);
 }
 
 // The linearization's two reductions of k_linearize's output in one launch
@@ -1264,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
                                                     const double *__restrict__ x,
                                                     double *__restrict__ out,
                                                     double *__restrict__ hout, const double *__restrict__ scale,
-                                                    double dmin, double dmax, double *__restrict__ diag) {
+                                                    double dmin, double dmax, double *__restrict__ diag, double seq) {
   __shared__ double rs[6][256];
   __shared__ int last;
   const int t = threadIdx.x;
@@ -1331,9 +1341,16 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
   }
   if (t < 6) {
     out[t] = rs[t][0];
-    if (hout) hout[t] = rs[t][0];
+    if (hout) {
+      hout[t] = rs[t][0];
+      __threadfence_system();
+    }
   }
   if (t == 0) atomicExch(done, 0);
+  if (hout && seq > 0.0) {
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(hout + kHostSeq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---- multi-rank exchange buffers (lm_solver.hip) ----
@@ -1547,16 +1564,17 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 }
 
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
-                         hipStream_t s, const int *flag, double *hout) {
-  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, hout);
+                         hipStream_t s, const int *flag, double *hout, int *seq_done, double seq) {
+  hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, hout,
+                     seq_done, seq);
 }
 
 void launch_slot_norms(const DevProblem &P, const double *red, double *g, double *colnorm, const double *x,
-                       double *out, hipStream_t s, double *hout, const LmDiagArgs *ld) {
+                       double *out, hipStream_t s, double *hout, const LmDiagArgs *ld, double seq) {
   // out[0..5] results, out[7] the block count (zero between launches), out[8..] the per-block partials
   hipLaunchKernelGGL(k_slot_norms, dim3(kNormBlocks), dim3(256), 0, s, P.n, 3L, 3L + 6L * P.nc, P.slot_free, P.f_own, g,
                      colnorm, red, x, out, hout, ld ? ld->scale : nullptr, ld ? ld->dmin : 0.0,
-                     ld ? ld->dmax : 0.0, ld ? ld->diag : nullptr);
+                     ld ? ld->dmax : 0.0, ld ? ld->diag : nullptr, seq);
 }
 
 void launch_pack(const PackSegs &sg, double *buf, bool unpack, hipStream_t s) {

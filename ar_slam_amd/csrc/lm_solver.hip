@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -205,9 +206,10 @@ struct Timer {
     HIP_CHECK(hipEventRecord(b, s));
     pending = true;
   }
-  void collect() {  // call after the stream was synchronized
+  void collect() {  // call after the stream was synchronized (or its flag seen: b may still be pending)
     if (!pending) return;
     float ms = 0.f;
+    HIP_CHECK(hipEventSynchronize(b));
     HIP_CHECK(hipEventElapsedTime(&ms, a, b));
     acc_ms += ms;
     pending = false;
@@ -318,6 +320,7 @@ struct arslam_lm {
     if (!opt.kernel_timing || !has_f) return;
     for (int i = 0; i < upd_timing.used; ++i) {
       float ms = 0.f;
+      HIP_CHECK(hipEventSynchronize(upd_events[2 * i + 1]));
       HIP_CHECK(hipEventElapsedTime(&ms, upd_events[2 * i], upd_events[2 * i + 1]));
       dom_ms += ms;
     }
@@ -522,7 +525,12 @@ struct arslam_lm {
   void exchange_norms() {
     if (norms_pending) exchange_scalars(arslam::AgFields{});
   }
-  PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [16..21] slot norms
+  PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [16..21] slot norms; [16 + kHostSeq] lin_seq
+  double lin_seq = 0.0;   // (one rank) the last linearization's sequence number
+  void lin_sync() {   // the linearization's host words (one rank: its flag; several: after the copies)
+    if (nranks == 1 && lin_seq > 0.0) flag_sync(h_lin.p + 16 + arslam::kHostSeq, lin_seq);
+    else spin_sync();
+  }
   // host LM loop: the Jacobi scale of this solve is set, so each later
   // linearization also forms the LM diagonal (k_slot_norms) and the step's
   // executor reset rides in k_schur's launch
@@ -539,6 +547,31 @@ struct arslam_lm {
     while ((e = hipEventQuery(ev_sync)) == hipErrorNotReady) {
     }
     HIP_CHECK(e);
+  }
+  // One rank: the LM loop's host reads wait for the kernel that stores their
+  // page-locked words to store its sequence number last (hout[kHostSeq]),
+  // instead of an event behind it: ~8 against ~13 us per round trip on
+  // MI355X (tools/sync_bench.hip), ~7 round trips per cfg3 solve and ~7,000
+  // in the incremental cfg2 flow.  The stream is queried now and then so a
+  // launch that never stores it (an error) is reported, not waited for.
+  double host_seq = 0.0;
+  DevBuf<int> d_seq_done;   // k_reduce_parts' finished blocks (zero between launches)
+  double next_seq(double *word) {
+    *(volatile double *)word = -1.0;   // (before the launch: the kernel's store lands after it)
+    return host_seq += 1.0;
+  }
+  void flag_sync(const double *word, double seq) {
+    for (long k = 1;; ++k) {
+      if (*(const volatile double *)word == seq) break;
+      if ((k & 4095) == 0) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipErrorNotReady) continue;
+        HIP_CHECK(e);
+        if (*(const volatile double *)word == seq) break;
+        throw Error(ARSLAM_E_DEVICE, "the stream finished without storing the host sequence word");
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
   }
   void solve(arslam_lm_summary *s);
   void write_back(const double *d_src);
@@ -819,6 +852,9 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   d_norms_p = d_red.p + 16;       // (one D2H carries both after a linearization)
   if (d_red.p != red_prev) HIP_CHECK(hipMemsetAsync(d_norms_p + 7, 0, sizeof(double), stream));   // the count
   d_flag.alloc(1);
+  const int *seq_prev = d_seq_done.p;
+  d_seq_done.alloc(1);
+  if (d_seq_done.p != seq_prev) HIP_CHECK(hipMemsetAsync(d_seq_done.p, 0, sizeof(int), stream));
   if (has_f) {
     d_slab.alloc(std::max(sg.cap_off[nc], 1L));
     d_gather_part.alloc(36L * std::max(sg.n_pslots, 1));
@@ -996,8 +1032,9 @@ void arslam_lm::linearize_launch() {
     lin_xpending = true;
   }
   const arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, opt.min_lm_diagonal, opt.max_lm_diagonal, d_diag.p};
+  lin_seq = direct ? next_seq(h_lin.p + 16 + arslam::kHostSeq) : 0.0;
   arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, direct ? h_lin.p + 16 : nullptr,
-                            diag_in_lin ? &ld : nullptr);
+                            diag_in_lin ? &ld : nullptr, lin_seq);
   timers[PH_LIN].stop(stream);
 }
 
@@ -1070,7 +1107,7 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
   linearize_launch();
   complete_pending_lin();
   exchange_norms();
-  spin_sync();
+  lin_sync();
   linearize_collect(x_cost, fixed_cost, gmax, gnorm, xnorm);
 }
 
@@ -1297,7 +1334,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     if (lin_pending && stop_rule) {
       complete_pending_lin();
       exchange_norms();
-      spin_sync();
+      lin_sync();
     }
     const bool deferred = lin_pending && !stop_rule;
     if (!deferred && finalize()) break;
@@ -1447,8 +1484,9 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     timers[PH_COST].start(stream);
     h_step.alloc(16);
     // (one rank: the scalars are also stored straight into the page-locked h_step)
+    const double step_seq = nranks == 1 ? next_seq(h_step.p + arslam::kHostSeq) : 0.0;
     arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p,
-                                nranks == 1 ? h_step.p : nullptr);
+                                nranks == 1 ? h_step.p : nullptr, d_seq_done.p, step_seq);
     if (nranks > 1) {
       // candidate cost, fixed, model change, capture step^2 by sum; the
       // non-finite flags, the f-side non-finite step, indefinite and executor
@@ -1463,9 +1501,12 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       exchange_scalars(fl);
     }
     timers[PH_COST].stop(stream);
-    if (nranks > 1)
+    if (nranks > 1) {
       HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 5) * sizeof(double), hipMemcpyDeviceToHost, stream));
-    spin_sync();
+      spin_sync();
+    } else {
+      flag_sync(h_step.p + arslam::kHostSeq, step_seq);
+    }
     const double *red = h_step.p;
     // A stuck dependency wait of a persistent executor is a device fault, not
     // an indefinite system: fail loudly instead of shrinking the radius.
