@@ -204,10 +204,6 @@ __device__ __forceinline__ double rowbcast(double v, int g) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
-#ifndef ARSLAM_D16_PERMLANE
-#define ARSLAM_D16_PERMLANE 0   // (debug variant: diag16's column j+2 by permlane swaps, not LDS)
-#endif
-
 // One elimination step of diag16 under an explicit exec mask (constant per
 // pivot, so no per-lane selects): in the rows below the pivot,
 // x_q += nf * xj_q and R += nf * rj; then, in the pivot column's group,
@@ -276,13 +272,8 @@ __device__ __forceinline__ void diag16_pivot(double (&x)[4], double &R, double &
   // pivot); then column j of those rows (group j / 4) becomes -f_ij
   elim_step<j>(x[0], x[1], x[2], x[3], R, nf, xj[0], xj[1], xj[2], xj[3], rj);
   if (j + 2 < 16) {   // column j+2 after this pivot, a pivot before it is needed
-#if ARSLAM_D16_PERMLANE
-    (void)colx;
-    R2 = rowbcast(x[(j + 2) & 3], (j + 2) >> 2);
-#else
     colx[lane] = x[(j + 2) & 3];
     R2 = colx[16 * ((j + 2) >> 2) + i];
-#endif
   }
 }
 
