@@ -1140,6 +1140,25 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   }
 }
 
+// The levels of offset < 64 of a block's pairwise tree reduction
+// red[t] = op(red[t], red[t + off]) (off = n/2 .. 1), on wave 0 by lane shifts
+// instead of an LDS round trip and a block barrier per level: the same pairs
+// in the same order, so the same bits.  v: lane t's red[t] after the level of
+// offset 64 (n: the elements left, <= 64); the result lands in lane 0.  All of
+// wave 0 must be active.
+__device__ __forceinline__ double wave_tree_sum(double v, int n) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+    if (off < n) v += __shfl_down(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_tree_max(double v, int n) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+    if (off < n) v = fmax(v, __shfl_down(v, off, kWave));
+  return v;
+}
+
 // Candidate update of the tag and camera slots from the reduced solution
 // (every f-side slot of xc is written, so xc needs no copy of x first:
 // k_backsub writes every capture slot).
@@ -1169,16 +1188,20 @@ __global__ __launch_bounds__(256) void k_update_f(DevProblem P, const double *__
   red[0][threadIdx.x] = st;
   red[1][threadIdx.x] = bad;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
+  for (int off = 128; off >= kWave; off >>= 1) {
     if (threadIdx.x < off) {
       red[0][threadIdx.x] += red[0][threadIdx.x + off];
       red[1][threadIdx.x] = fmax(red[1][threadIdx.x], red[1][threadIdx.x + off]);
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    fparts[2L * blockIdx.x] = red[0][0];
-    fparts[2L * blockIdx.x + 1] = red[1][0];
+  if (threadIdx.x < kWave) {
+    const double s0 = wave_tree_sum(red[0][threadIdx.x], kWave);
+    const double s1 = wave_tree_max(red[1][threadIdx.x], kWave);
+    if (threadIdx.x == 0) {
+      fparts[2L * blockIdx.x] = s0;
+      fparts[2L * blockIdx.x + 1] = s1;
+    }
   }
 }
 
@@ -1210,13 +1233,16 @@ __device__ __forceinline__ void reduce_parts_block(int p, const double *__restri
   }
   red[t] = acc;
   __syncthreads();
-  for (int off = 512; off > 0; off >>= 1) {
+  for (int off = 512; off >= kWave; off >>= 1) {
     if (t < off) red[t] = is_max ? fmax(red[t], red[t + off]) : red[t] + red[t + off];
     __syncthreads();
   }
-  if (t == 0) {
-    out[p] = red[0];
-    if (hout) hout[p] = red[0];
+  if (t < kWave) {
+    const double r = is_max ? wave_tree_max(red[t], kWave) : wave_tree_sum(red[t], kWave);
+    if (t == 0) {
+      out[p] = r;
+      if (hout) hout[p] = r;
+    }
   }
   if (flag && p == 0 && t == 0) {   // rides along the step's one host read
     const int f = *flag;
@@ -1305,7 +1331,7 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
   }
   for (int q = 0; q < 6; ++q) rs[q][t] = v[q];
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
+  for (int off = 128; off >= kWave; off >>= 1) {
     if (t < off) {
       rs[0][t] = fmax(rs[0][t], rs[0][t + off]);
       rs[1][t] += rs[1][t + off];
@@ -1316,6 +1342,11 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
     }
     __syncthreads();
   }
+  if (t < kWave)
+    for (int q = 0; q < 6; ++q) {
+      const double r = (q % 3 == 0) ? wave_tree_max(rs[q][t], kWave) : wave_tree_sum(rs[q][t], kWave);
+      if (t == 0) rs[q][0] = r;
+    }
   // out[8 + 6 b + q]: block b's partials; out[7] (as an int): blocks done.
   // The last block to finish reduces the kNormBlocks partials over a fixed
   // tree (independent of which block is last) into out[0..5], and resets the
@@ -1333,12 +1364,23 @@ __global__ __launch_bounds__(256) void k_slot_norms(long n, long cap_lo, long ca
   if (t < kNormBlocks)
     for (int q = 0; q < 6; ++q) rs[q][t] = part[6L * t + q];
   __syncthreads();
-  for (int off = kNormBlocks / 2; off > 0; off >>= 1) {
+  for (int off = kNormBlocks / 2; off >= kWave; off >>= 1) {
     if (t < off)
       for (int q = 0; q < 6; ++q)
         rs[q][t] = (q % 3 == 0) ? fmax(rs[q][t], rs[q][t + off]) : rs[q][t] + rs[q][t + off];
     __syncthreads();
   }
+  if (t < kWave) {
+    const int left = kNormBlocks < kWave ? kNormBlocks : kWave;
+    double r6[6];
+    for (int q = 0; q < 6; ++q) {
+      const double v0 = t < left ? rs[q][t] : 0.0;
+      r6[q] = (q % 3 == 0) ? wave_tree_max(v0, left) : wave_tree_sum(v0, left);
+    }
+    if (t == 0)
+      for (int q = 0; q < 6; ++q) rs[q][0] = r6[q];
+  }
+  __syncthreads();
   if (t < 6) {
     out[t] = rs[t][0];
     if (hout) {
