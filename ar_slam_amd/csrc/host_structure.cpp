@@ -726,8 +726,11 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   }
   for (auto &v : adj) L.n_edges += (long)v.size();
   if (prof) tl[1] = clk();
-  bool reuse = reuse_tag_row && (int)reuse_tag_row->size() == std::max(nt, 1) && 10 * L.n_edges <= 11 * reuse_edges;
-  for (int t = 0; reuse && t < nt; ++t) reuse = ((*reuse_tag_row)[t] >= 0) == (tfree[t] != 0);
+  // (tags past the earlier order's -- new parameter blocks are appended --
+  // are placed after its rows, at the end of its last part: below)
+  const int n_old = reuse_tag_row ? std::min((int)reuse_tag_row->size(), nt) : 0;
+  bool reuse = reuse_tag_row && (int)reuse_tag_row->size() <= std::max(nt, 1) && 10 * L.n_edges <= 11 * reuse_edges;
+  for (int t = 0; reuse && t < n_old; ++t) reuse = ((*reuse_tag_row)[t] >= 0) == (tfree[t] != 0);
   L.order_edges = reuse ? reuse_edges : L.n_edges;
   L.order_reused = reuse;
   std::vector<std::vector<int>> parts;
@@ -752,10 +755,20 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   }
   long row = 0, real = 0;
   if (reuse) {
-    L.tag_row = *reuse_tag_row;
-    for (int t = 0; t < nt; ++t)
+    for (int t = 0; t < n_old; ++t) L.tag_row[t] = (*reuse_tag_row)[t];
+    for (int t = 0; t < n_old; ++t)
       if (L.tag_row[t] >= 0) {
         row = std::max(row, (long)L.tag_row[t] + 6);
+        real += 6;
+      }
+    // the tags new since the order was made, at the end of its last part (the
+    // root separator): a valid order whatever they couple to, since every
+    // part's elimination path ends there; the caller recomputes the order
+    // once the tile elimination tree grows taller than a fresh one
+    for (int t = n_old; t < nt; ++t)
+      if (tfree[t]) {
+        L.tag_row[t] = (int)row;
+        row += 6;
         real += 6;
       }
   }
