@@ -1175,6 +1175,10 @@ struct DagArgs {
   int *ticket;                // its ticket counter
   int *progress;              // debug: [grid][4] host-visible (ticket, phase, task type, spins)
   unsigned long long *trace;  // debug: [n_tasks][8] s_memrealtime at draw / waits met / end, workgroup, sub-phases
+  // tiles >= first_store are fill tiles the Schur gather does not write -- S
+  // never clears them, and their first update stores 0 - acc instead of
+  // reading the tile (INT_MAX: every tile is cleared and read-modify-written)
+  int first_store;
 };
 
 // A ticket's 32-int record: two scalar loads in flight, one wait (the record
@@ -1637,6 +1641,11 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
       double *C = a.S + (long)task.w * (T64 * T64);
       double cv[16];
       bool c_pre = false;
+      if (task.z == 0 && task.w >= a.first_store) {   // (0 - acc below: the same bits)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) cv[u] = 0.0;
+        c_pre = true;
+      }
       for (int q = it.y; q < it.z; ++q) {
         // (operand tile ids: the first column's in the record, no column -> tile lookup chain)
         const int2 kt = q == it.y ? make_int2(r[kRecTile0I], r[kRecTile0J]) : a.ks_tiles[q];
@@ -1657,7 +1666,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         else
           load_tile_wt(a.S + (long)kt.x * (T64 * T64), D, tid);
         __syncthreads();
-        const bool c_issue = q == it.z - 1 && sid < 0 && sh[3];
+        const bool c_issue = q == it.z - 1 && sid < 0 && sh[3] && !c_pre;
         if (c_issue) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -2029,7 +2038,7 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
 }
 
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
-                          unsigned long long *trace, bool reset, int phase) {
+                          unsigned long long *trace, bool reset, int phase, long first_store) {
   const int t_begin = phase == 1 ? (int)P.phase_split : 0;
   const int t_end = phase == 0 ? (int)P.phase_split : (int)P.n_dag_tasks;
   if (t_end <= t_begin) return;
@@ -2040,7 +2049,8 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
   }
   DagArgs a{S, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_rec, P.dag_ks_tiles, P.upd_ks, P.dag_claimed,
             P.dag_waits, P.dag_counters, (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_part, P.upd_cnt, flag, t_begin, t_end,
-            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagOffTicket1 : kDagOffTicket0), progress, trace};
+            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagOffTicket1 : kDagOffTicket0), progress, trace,
+            (int)std::min<long>(first_store, INT_MAX)};
   // A small task graph runs on fewer workgroups (a quarter of its tasks, at
   // least 64): its time is the elimination tree's chain, which runs faster
   // beside fewer co-resident update workgroups (cfg2, 580 tasks: 219.6 us on

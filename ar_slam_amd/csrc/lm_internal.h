@@ -11,6 +11,7 @@
 // reduced matrix is an arrow-head (sparse tag block + one dense border).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <climits>
 #include <cstdint>
 #include <stdexcept>
 #include <vector>
@@ -431,9 +432,12 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
 // (tickets in a topological order, dependency counters in global memory).
 // (reset = false: the counters were zeroed by launch_exec_reset)
 // (phase: -1 every task; 0 / 1 one phase of a multi-rank plan, LltPlan)
+// (first_store: the tiles from first_store on are fill tiles the Schur gather
+// does not write and S is not cleared for -- their first update stores
+// instead of reading the tile; LONG_MAX: none)
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups,
                           int *progress = nullptr, unsigned long long *trace = nullptr, bool reset = true,
-                          int phase = -1);
+                          int phase = -1, long first_store = LONG_MAX);
 // the LM diagonal clamp(s^2 colnorm, dmin, dmax) over n slots (k_lm_diag)
 struct LmDiagArgs {
   long n;

@@ -273,6 +273,11 @@ struct arslam_lm {
   int2 *u_dest_row = nullptr;
   int4 *u_gather_items = nullptr, *u_gather_splits = nullptr;
   arslam::SchurContrib *u_contrib = nullptr;
+  // One rank, persistent executor: the fill tiles (numbered after the
+  // assembled ones) are never cleared -- their first update stores.  n_clear:
+  // the tiles k_schur clears (the assembled ones; every tile when an appended
+  // problem's gather writes into a fill tile: then no first-update store)
+  long n_clear = 0;
   DevBuf<double> d_xa, d_xb, d_xbest, d_g, d_colnorm, d_scale, d_diag;
   DevBuf<double> d_obs_tg, d_parts, d_fparts, d_red, d_S, d_z, d_yF;
   // the reduced system's tiles: Sp = d_S.p + s_pre.  Several ranks: the top
@@ -836,6 +841,21 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
     upload.add(&u_gather_items, reinterpret_cast<const int4 *>(sg.items.data()), n_items);
     upload.add(&u_gather_splits, reinterpret_cast<const int4 *>(sg.splits.data()), n_splits);
   }
+  n_clear = has_f ? plan.n_tiles : 0;
+  if (has_f && nranks == 1) {
+    // does the gather write into a fill tile (an appended problem's new
+    // coupling; the plan is kept)?
+    const int T = plan.T;
+    bool fill_gathered = false;
+    for (int d = 0; d < n_dest && !fill_gathered; ++d) {
+      const int rX = sg.dest_row[2L * d], rY = sg.dest_row[2L * d + 1];
+      const int sx = (rX == nR || rX == L.cam_row) ? 1 : 6, sy = rY == L.cam_row ? 1 : 6;
+      for (int I = rX >> 6; I <= (rX + sx - 1) >> 6; ++I)
+        for (int J = rY >> 6; J <= (rY + sy - 1) >> 6 && J <= I; ++J)
+          fill_gathered = fill_gathered || plan.h_tile_id[(long)I * T + J] >= plan.n_assembled;
+    }
+    if (!fill_gathered) n_clear = plan.n_assembled;
+  }
   upload.commit(stream);
   d_xa.alloc(n); d_xb.alloc(n); d_xbest.alloc(n);
   d_g.alloc(n); d_colnorm.alloc(n); d_scale.alloc(n); d_diag.alloc(n);
@@ -1369,8 +1389,11 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       // included).  Several: this rank's captures' share; the D_f^2 of the
       // rank's own subtree rows now, of the top rows after their exchange
       // (below).  k_schur's extra blocks clear S's tiles first.
-      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, Sp, stream, nranks == 1, plan.n_tiles,
-                           reset_in_schur ? &er : nullptr);
+      // (one rank on the persistent executor: the fill tiles the gather does
+      // not write are left as they are -- their first update stores)
+      const bool fill_first_store = nranks == 1 && opt.factor_executor == 1;
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, Sp, stream, nranks == 1,
+                           fill_first_store ? n_clear : plan.n_tiles, reset_in_schur ? &er : nullptr);
       const bool force_indefinite = dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull;
       const long hook_row = P.cam_row >= 0 ? P.cam_row : nR - 1;   // (a top row with several ranks)
       if (nranks > 1) arslam::launch_prep_reduced(P, d_diag.p, radius, Sp, stream, 0);
@@ -1387,7 +1410,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           DevBuf<unsigned long long> tr;
           tr.alloc(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemsetAsync(tr.p, 0, tr.n * 8, stream));
-          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, tr.p, false);
+          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, tr.p, false, -1,
+                                       fill_first_store ? n_clear : LONG_MAX);
           std::vector<unsigned long long> h(8 * plan.n_dag_tasks);
           HIP_CHECK(hipMemcpyAsync(h.data(), tr.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
           HIP_CHECK(hipStreamSynchronize(stream));
@@ -1427,7 +1451,8 @@ void arslam_lm::solve(arslam_lm_summary *s) {
           arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, 1);
           timers[PH_FAC1].stop(stream);
         } else {
-          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false);
+          arslam::launch_dense_llt_dag(plan, Sp, d_flag.p, stream, dag_workgroups, nullptr, nullptr, false, -1,
+                                       fill_first_store ? n_clear : LONG_MAX);
         }
         if (rec) {
           HIP_CHECK(hipEventRecord(upd_timing.ev[2 * upd_timing.used + 1], stream));
