@@ -349,6 +349,29 @@ extern "C" int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[
   }
 }
 
+extern "C" int arslam_debug_mixed_groups(const arslam_soa_problem *p, int out[4], unsigned char *e_cap,
+                                         unsigned char *e_tag) {
+  if (!p || !out) return ARSLAM_E_INVALID_ARG;
+  try {
+    std::vector<uint8_t> ec, et;
+    (void)arslam::ceres_schur_side(p, &ec, &et);
+    if (e_cap) std::copy(ec.begin(), ec.end(), e_cap);
+    if (e_tag) std::copy(et.begin(), et.end(), e_tag);
+    const arslam::MixedProblem m = arslam::mixed_problem(*p, ec, et);
+    arslam::HostProblem h = arslam::host_problem(&m.soa, nullptr);
+    arslam::mixed_patch(h, m, *p);
+    out[0] = h.nc;
+    out[1] = h.nt;
+    out[2] = m.n_direct;
+    out[3] = h.maxblk;
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}
+
 // diagnostic build only (-DARSLAM_SCHUR_STAMPS): accumulated per-phase cycles of k_schur
 extern "C" int arslam_debug_schur_stamps(unsigned long long out[16]) {
   if (!out) return ARSLAM_E_INVALID_ARG;

@@ -454,8 +454,10 @@ double scalar_cholesky_flops(const std::vector<std::vector<int>> &adj, const std
 // blocks of one residual.  The vertices are stable-sorted by ascending degree
 // and taken greedily: a vertex none of whose neighbours is taken joins the
 // independent set (the e-blocks).
-SchurSide ceres_schur_side(const arslam_soa_problem *p) {
+SchurSide ceres_schur_side(const arslam_soa_problem *p, std::vector<uint8_t> *e_cap, std::vector<uint8_t> *e_tag) {
   SchurSide out;
+  if (e_cap) e_cap->assign(p ? std::max(p->n_cap, 0) : 0, 0);
+  if (e_tag) e_tag->assign(p ? std::max(p->n_tag, 0) : 0, 0);
   api_check(p != nullptr, ARSLAM_E_INVALID_ARG, "null problem");
   api_check(p->n_cap >= 0 && p->n_tag >= 0 && p->n_obs >= 0, ARSLAM_E_INVALID_ARG, "negative sizes");
   api_check(!p->n_obs || (p->obs_cap && p->obs_tag), ARSLAM_E_INVALID_ARG, "null observation arrays");
@@ -559,6 +561,7 @@ SchurSide ceres_schur_side(const arslam_soa_problem *p) {
     if (cam_free && color[0] == kWhite) color[0] = kGrey;
     if (v <= nc) {
       ++out.e_cap;
+      if (e_cap) (*e_cap)[v - 1] = 1;
       for (int q = cap_adj_start[v - 1]; q < cap_adj_start[v]; ++q) {
         const int u = 1 + nc + cap_adj[q];
         if (color[u] == kWhite) color[u] = kGrey;
@@ -566,6 +569,7 @@ SchurSide ceres_schur_side(const arslam_soa_problem *p) {
     } else {
       ++out.e_tag;
       const int t = v - 1 - nc;
+      if (e_tag) (*e_tag)[t] = 1;
       for (int q = tag_adj_start[t]; q < tag_adj_start[t + 1]; ++q) {
         const int u = 1 + tag_adj[q];
         if (color[u] == kWhite) color[u] = kGrey;
@@ -582,6 +586,113 @@ arslam_soa_problem swap_roles(const arslam_soa_problem &p) {
   s.obs_cap = p.obs_tag; s.obs_tag = p.obs_cap;
   s.cap_const = p.tag_const; s.tag_const = p.cap_const;
   return s;
+}
+
+MixedProblem mixed_problem(const arslam_soa_problem &p, const std::vector<uint8_t> &e_cap,
+                           const std::vector<uint8_t> &e_tag) {
+  MixedProblem m;
+  const int nc = p.n_cap, nt = p.n_tag, nb = p.n_obs;
+  std::vector<int> cap_f(nc, -1), tag_f(nt, -1), cap_g(nc, -1), tag_g(nt, -1), cap_d(nc, -1);
+  for (int t = 0; t < nt; ++t)
+    if (!e_tag[t]) { tag_f[t] = (int)m.f_src.size(); m.f_src.push_back(t); m.f_is_cap.push_back(0); }
+  for (int c = 0; c < nc; ++c)
+    if (!e_cap[c]) { cap_f[c] = (int)m.f_src.size(); m.f_src.push_back(c); m.f_is_cap.push_back(1); }
+  for (int c = 0; c < nc; ++c)
+    if (e_cap[c]) { cap_g[c] = (int)m.kind.size(); m.kind.push_back(kMixCap); m.group_src.push_back(c); }
+  for (int t = 0; t < nt; ++t)
+    if (e_tag[t]) { tag_g[t] = (int)m.kind.size(); m.kind.push_back(kMixTag); m.group_src.push_back(t); }
+  for (int b = 0; b < nb; ++b) {
+    const int c = p.obs_cap[b], t = p.obs_tag[b];
+    api_check(!(e_cap[c] && e_tag[t]), ARSLAM_E_INVALID_ARG, "mixed e-set: a residual joins two e-blocks");
+    if (!e_cap[c] && !e_tag[t] && cap_d[c] < 0) {
+      cap_d[c] = (int)m.kind.size();
+      m.kind.push_back(kMixDirect);
+      m.group_src.push_back(c);
+    }
+  }
+  const int ng = (int)m.kind.size(), nf = (int)m.f_src.size();
+  m.f_alias.assign(nf, -1);
+  for (int c = 0; c < nc; ++c)
+    if (cap_d[c] >= 0) { m.f_alias[cap_f[c]] = cap_d[c]; ++m.n_direct; }
+  m.obs_cap.resize(nb);
+  m.obs_tag.resize(nb);
+  for (int b = 0; b < nb; ++b) {
+    const int c = p.obs_cap[b], t = p.obs_tag[b];
+    if (e_cap[c]) { m.obs_cap[b] = cap_g[c]; m.obs_tag[b] = tag_f[t]; }
+    else if (e_tag[t]) { m.obs_cap[b] = tag_g[t]; m.obs_tag[b] = cap_f[c]; }
+    else { m.obs_cap[b] = cap_d[c]; m.obs_tag[b] = tag_f[t]; }
+  }
+  m.cap.resize(6L * ng);
+  m.tag.resize(6L * nf);
+  m.cap_const.resize(ng);
+  m.tag_const.resize(nf);
+  for (int g = 0; g < ng; ++g) {
+    const bool is_tag = m.kind[g] == kMixTag;
+    const unsigned char *cst = is_tag ? p.tag_const : p.cap_const;
+    m.cap_const[g] = cst ? cst[m.group_src[g]] : 0;
+  }
+  for (int f = 0; f < nf; ++f) {
+    const unsigned char *cst = m.f_is_cap[f] ? p.cap_const : p.tag_const;
+    m.tag_const[f] = cst ? cst[m.f_src[f]] : 0;
+  }
+  m.soa = p;
+  m.soa.n_cap = ng;
+  m.soa.n_tag = nf;
+  m.soa.cap = m.cap.data();
+  m.soa.tag = m.tag.data();
+  m.soa.obs_cap = m.obs_cap.data();
+  m.soa.obs_tag = m.obs_tag.data();
+  m.soa.cap_const = m.cap_const.data();
+  m.soa.tag_const = m.tag_const.data();
+  std::vector<double> x(3 + 6L * ng + 6L * nf);
+  mixed_values(m, p, x.data());
+  if (ng) std::memcpy(m.cap.data(), x.data() + 3, 6L * ng * sizeof(double));
+  if (nf) std::memcpy(m.tag.data(), x.data() + 3 + 6L * ng, 6L * nf * sizeof(double));
+  return m;
+}
+
+void mixed_values(const MixedProblem &m, const arslam_soa_problem &p, double *x) {
+  const long ng = (long)m.kind.size(), nf = (long)m.f_src.size();
+  std::memcpy(x, p.camera, 3 * sizeof(double));
+  for (long g = 0; g < ng; ++g) {
+    const double *src = m.kind[g] == kMixTag ? p.tag : p.cap;
+    std::memcpy(x + 3 + 6 * g, src + 6L * m.group_src[g], 6 * sizeof(double));
+  }
+  for (long f = 0; f < nf; ++f) {
+    const double *src = m.f_is_cap[f] ? p.cap : p.tag;
+    std::memcpy(x + 3 + 6 * ng + 6 * f, src + 6L * m.f_src[f], 6 * sizeof(double));
+  }
+}
+
+void mixed_patch(HostProblem &h, const MixedProblem &m, const arslam_soa_problem &p) {
+  const int ng = h.nc, nf = h.nt;
+  // the direct groups' own f-block, last in their block lists
+  std::vector<int> own(ng, -1);
+  for (int f = 0; f < nf; ++f)
+    if (m.f_alias[f] >= 0) own[m.f_alias[f]] = f;
+  std::vector<int> start(ng + 1, 0), blk;
+  blk.reserve(h.blk_tag.size() + m.n_direct);
+  h.maxblk = 0;
+  for (int g = 0; g < ng; ++g) {
+    start[g] = (int)blk.size();
+    blk.insert(blk.end(), h.blk_tag.begin() + h.cap_blk_start[g], h.blk_tag.begin() + h.cap_blk_start[g + 1]);
+    if (own[g] >= 0) blk.push_back(own[g]);
+    h.maxblk = std::max(h.maxblk, (int)blk.size() - start[g]);
+  }
+  start[ng] = (int)blk.size();
+  h.cap_blk_start.swap(start);
+  h.blk_tag.swap(blk);
+  api_check(h.maxblk <= kMaxSchurBlocks, ARSLAM_E_UNSUPPORTED,
+            "an eliminated block (or a direct group) couples more than 256 distinct blocks");
+  // an f-block is free iff its original block is (a capture on the reduced side
+  // may be used only by residuals of its own direct group)
+  std::vector<char> used_c(p.n_cap, 0), used_t(p.n_tag, 0);
+  for (int b = 0; b < p.n_obs; ++b) { used_c[p.obs_cap[b]] = 1; used_t[p.obs_tag[b]] = 1; }
+  for (int f = 0; f < nf; ++f) {
+    const int o = m.f_src[f];
+    const bool fr = (m.f_is_cap[f] ? used_c[o] : used_t[o]) && !m.tag_const[f];
+    for (int j = 0; j < 6; ++j) h.slot_free[3 + 6L * ng + 6L * f + j] = fr;
+  }
 }
 
 HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum) {
@@ -700,18 +811,24 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
         for (int b = 0; b < nt; ++b)
           if (bm[(size_t)a * nt + b] && tfree[a] && tfree[b]) adj[a].push_back(b);
     } else {
-      // per tag, the distinct tags of the captures observing it (a stamp
-      // array dedupes them before the sort: the pairs repeat in every
-      // capture that sees both)
-      std::vector<int> obs_cap(h.cap_start.empty() ? 0 : h.cap_start[nc]);
-      for (int c = 0; c < nc; ++c)
-        for (int o = h.cap_start[c]; o < h.cap_start[c + 1]; ++o) obs_cap[o] = c;
+      // per tag, the distinct tags of the captures whose blocks list it (a
+      // stamp array dedupes them before the sort: the pairs repeat in every
+      // capture that sees both; a mixed set's direct group lists its own
+      // pose, which no residual of the group has as its tag)
+      std::vector<int> tcap_start(nt + 1, 0), tcap(h.blk_tag.size());
+      for (int t : h.blk_tag) tcap_start[t + 1]++;
+      for (int t = 0; t < nt; ++t) tcap_start[t + 1] += tcap_start[t];
+      {
+        std::vector<int> fill(tcap_start.begin(), tcap_start.end() - 1);
+        for (int c = 0; c < nc; ++c)
+          for (int bb = h.cap_blk_start[c]; bb < h.cap_blk_start[c + 1]; ++bb) tcap[fill[h.blk_tag[bb]]++] = c;
+      }
       std::vector<int> stamp(nt, -1);
       for (int a = 0; a < nt; ++a) {
         if (!tfree[a]) continue;
         std::vector<int> &v = adj[a];
-        for (int q = h.tag_start[a]; q < h.tag_start[a + 1]; ++q) {
-          const int c = obs_cap[h.tag_obs[q]];
+        for (int q = tcap_start[a]; q < tcap_start[a + 1]; ++q) {
+          const int c = tcap[q];
           for (int bb = h.cap_blk_start[c]; bb < h.cap_blk_start[c + 1]; ++bb) {
             const int b = h.blk_tag[bb];
             if (b != a && tfree[b] && stamp[b] != a) {

@@ -82,9 +82,47 @@ struct SchurSide {
   int max_tag_obs = 0;
   int max_cap_blk = 0, max_tag_blk = 0;
 };
-SchurSide ceres_schur_side(const arslam_soa_problem *p);
+// (e_cap / e_tag: also the set itself, 1 per eliminated capture / tag)
+SchurSide ceres_schur_side(const arslam_soa_problem *p, std::vector<uint8_t> *e_cap = nullptr,
+                           std::vector<uint8_t> *e_tag = nullptr);
 // the same problem with the roles of captures and tags exchanged (pointers only)
 arslam_soa_problem swap_roles(const arslam_soa_problem &p);
+
+// Ceres' exact e-block set when it mixes captures and tags (ARSLAM_ELIM_MIXED),
+// as a device problem the per-e-block kernels run unchanged per group:
+//   "captures" (groups, the kernels' e-slots): the eliminated captures (kind
+//     kMixCap), the eliminated tags (kind kMixTag: roles swapped, as under tag
+//     elimination) and, per capture on the reduced side that has residuals
+//     with no e-block (both poses on the reduced side), one direct group (kind
+//     kMixDirect) holding those residuals -- its own pose is not eliminated:
+//     its k_schur wave stores the plain normal-equation blocks, its own pose
+//     included as one more local f-block (appended last, mixed_patch);
+//   "tags" (f-blocks, the reduced side): every tag and capture outside the
+//     set (tags first, then captures).
+// A direct group's slot is a copy of its capture's f-block slot: the same
+// values, scale and step, summed into the f-block's gradient / column norm
+// (f_alias) and left out of the norms (DevProblem::f_own).
+enum MixKind : unsigned char { kMixCap = 0, kMixTag = 1, kMixDirect = 2 };
+struct MixedProblem {
+  arslam_soa_problem soa{};               // the device problem (points into the arrays below)
+  std::vector<double> cap, tag;
+  std::vector<int> obs_cap, obs_tag;
+  std::vector<unsigned char> cap_const, tag_const;
+  std::vector<unsigned char> kind;        // [groups]
+  std::vector<int> group_src;             // [groups] original capture (kMixCap, kMixDirect) or tag (kMixTag)
+  std::vector<int> f_src;                 // [f-blocks] original tag or capture
+  std::vector<unsigned char> f_is_cap;    // [f-blocks]
+  std::vector<int> f_alias;               // [f-blocks] the direct group copying it, -1
+  int n_direct = 0;
+};
+// p's observations regrouped by the e-set (e_cap / e_tag from ceres_schur_side)
+MixedProblem mixed_problem(const arslam_soa_problem &p, const std::vector<uint8_t> &e_cap,
+                           const std::vector<uint8_t> &e_tag);
+// host_problem(&m.soa) patched: each direct group's own f-block appended to its
+// block list, and every f-block free iff its original block is
+void mixed_patch(HostProblem &h, const MixedProblem &m, const arslam_soa_problem &p);
+// the parameter vector of the mixed device problem from the original blocks
+void mixed_values(const MixedProblem &m, const arslam_soa_problem &p, double *x);
 
 // Row layout of the reduced system and its tile pattern (before fill).
 //   ordering 0 natural, 1 reverse Cuthill-McKee, 2 nested dissection (parts

@@ -104,6 +104,11 @@ struct DevProblem {
   // residual is then evaluated with the two pose arguments exchanged and the
   // two 6-column halves of its Jacobian row swapped back into e|f order
   int swap_roles;
+  // ARSLAM_ELIM_MIXED (MixedProblem): each group's kind (kMixCap, kMixTag --
+  // roles swapped for that group -- or kMixDirect), and per f-block the direct
+  // group whose slot copies it, -1; null otherwise (swap_roles holds for all)
+  const unsigned char *cap_kind = nullptr;
+  const int *f_alias = nullptr;
   int nf;                    // f-side parameter slots: camera 3 + 6 nt
   const int *fslot_row;      // [nf]    reduced row of f-side slot j (camera j < 3, tag slot 3 + 6 t + a), -1 if none
   int cam_row;               // first reduced row of the camera block, -1 if the camera is not free

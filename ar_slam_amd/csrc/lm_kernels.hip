@@ -56,6 +56,15 @@ namespace {
 __device__ __forceinline__ long slot_cap(const DevProblem &P, int c) { return 3 + 6L * c; }
 __device__ __forceinline__ long slot_tag(const DevProblem &P, int t) { return 3 + 6L * P.nc + 6L * t; }
 
+// does group c evaluate its residuals with the two poses exchanged (its e-block is a tag)?
+__device__ __forceinline__ bool group_swapped(const DevProblem &P, int c) {
+  return P.cap_kind ? P.cap_kind[c] == kMixTag : P.swap_roles != 0;
+}
+// a direct group of the mixed e-set (its own pose stays on the reduced side)?
+__device__ __forceinline__ bool group_direct(const DevProblem &P, int c) {
+  return P.cap_kind && P.cap_kind[c] == kMixDirect;
+}
+
 __device__ __forceinline__ double lm_d2(const double *diag, long slot, double radius) {
   const double d = sqrt(diag[slot] / radius);   // lm_diagonal_ = sqrt(diag / radius)
   return d * d;
@@ -81,7 +90,7 @@ __device__ __forceinline__ void fill_rows(const DevProblem &P, const double *x, 
     double J[13];
     // (tag elimination: the e-block is the problem's tag -- projectCorner
     // still takes the capture first; the Jacobian halves come back as e|f)
-    const bool sw = P.swap_roles != 0;
+    const bool sw = group_swapped(P, c);
     const double r = residual_jacobian_row(cam, sw ? tag : cap, sw ? cap : tag, corner, comp,
                                            P.corners[8L * obs + 2 * corner + comp], J);
     if (sw) {
@@ -342,6 +351,17 @@ __device__ __forceinline__ void tag_reduce_elem(const DevProblem &P, const doubl
     for (int u = 0; u < 32; ++u) s += (q0 + u < qb) ? v[u] : 0.0;
   }
   const long slot = slot_tag(P, t) + (j % 6);
+  if (P.f_alias) {
+    // (mixed e-set) a capture on the reduced side with a direct group: that
+    // group's sums over its own pose (k_linearize) belong to this block; the
+    // group's slot gets the total too, so its scale and LM diagonal are the block's
+    const int d = P.f_alias[t];
+    if (d >= 0) {
+      double *dv = (j < 6 ? g : colnorm) + slot_cap(P, d) + (j % 6);
+      s += *dv;
+      *dv = P.slot_free[slot] ? s : 0.0;
+    }
+  }
   const double v = P.slot_free[slot] ? s : 0.0;
   if (j < 6) g[slot] = v; else colnorm[slot] = v;
 }
@@ -363,6 +383,55 @@ __global__ void k_lm_diag(long n, const double *__restrict__ scale, const double
   if (i >= n) return;
   const double d = scale[i] * scale[i] * colnorm[i];   // squared column norm of J * diag(s)
   diag[i] = fmin(fmax(d, dmin), dmax);
+}
+
+// A direct group of the mixed e-set (MixedProblem): residuals whose two poses
+// are both on the reduced side, grouped by their capture, whose pose is the
+// group's last local f-block (nblk - 1: no residual lists it, so its W, F'r and
+// F'F entries stayed zero).  Nothing is eliminated: the stored local system is
+// the plain normal-equation blocks of [f | tag blocks | own pose | r] (Ceres'
+// SchurEliminator adds such rows to the reduced system as they are), the own
+// pose's from the capture-wide sums U = E'E, E'f, E'F_u and E'r.
+__device__ void store_direct_group(double *out, int nblk, int m, const double *U, const double *Etr, const double *W,
+                                   const double *Ftr, const double *FF, double ff00, int lane) {
+  const int own = nblk - 1;
+  // local column x: 0 f, 1 a tag block's row, 2 the own pose's, 3 the rhs; u its block, i the row in it
+  auto cls = [&](int x, int &u, int &i) {
+    u = x >= 1 && x < m ? (x - 1) / 6 : 0;
+    i = x >= 1 && x < m ? (x - 1) - 6 * u : 0;
+    return x == 0 ? 0 : x == m ? 3 : (u == own ? 2 : 1);
+  };
+  for (int Ub = 0; Ub <= nblk + 1; ++Ub) {
+    const int sU = schur_blk_size(Ub, nblk), p0 = schur_blk_start(Ub, nblk), ncol = p0 + sU;
+    double *dst = out + schur_block_off(Ub, 0, nblk);
+    for (int e = lane; e < sU * ncol; e += kWave) {
+      const int ip = e / ncol, q = e - ip * ncol, p = p0 + ip;
+      int ua, ia, ub, ib;
+      int ka = cls(q, ua, ia), kb = cls(p, ub, ib);   // (the pair in f < tag < own < rhs order)
+      if (ka > kb || (ka == kb && q > p)) {
+        const int tk = ka, tu = ua, ti = ia;
+        ka = kb; ua = ub; ia = ib;
+        kb = tk; ub = tu; ib = ti;
+      }
+      double v = 0.0;
+      if (ka == 0) {
+        v = kb == 0 ? ff00 : kb == 1 ? FF[28 * ub + 21 + ib] : kb == 2 ? W[ib * m] : Ftr[0];
+      } else if (ka == 1) {
+        if (kb == 1) {
+          if (ua == ub) {
+            const int lo = min(ia, ib), hi = max(ia, ib);
+            v = FF[28 * ua + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+          }
+        } else {
+          v = kb == 2 ? W[ib * m + 1 + 6 * ua + ia] : Ftr[1 + 6 * ua + ia];
+        }
+      } else if (ka == 2) {
+        v = kb == 2 ? U[6 * ia + ib] : Etr[ia];
+      }
+      const int V = schur_blk(q, m), q0V = schur_blk_start(V, nblk);
+      dst[(long)sU * q0V + ip * schur_blk_size(V, nblk) + (q - q0V)] = v;
+    }
+  }
 }
 
 // Schur elimination of capture c (ComputeTrustRegionStep's DENSE_SCHUR
@@ -554,6 +623,10 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   }
   __syncthreads();
   SCHUR_STAMP(1);
+  if (group_direct(P, c)) {
+    store_direct_group(P.slab + P.cap_off[c], nblk, m, U, Etr, W, Ftr, FF, *ff00, lane);
+    return;
+  }
   // (U + D_c^2)^{-1}: every lane factors U (one reciprocal per pivot), lane j
   // solves for column j
   {
@@ -953,7 +1026,7 @@ __device__ __forceinline__ void capture_cost(const DevProblem &P, const double *
       const double *tag = x + slot_tag(P, P.obs_tag[obs]);
       const AngleAxis at = aa_prepare(tag + 3);
       const double obsv = P.corners[8L * obs + 2 * corner + comp];
-      const bool sw = P.swap_roles != 0;   // tag elimination: the capture is the f-block
+      const bool sw = group_swapped(P, c);   // tag e-block: the capture is the f-block
       const double r = residual_row(sw ? at : ac, sw ? tag : cap, sw ? ac : at, sw ? cap : tag, cam[0], corner,
                                     comp, obsv, nullptr, nullptr);
       if (!isfinite(r)) bad = 1.0;
@@ -1069,7 +1142,15 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
     }
   }
   __syncthreads();
-  if (reuse_ui) {
+  const bool direct = group_direct(P, c);
+  if (direct) {
+    // (mixed e-set) a direct group's own pose is a reduced-side block (its last
+    // local block): its step is the reduced solution's, as k_update_f forms it
+    if (lane < 6) {
+      const int r0 = P.tag_row[P.blk_tag[P.cap_blk_start[c + 1] - 1]];
+      yc[lane] = r0 >= 0 ? yF[r0 + lane] : 0.0;
+    }
+  } else if (reuse_ui) {
     if (lane < 6) {
       double t = 0.0;
 #pragma unroll
@@ -1122,7 +1203,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
     const double xn = xo + d;
     xc[sc + lane] = xn;
     capc[lane] = xn;
-    if (P.slot_free[sc + lane]) st = (xo - xn) * (xo - xn);
+    if (P.slot_free[sc + lane] && !direct) st = (xo - xn) * (xo - xn);   // (a direct group: counted on its f-block)
     bad = isfinite(yv) ? 0.0 : 1.0;
   }
   st = wave_sum(st);

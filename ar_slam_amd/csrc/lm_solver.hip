@@ -263,6 +263,8 @@ struct arslam_lm {
       *u_blk_tag = nullptr, *u_tag_start = nullptr, *u_tag_obs = nullptr, *u_tag_row = nullptr,
       *u_row_slot = nullptr, *u_fslot_row = nullptr, *u_dest_start = nullptr, *u_big_caps = nullptr;
   unsigned char *u_f_own = nullptr;
+  unsigned char *u_cap_kind = nullptr;   // ARSLAM_ELIM_MIXED: DevProblem::cap_kind, f_alias
+  int *u_f_alias = nullptr;
   std::vector<unsigned char> f_own;   // several ranks: DevProblem::f_own
   std::vector<int> big_caps;   // captures with more than kSchurMfmaBlocks distinct tags (k_schur's second launch)
   std::vector<int> chunk_caps;   // captures with more than kObsChunk observations (the chunked launches)
@@ -449,6 +451,7 @@ struct arslam_lm {
   bool pk_appended_only = false;  // since the last load only residual blocks of known tags were added
   int setup_kind = ARSLAM_SETUP_LOAD;
   int elim_used = ARSLAM_ELIM_CAPTURES;   // the side load() eliminates (the device problem is role-swapped for TAGS)
+  arslam::MixedProblem mx;                // ARSLAM_ELIM_MIXED: the regrouped device problem (host_structure.h)
   int ceres_e_cap = 0, ceres_e_tag = 0;   // Ceres 2.0's e-block set of the loaded problem, by kind
   void reload_values(const arslam_soa_problem *p);
   bool pk_loaded = false;   // the resident problem came from the pointer-keyed API
@@ -608,7 +611,10 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   ensure_stream();
   // the e-block side (ARSLAM_ELIM_*): Ceres' own independent set decides AUTO;
   // tag elimination runs the same kernels on the role-swapped problem
-  const arslam::SchurSide cs = arslam::ceres_schur_side(p_in);
+  std::vector<uint8_t> e_cap, e_tag;
+  const bool want_set = opt.elimination == ARSLAM_ELIM_MIXED;
+  const arslam::SchurSide cs =
+      arslam::ceres_schur_side(p_in, want_set ? &e_cap : nullptr, want_set ? &e_tag : nullptr);
   ceres_e_cap = cs.e_cap;
   ceres_e_tag = cs.e_tag;
   // (an eliminated block's local system over its distinct f-blocks lives in
@@ -617,6 +623,15 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   int side = opt.elimination;
   if (side == ARSLAM_ELIM_AUTO)
     side = (nranks == 1 && tags_fit && (cs.e_tag > cs.e_cap || !caps_fit)) ? ARSLAM_ELIM_TAGS : ARSLAM_ELIM_CAPTURES;
+  if (side == ARSLAM_ELIM_MIXED) {
+    // Ceres' exact set: a whole side when it holds one kind only (then it is
+    // every free block of that kind), the mixed device problem otherwise; the
+    // camera joins it only in degenerate graphs (one residual), where the
+    // device eliminates the captures instead
+    fail_if(nranks > 1, ARSLAM_E_UNSUPPORTED, "the mixed e-block set is single-rank only (the ranks own captures)");
+    if (cs.e_cam || cs.e_tag == 0) side = ARSLAM_ELIM_CAPTURES;
+    else if (cs.e_cap == 0) side = ARSLAM_ELIM_TAGS;
+  }
   fail_if(side == ARSLAM_ELIM_TAGS && nranks > 1, ARSLAM_E_UNSUPPORTED,
           "tag elimination is single-rank only (the ranks own captures)");
   fail_if(nranks > 1 && opt.factor_executor != 1, ARSLAM_E_UNSUPPORTED,
@@ -625,10 +640,13 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
           "tag elimination: a tag seen by more than 256 distinct captures");
   fail_if(side == ARSLAM_ELIM_CAPTURES && !caps_fit, ARSLAM_E_UNSUPPORTED,
           "capture elimination: a capture sees more than 256 distinct tags");
-  if (side != elim_used) prev_tag_row.clear();   // the f-side changed: no order to reuse
+  // (the f-side changed, or is a mixed set of its own: no order to reuse)
+  if (side != elim_used || side == ARSLAM_ELIM_MIXED) prev_tag_row.clear();
   elim_used = side;
   const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
-  const arslam_soa_problem *p = side == ARSLAM_ELIM_TAGS ? &swapped : p_in;
+  if (side == ARSLAM_ELIM_MIXED) mx = arslam::mixed_problem(*p_in, e_cap, e_tag);
+  else mx = arslam::MixedProblem{};
+  const arslam_soa_problem *p = side == ARSLAM_ELIM_TAGS ? &swapped : side == ARSLAM_ELIM_MIXED ? &mx.soa : p_in;
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
   double tp[6] = {now_s(), 0, 0, 0, 0, 0};
   double t_host = tp[0];   // (one rank: after host_problem)
@@ -698,6 +716,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
       if (sl >= 3) sl -= (int)shift;
   } else {
     h = arslam::host_problem(p, nullptr);   // validates p
+    if (side == ARSLAM_ELIM_MIXED) arslam::mixed_patch(h, mx, *p_in);
     t_host = now_s();
     // (a grown pointer-keyed problem: a fresh order takes the faster separator search)
     L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
@@ -745,7 +764,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   tp[5] = now_s();
   if (nranks == 1) lay = std::move(L);   // (try_extend: an appended problem keeps this layout and plan)
   setup_kind = ARSLAM_SETUP_LOAD;
-  soa = *p;
+  soa = side == ARSLAM_ELIM_MIXED ? *p_in : *p;   // (mixed: write_back maps the device slots to p_in's blocks)
   loaded = true;
   pk_appended_only = true;
   const double t_end = now_s();
@@ -824,6 +843,16 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
       f_own[sl] = cls == 0 || (cls == 1 && rank == 0);
     }
     upload.add(&u_f_own, f_own.data(), f_own.size());
+  }
+  const bool mixed = elim_used == ARSLAM_ELIM_MIXED;
+  if (mixed) {
+    // the direct groups' slots copy f-block slots: counted once, on the f-block
+    f_own.assign(n, 1);
+    for (int g = 0; g < nc; ++g)
+      if (mx.kind[g] == arslam::kMixDirect) std::fill(f_own.begin() + 3 + 6L * g, f_own.begin() + 9 + 6L * g, 0);
+    upload.add(&u_f_own, f_own.data(), f_own.size());
+    upload.add(&u_cap_kind, mx.kind.data(), mx.kind.size());
+    upload.add(&u_f_alias, mx.f_alias.data(), mx.f_alias.size());
   }
   big_caps.clear();
   for (int c = 0; c < nc; ++c)
@@ -909,7 +938,9 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.tag_row = u_tag_row; P.row_slot = u_row_slot;
   P.tile_id = plan.tile_id; P.T = plan.T;
   P.tile_class = nranks > 1 && has_f ? plan.tile_class : nullptr;
-  P.f_own = nranks > 1 ? u_f_own : nullptr;
+  P.f_own = nranks > 1 || mixed ? u_f_own : nullptr;
+  P.cap_kind = mixed ? u_cap_kind : nullptr;
+  P.f_alias = mixed ? u_f_alias : nullptr;
   P.cap_off = u_cap_off; P.slab = d_slab.p; P.dest_row = u_dest_row; P.dest_start = u_dest_start;
   P.contrib = u_contrib; P.n_dest = n_dest; P.jrows = d_jrows.p; P.cap_ui = d_cap_ui.p;
   P.gather_items = u_gather_items; P.gather_splits = u_gather_splits; P.gather_part = d_gather_part.p;
@@ -931,7 +962,8 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
 // load() instead.  (summary.factor_scalar_flops keeps the loaded problem's
 // count: a new coupling inside a fill tile changes the scalar structure.)
 bool arslam_lm::try_extend(const arslam_soa_problem *p) {
-  if (!loaded || nranks > 1 || elim_used != ARSLAM_ELIM_CAPTURES || !has_f || opt.elimination == ARSLAM_ELIM_TAGS)
+  if (!loaded || nranks > 1 || elim_used != ARSLAM_ELIM_CAPTURES || !has_f ||
+      (opt.elimination != ARSLAM_ELIM_AUTO && opt.elimination != ARSLAM_ELIM_CAPTURES))
     return false;
   const double t0 = now_s();
   if (opt.elimination == ARSLAM_ELIM_AUTO) {   // the side Ceres would eliminate may change as the graph grows
@@ -1013,6 +1045,17 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
 // path when no block, residual or constant changed since the last load).
 void arslam_lm::reload_values(const arslam_soa_problem *p_in) {
   const double t0 = now_s();
+  if (elim_used == ARSLAM_ELIM_MIXED) {   // the regrouped slots from p_in's blocks
+    fail_if(!loaded || p_in->n_obs != (int)mx.obs_cap.size(), ARSLAM_E_STATE,
+            "reload_values: structure differs from the loaded problem");
+    arslam::mixed_values(mx, *p_in, x0.data());
+    HIP_CHECK(hipMemcpyAsync(u_x0, x0.data(), n * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    soa = *p_in;
+    setup_kind = ARSLAM_SETUP_VALUES;
+    setup_s = now_s() - t0;
+    return;
+  }
   const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
   const arslam_soa_problem *p = elim_used == ARSLAM_ELIM_TAGS ? &swapped : p_in;
   fail_if(!loaded || p->n_cap != nc_full || p->n_tag != nt || (nranks == 1 && p->n_obs != nb), ARSLAM_E_STATE,
@@ -1150,12 +1193,20 @@ void arslam_lm::write_back(const double *d_src) {
   spin_sync();
   const double *h = h_x.p;
   std::memcpy(soa.camera, h, 3 * sizeof(double));
-  if (nranks > 1) {   // this rank's captures into the whole problem's array
+  if (elim_used == ARSLAM_ELIM_MIXED) {   // groups (not the direct ones: copies) and f-blocks to their blocks
+    for (int g = 0; g < nc; ++g)
+      if (mx.kind[g] != arslam::kMixDirect)
+        std::memcpy((mx.kind[g] == arslam::kMixTag ? soa.tag : soa.cap) + 6L * mx.group_src[g], h + 3 + 6L * g,
+                    6 * sizeof(double));
+    for (int f = 0; f < nt; ++f)
+      std::memcpy((mx.f_is_cap[f] ? soa.cap : soa.tag) + 6L * mx.f_src[f], h + 3 + 6L * nc + 6L * f,
+                  6 * sizeof(double));
+  } else if (nranks > 1) {   // this rank's captures into the whole problem's array
     for (int c = 0; c < nc; ++c) std::memcpy(soa.cap + 6L * own_caps[c], h + 3 + 6L * c, 6 * sizeof(double));
   } else if (nc) {
     std::memcpy(soa.cap, h + 3, 6L * nc * sizeof(double));
   }
-  if (nt) std::memcpy(soa.tag, h + 3 + 6L * nc, 6L * nt * sizeof(double));
+  if (nt && elim_used != ARSLAM_ELIM_MIXED) std::memcpy(soa.tag, h + 3 + 6L * nc, 6L * nt * sizeof(double));
   if (pk_stage) scatter_to_blocks();
 }
 
@@ -1716,9 +1767,9 @@ int arslam_lm_create(arslam_lm **out, const arslam_lm_options *opt) {
   return guarded([&] {
     auto *h = new arslam_lm();
     if (opt) h->opt = *opt; else arslam_lm_options_init(&h->opt);
-    if (h->opt.elimination < ARSLAM_ELIM_AUTO || h->opt.elimination > ARSLAM_ELIM_TAGS) {
+    if (h->opt.elimination < ARSLAM_ELIM_AUTO || h->opt.elimination > ARSLAM_ELIM_MIXED) {
       delete h;
-      throw Error(ARSLAM_E_INVALID_ARG, "elimination must be ARSLAM_ELIM_AUTO, _CAPTURES or _TAGS");
+      throw Error(ARSLAM_E_INVALID_ARG, "elimination must be ARSLAM_ELIM_AUTO, _CAPTURES, _TAGS or _MIXED");
     }
     *out = h;
   });
@@ -1729,8 +1780,8 @@ void arslam_lm_destroy(arslam_lm *h) { delete h; }
 int arslam_lm_set_options(arslam_lm *h, const arslam_lm_options *opt) {
   if (!h || !opt) return ARSLAM_E_INVALID_ARG;
   return guarded([&] {
-    fail_if(opt->elimination < ARSLAM_ELIM_AUTO || opt->elimination > ARSLAM_ELIM_TAGS, ARSLAM_E_INVALID_ARG,
-            "elimination must be ARSLAM_ELIM_AUTO, _CAPTURES or _TAGS");
+    fail_if(opt->elimination < ARSLAM_ELIM_AUTO || opt->elimination > ARSLAM_ELIM_MIXED, ARSLAM_E_INVALID_ARG,
+            "elimination must be ARSLAM_ELIM_AUTO, _CAPTURES, _TAGS or _MIXED");
     fail_if(opt->factor_executor != 0 && opt->factor_executor != 1, ARSLAM_E_INVALID_ARG,
             "factor_executor must be 0 or 1");
     fail_if(opt->max_num_iterations < 0 || opt->max_num_iterations > ARSLAM_LM_MAX_ITERS,

@@ -48,6 +48,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
+           "arslam_debug_mixed_groups",
            "arslam_debug_dag_simulate", "arslam_debug_dag_fault_detail", "arslam_debug_box_fingerprint",
            "arslam_debug_rank_split", "arslam_debug_gather_extend",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
@@ -64,7 +65,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
 _dp = C.POINTER(C.c_double)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int)
 SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = 0, 1, 2
-ELIM_AUTO, ELIM_CAPTURES, ELIM_TAGS = 0, 1, 2   # arslam_lm_options.elimination
+ELIM_AUTO, ELIM_CAPTURES, ELIM_TAGS, ELIM_MIXED = 0, 1, 2, 3   # arslam_lm_options.elimination
 SETUP_LOAD, SETUP_VALUES, SETUP_APPEND = 0, 1, 2   # arslam_lm_summary.setup_kind
 _ip = C.POINTER(C.c_int)
 _up = C.POINTER(C.c_ubyte)
@@ -222,6 +223,7 @@ def lib():
     L.arslam_debug_dense_llt.argtypes = [C.c_long, _dp, _dp, _dp, C.POINTER(C.c_int)]
     L.arslam_debug_angle_axis_rotate.argtypes = [C.c_int, _dp, _dp, _dp, _ip]
     L.arslam_debug_ceres_e_blocks.argtypes = [C.POINTER(SoaProblem), _ip]
+    L.arslam_debug_mixed_groups.argtypes = [C.POINTER(SoaProblem), _ip, C.POINTER(C.c_ubyte), C.POINTER(C.c_ubyte)]
     L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
     L.arslam_lm_set_iteration_callback.argtypes = [C.c_void_p, ITER_CB, C.c_void_p]
     L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
@@ -592,6 +594,23 @@ def debug_ceres_e_blocks(camera, cap, tag, obs_cap, obs_tag, corners=None, camer
     out = np.zeros(4, np.int32)
     _check(lib().arslam_debug_ceres_e_blocks(C.byref(A.s), out.ctypes.data_as(_ip)))
     return dict(captures=int(out[0]), tags=int(out[1]), camera=int(out[2]), max_tag_obs=int(out[3]))
+
+
+def debug_mixed_groups(camera, cap, tag, obs_cap, obs_tag, corners=None, camera_const=False, cap_const=None,
+                       tag_const=None):
+    """Host-only: Ceres' e-block set (e_cap, e_tag: 0/1 per capture / tag) and the ELIM_MIXED
+    device problem's {groups, f_blocks, direct, max_blk}."""
+    if corners is None:
+        corners = np.zeros((len(obs_cap), 8))
+    A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const, cap_const, tag_const)
+    out = np.zeros(4, np.int32)
+    e_cap = np.zeros(max(A.cap.shape[0], 1), np.uint8)
+    e_tag = np.zeros(max(A.tag.shape[0], 1), np.uint8)
+    _check(lib().arslam_debug_mixed_groups(C.byref(A.s), out.ctypes.data_as(_ip),
+                                           e_cap.ctypes.data_as(C.POINTER(C.c_ubyte)),
+                                           e_tag.ctypes.data_as(C.POINTER(C.c_ubyte))))
+    return dict(groups=int(out[0]), f_blocks=int(out[1]), direct=int(out[2]), max_blk=int(out[3]),
+                e_cap=e_cap[:A.cap.shape[0]], e_tag=e_tag[:A.tag.shape[0]])
 
 
 # ---- batched localize (include/arslam_localize.h) ----

@@ -373,3 +373,16 @@ def config_graph(name, **kw):
 def rms_px(cost, n_obs):
     """Reprojection RMS per corner, sqrt(2 cost / (4 N_obs))."""
     return float(np.sqrt(2.0 * cost / (4.0 * n_obs))) if n_obs else 0.0
+
+
+def prefix_graph(g, k):
+    """The first k captures of g and the tags they see (renumbered in first-seen index order):
+    the problem ArSlamSolver::solveIncremental solves after its k-th capture
+    (ar_slam_util.cpp:629-742, one Solve of the whole problem so far)."""
+    sel = g.obs_cap < k
+    tags, inv = np.unique(g.obs_tag[sel], return_inverse=True)
+    return Graph(camera=g.camera.copy(), cap=g.cap[:k].copy(), tag=g.tag[tags].copy(),
+                 obs_cap=g.obs_cap[sel].astype(np.int32), obs_tag=inv.astype(np.int32),
+                 corners=g.corners[sel], camera_true=g.camera_true, cap_true=g.cap_true[:k],
+                 tag_true=g.tag_true[tags], name=f"{g.name}[:{k}]")
+

@@ -55,9 +55,13 @@ enum {
  * the stable greedy independent set of the Hessian graph in ascending degree,
  * blocks in program order): the side that holds the majority of that set is
  * eliminated (Ceres may mix the two sides; the step is the same exact solve of
- * the same system, only the rounding differs).  Multi-rank solves always
- * eliminate captures (the shards are capture ranges). */
-enum { ARSLAM_ELIM_AUTO = 0, ARSLAM_ELIM_CAPTURES = 1, ARSLAM_ELIM_TAGS = 2 };
+ * the same system, only the rounding differs).  MIXED eliminates exactly
+ * Ceres' set -- captures and tags together when it mixes them (residuals
+ * joining two reduced-side blocks then go straight into the reduced system, as
+ * in Ceres' SchurEliminator); summary.elimination_used then reports MIXED, or
+ * the side when the set is one whole side.  Multi-rank solves always
+ * eliminate captures (the shards are capture ranges); MIXED is single-rank. */
+enum { ARSLAM_ELIM_AUTO = 0, ARSLAM_ELIM_CAPTURES = 1, ARSLAM_ELIM_TAGS = 2, ARSLAM_ELIM_MIXED = 3 };
 
 /* Ceres termination types (ceres::TerminationType) */
 enum { ARSLAM_CONVERGENCE = 0, ARSLAM_NO_CONVERGENCE = 1, ARSLAM_FAILURE = 2, ARSLAM_USER_SUCCESS = 3,
@@ -143,7 +147,7 @@ typedef struct {
   double factor_scalar_flops;   /* flops of the scalar Cholesky of the real rows (the algorithmic count:
                                    no padding rows, no zeros inside fill tiles) per factorization */
   double comm_bytes;            /* multi-rank: bytes this rank all-reduced during the solve */
-  int elimination_used;         /* ARSLAM_ELIM_CAPTURES or ARSLAM_ELIM_TAGS */
+  int elimination_used;         /* ARSLAM_ELIM_CAPTURES, _TAGS or _MIXED (Ceres' set, both kinds) */
   int ceres_e_captures;         /* Ceres 2.0's e-block set for this problem (ComputeStableSchurOrdering): */
   int ceres_e_tags;             /*   captures and tags in it (the camera joins it only in degenerate graphs) */
   /* several ranks (subtree-to-rank split of the reduced system's elimination tree) */

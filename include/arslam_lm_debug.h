@@ -93,6 +93,12 @@ int arslam_lm_debug_tag_pair_tile(arslam_lm *h, const double *tag_a, const doubl
  * camera (0/1) in the set, most observations of one tag}. */
 int arslam_debug_ceres_e_blocks(const arslam_soa_problem *p, int out[4]);
 
+/* Host only: the set itself (e_cap[n_cap], e_tag[n_tag]: 1 = eliminated) and the
+ * ARSLAM_ELIM_MIXED device problem built from it: out = {groups (eliminated
+ * captures + eliminated tags + direct groups), reduced-side blocks, direct
+ * groups, most local blocks of one group}. */
+int arslam_debug_mixed_groups(const arslam_soa_problem *p, int out[4], unsigned char *e_cap, unsigned char *e_tag);
+
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);
 

@@ -53,6 +53,8 @@ void or_default_options(or_options *o) {
   o->num_threads = 1;
   o->progress = 0;
   o->debug_indefinite_mask = 0;
+  o->e_cap = NULL;
+  o->e_tag = NULL;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -332,6 +334,11 @@ typedef struct {
   double *delta;
   int nthreads;
   int dbg_indefinite;   /* test hook for this linear solve (or_options.debug_indefinite_mask) */
+  /* OR_ELIM_MIXED: the e-set, the reduced index of each slot (-1: an e-block's
+   * slot), and the observations by tag */
+  const unsigned char *e_cap, *e_tag;
+  long *fidx;
+  int *tag_start, *tag_obs;
 } lm_t;
 
 static inline long slot_cam(void) { return 0; }
@@ -615,6 +622,180 @@ static int solve_schur(lm_t *L, const double *D2) {
   return 0;
 }
 
+/* DENSE_SCHUR over an arbitrary independent e-block set (OR_ELIM_MIXED): the
+ * set Ceres 2.0 itself takes with no linear_solver_ordering ([P:1011];
+ * ReorderProgramForSchurTypeLinearSolver -> ComputeStableSchurOrdering [C]),
+ * which mixes captures and tags.  Each e-block (an eliminated capture or tag)
+ * is eliminated from its own residuals exactly as in solve_schur, with the
+ * other pose block of each residual on the reduced side; residuals touching
+ * no e-block add their normal-equation blocks to the reduced system directly
+ * (SchurEliminator's rows without an e-block [C schur_eliminator_impl.h
+ * NoEBlockRowsUpdate]).  Reduced rows: every non-e capture and tag (L->fidx),
+ * the camera last.  Returns 0 ok, 1 on Cholesky failure; writes L->y. */
+static int solve_schur_mixed(lm_t *L, const double *D2) {
+  const long nF = L->nF, ld = nF;
+  memset(L->S, 0, (size_t)nF * nF * sizeof(double));
+  memset(L->rhs, 0, nF * sizeof(double));
+  int maxk = 0;
+  for (int c = 0; c < L->nc; ++c)
+    if (L->e_cap[c] && L->cap_start[c + 1] - L->cap_start[c] > maxk) maxk = L->cap_start[c + 1] - L->cap_start[c];
+  for (int t = 0; t < L->nt; ++t)
+    if (L->e_tag[t] && L->tag_start[t + 1] - L->tag_start[t] > maxk) maxk = L->tag_start[t + 1] - L->tag_start[t];
+  const int mmax = 3 + 6 * maxk;
+  double *W = malloc(sizeof(double) * 6 * mmax);
+  double *FtF = malloc(sizeof(double) * mmax * mmax);
+  double *Ftr = malloc(sizeof(double) * mmax);
+  double *Z = malloc(sizeof(double) * 6 * mmax);
+  long *gidx = malloc(sizeof(long) * mmax);
+  int *lblk = malloc(sizeof(int) * (maxk + 1));
+  long *bslot = malloc(sizeof(long) * (maxk + 1));
+  const int n_eb = L->nc + L->nt;
+  /* e-block eb < nc: capture eb; else tag eb - nc.  eoff / foff: its own and
+   * the other pose's columns in the 15-column Jacobian row */
+  for (int eb = 0; eb < n_eb; ++eb) {
+    const int is_cap = eb < L->nc, id = is_cap ? eb : eb - L->nc;
+    if (is_cap ? !L->e_cap[id] : !L->e_tag[id]) continue;
+    const int *olist = is_cap ? L->cap_obs + L->cap_start[id] : L->tag_obs + L->tag_start[id];
+    const int k = is_cap ? L->cap_start[id + 1] - L->cap_start[id] : L->tag_start[id + 1] - L->tag_start[id];
+    const long se = is_cap ? slot_cap(L, id) : slot_tag(L, id);
+    const int eoff = is_cap ? 3 : 9, foff = is_cap ? 9 : 3;
+    if (k == 0) continue;
+    int nblk = 1;
+    for (int q = 0; q < k; ++q) {
+      const int o = olist[q];
+      const long sf = is_cap ? slot_tag(L, L->p->obs_tag[o]) : slot_cap(L, L->p->obs_cap[o]);
+      int b = -1;
+      for (int u = 1; u < nblk; ++u)
+        if (bslot[u] == sf) { b = u; break; }
+      if (b < 0) { b = nblk++; bslot[b] = sf; }
+      lblk[q] = b;
+    }
+    const int m = 3 + 6 * (nblk - 1);
+    for (int j = 0; j < 3; ++j) gidx[j] = L->fidx[slot_cam() + j];
+    for (int u = 1; u < nblk; ++u)
+      for (int j = 0; j < 6; ++j) gidx[3 + 6 * (u - 1) + j] = L->fidx[bslot[u] + j];
+    double U[36] = {0}, Etr[6] = {0};
+    memset(W, 0, sizeof(double) * 6 * m);
+    memset(FtF, 0, sizeof(double) * m * m);
+    memset(Ftr, 0, sizeof(double) * m);
+    for (int q = 0; q < k; ++q) {
+      const int o = olist[q];
+      const double *r = L->r + 8L * o;
+      const int fo = 3 + 6 * (lblk[q] - 1);
+      for (int i = 0; i < 8; ++i) {
+        double row[15];
+        scaled_row(L, o, i, row);
+        const double *E = row + eoff;
+        double Fv[9];
+        long fl[9];
+        for (int j = 0; j < 3; ++j) { Fv[j] = row[j]; fl[j] = j; }
+        for (int j = 0; j < 6; ++j) { Fv[3 + j] = row[foff + j]; fl[3 + j] = fo + j; }
+        for (int a = 0; a < 6; ++a) {
+          Etr[a] += E[a] * r[i];
+          for (int b = 0; b < 6; ++b) U[6 * a + b] += E[a] * E[b];
+          for (int j = 0; j < 9; ++j) W[a * m + fl[j]] += E[a] * Fv[j];
+        }
+        for (int j = 0; j < 9; ++j) {
+          Ftr[fl[j]] += Fv[j] * r[i];
+          for (int jj = 0; jj < 9; ++jj) FtF[fl[j] * m + fl[jj]] += Fv[j] * Fv[jj];
+        }
+      }
+    }
+    for (int a = 0; a < 6; ++a) U[6 * a + a] += D2[se + a];
+    double Ui[36];
+    inv6(U, Ui);
+    for (int a = 0; a < 6; ++a)
+      for (int j = 0; j < m; ++j) {
+        double s = 0.0;
+        for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * W[b * m + j];
+        Z[a * m + j] = s;
+      }
+    double UiE[6];
+    for (int a = 0; a < 6; ++a) {
+      double s = 0.0;
+      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * Etr[b];
+      UiE[a] = s;
+    }
+    for (int i = 0; i < m; ++i) {
+      double s = 0.0;
+      for (int a = 0; a < 6; ++a) s += W[a * m + i] * UiE[a];
+      L->rhs[gidx[i]] += Ftr[i] - s;
+      for (int j = 0; j < m; ++j) {
+        const long gi = gidx[i], gj = gidx[j];
+        if (gj > gi) continue;
+        double t = 0.0;
+        for (int a = 0; a < 6; ++a) t += W[a * m + i] * Z[a * m + j];
+        L->S[gi * ld + gj] += FtF[i * m + j] - t;
+      }
+    }
+  }
+  /* residuals with no e-block: their J'J and J'r straight into the reduced system */
+  for (int o = 0; o < L->nb; ++o) {
+    if (L->e_cap[L->p->obs_cap[o]] || L->e_tag[L->p->obs_tag[o]]) continue;
+    const long base[3] = {slot_cam(), slot_cap(L, L->p->obs_cap[o]), slot_tag(L, L->p->obs_tag[o])};
+    long gi[15];
+    for (int j = 0; j < 3; ++j) gi[j] = L->fidx[base[0] + j];
+    for (int j = 0; j < 6; ++j) { gi[3 + j] = L->fidx[base[1] + j]; gi[9 + j] = L->fidx[base[2] + j]; }
+    for (int i = 0; i < 8; ++i) {
+      double row[15];
+      scaled_row(L, o, i, row);
+      for (int a = 0; a < 15; ++a) {
+        L->rhs[gi[a]] += row[a] * L->r[8L * o + i];
+        for (int b = 0; b < 15; ++b)
+          if (gi[b] <= gi[a]) L->S[gi[a] * ld + gi[b]] += row[a] * row[b];
+      }
+    }
+  }
+  free(W); free(FtF); free(Ftr); free(Z); free(gidx); free(lblk); free(bslot);
+  for (long sl = 0; sl < L->n; ++sl)
+    if (L->fidx[sl] >= 0) L->S[L->fidx[sl] * (ld + 1)] += D2[sl];
+  if (L->dbg_indefinite) L->S[L->fidx[slot_cam()] * (ld + 1)] = -1.0;   /* test hook */
+  if (or_llt_lower(L->S, nF, ld, L->nthreads) != 0) return 1;
+  double *yF = malloc(sizeof(double) * nF);
+  memcpy(yF, L->rhs, nF * sizeof(double));
+  llt_solve(L->S, nF, ld, yF);
+  for (long sl = 0; sl < L->n; ++sl)
+    if (L->fidx[sl] >= 0) L->y[sl] = yF[L->fidx[sl]];
+  /* back substitution per e-block: y_e = (E'E + D^2)^{-1} E'(r - F y_F) */
+  for (int eb = 0; eb < n_eb; ++eb) {
+    const int is_cap = eb < L->nc, id = is_cap ? eb : eb - L->nc;
+    if (is_cap ? !L->e_cap[id] : !L->e_tag[id]) continue;
+    const int *olist = is_cap ? L->cap_obs + L->cap_start[id] : L->tag_obs + L->tag_start[id];
+    const int k = is_cap ? L->cap_start[id + 1] - L->cap_start[id] : L->tag_start[id + 1] - L->tag_start[id];
+    const long se = is_cap ? slot_cap(L, id) : slot_tag(L, id);
+    const int eoff = is_cap ? 3 : 9, foff = is_cap ? 9 : 3;
+    if (k == 0) { for (int a = 0; a < 6; ++a) L->y[se + a] = 0.0; continue; }
+    double U[36] = {0}, v[6] = {0};
+    for (int q = 0; q < k; ++q) {
+      const int o = olist[q];
+      const double *r = L->r + 8L * o;
+      const long sf = is_cap ? slot_tag(L, L->p->obs_tag[o]) : slot_cap(L, L->p->obs_cap[o]);
+      for (int i = 0; i < 8; ++i) {
+        double row[15];
+        scaled_row(L, o, i, row);
+        double fz = 0.0;
+        for (int j = 0; j < 3; ++j) fz += row[j] * L->y[slot_cam() + j];
+        for (int j = 0; j < 6; ++j) fz += row[foff + j] * L->y[sf + j];
+        const double sj = r[i] - fz;
+        for (int a = 0; a < 6; ++a) {
+          v[a] += row[eoff + a] * sj;
+          for (int b = 0; b < 6; ++b) U[6 * a + b] += row[eoff + a] * row[eoff + b];
+        }
+      }
+    }
+    for (int a = 0; a < 6; ++a) U[6 * a + a] += D2[se + a];
+    double Ui[36];
+    inv6(U, Ui);
+    for (int a = 0; a < 6; ++a) {
+      double s = 0.0;
+      for (int b = 0; b < 6; ++b) s += Ui[6 * a + b] * v[b];
+      L->y[se + a] = s;
+    }
+  }
+  free(yF);
+  return 0;
+}
+
 /* DENSE_QR-free reference: full normal equations over every slot. */
 static int solve_full(lm_t *L, const double *D2) {
   const long n = L->n;
@@ -666,6 +847,32 @@ int or_solve(or_problem *p, const or_options *o, or_summary *s, const or_comm *c
   L.nc = p->n_cap; L.nt = p->n_tag; L.nb = p->n_obs;
   L.n = 3 + 6L * L.nc + 6L * L.nt;
   L.nF = 6L * L.nt + 3;
+  const int mixed = o->elimination == OR_ELIM_MIXED;
+  if (mixed) {
+    if (comm || !o->e_cap || !o->e_tag) return -1;   /* single process, both sets given */
+    L.e_cap = o->e_cap;
+    L.e_tag = o->e_tag;
+    for (int b = 0; b < L.nb; ++b)
+      if (L.e_cap[p->obs_cap[b]] && L.e_tag[p->obs_tag[b]]) return -1;   /* not an independent set */
+    /* reduced rows: the non-e captures, then the non-e tags, then the camera */
+    L.fidx = malloc(sizeof(long) * L.n);
+    long f = 0;
+    for (int c = 0; c < L.nc; ++c)
+      for (int j = 0; j < 6; ++j) L.fidx[3 + 6L * c + j] = L.e_cap[c] ? -1 : f++;
+    for (int t = 0; t < L.nt; ++t)
+      for (int j = 0; j < 6; ++j) L.fidx[3 + 6L * L.nc + 6L * t + j] = L.e_tag[t] ? -1 : f++;
+    for (int j = 0; j < 3; ++j) L.fidx[j] = f++;
+    L.nF = f;
+    /* observations by tag (stable) */
+    L.tag_start = calloc(L.nt + 1, sizeof(int));
+    L.tag_obs = malloc(sizeof(int) * (L.nb > 0 ? L.nb : 1));
+    for (int b = 0; b < L.nb; ++b) L.tag_start[p->obs_tag[b] + 1]++;
+    for (int t = 0; t < L.nt; ++t) L.tag_start[t + 1] += L.tag_start[t];
+    int *fill = malloc(sizeof(int) * (L.nt + 1));
+    memcpy(fill, L.tag_start, sizeof(int) * (L.nt + 1));
+    for (int b = 0; b < L.nb; ++b) L.tag_obs[fill[p->obs_tag[b]]++] = b;
+    free(fill);
+  }
 
   /* CSR by capture (stable) */
   L.cap_start = calloc(L.nc + 1, sizeof(int));
@@ -809,7 +1016,8 @@ int or_solve(or_problem *p, const or_options *o, or_summary *s, const or_comm *c
     }
     s->num_linear_solves++;
     L.dbg_indefinite = (int)((o->debug_indefinite_mask >> (s->num_linear_solves - 1 < 63 ? s->num_linear_solves - 1 : 63)) & 1ull);
-    int lin_fail = (o->elimination == OR_ELIM_NONE) ? solve_full(&L, D2) : solve_schur(&L, D2);
+    int lin_fail = (o->elimination == OR_ELIM_NONE) ? solve_full(&L, D2)
+                   : mixed ? solve_schur_mixed(&L, D2) : solve_schur(&L, D2);
     reuse_diag = 1;
     double model_cost_change = 0.0;
     int valid = 0;
@@ -932,6 +1140,7 @@ done:
   free(L.cap_start); free(L.cap_obs); free(L.free_); free(L.obs_active);
   free(L.x); free(L.xc); free(L.g); free(L.colnorm); free(L.scale); free(L.diag);
   free(L.y); free(L.delta); free(D2); free(L.r); free(L.J); free(L.S); free(L.rhs);
+  free(L.fidx); free(L.tag_start); free(L.tag_obs);
   return s->termination;
 }
 

@@ -43,7 +43,11 @@ typedef struct {
   const unsigned char *tag_const; /* [n_tag] or NULL                     */
 } or_problem;
 
-enum { OR_ELIM_CAPTURES = 0, OR_ELIM_NONE = 1 };
+/* OR_ELIM_MIXED: the e-blocks are exactly the captures with e_cap[c] != 0 and
+ * the tags with e_tag[t] != 0 (an independent set: no residual joins two of
+ * them) -- Ceres' own ComputeStableSchurOrdering set, which mixes the two
+ * kinds (ar_slam_util.cpp:1011 sets no ordering).  Single process only. */
+enum { OR_ELIM_CAPTURES = 0, OR_ELIM_NONE = 1, OR_ELIM_MIXED = 2 };
 
 typedef struct {
   int max_num_iterations;              /* 50 (ar_slam_util.cpp:1004) */
@@ -58,7 +62,7 @@ typedef struct {
   double max_lm_diagonal;              /* 1e32  */
   int max_num_consecutive_invalid_steps; /* 5 */
   int jacobi_scaling;                  /* 1 */
-  int elimination;                     /* OR_ELIM_CAPTURES | OR_ELIM_NONE */
+  int elimination;                     /* OR_ELIM_CAPTURES | OR_ELIM_NONE | OR_ELIM_MIXED */
   int num_threads;                     /* OpenMP threads for the dense LLT (1 = reference) */
   int progress;                        /* print the Ceres progress table */
   /* test hook (not a Ceres option): at linear solve i (0-based) with bit
@@ -66,6 +70,8 @@ typedef struct {
    * after D_f^2 is added, so its LLT fails and the step is invalid -- the
    * same hook as the device's arslam_lm_debug_force_indefinite. */
   unsigned long long debug_indefinite_mask;
+  const unsigned char *e_cap;          /* OR_ELIM_MIXED: [n_cap] eliminated captures */
+  const unsigned char *e_tag;          /* OR_ELIM_MIXED: [n_tag] eliminated tags */
 } or_options;
 
 typedef struct {

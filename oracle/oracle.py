@@ -16,6 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 MAX_ITERS = 1024
+ELIM_CAPTURES, ELIM_NONE, ELIM_MIXED = 0, 1, 2   # or_options.elimination
 TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE"}
 RULES = {0: "none", 1: "gradient_tolerance", 2: "parameter_tolerance", 3: "function_tolerance",
          4: "min_trust_region_radius", 5: "max_num_iterations", 6: "invalid_steps",
@@ -45,7 +46,8 @@ class Options(C.Structure):
                 ("max_num_consecutive_invalid_steps", C.c_int),
                 ("jacobi_scaling", C.c_int), ("elimination", C.c_int),
                 ("num_threads", C.c_int), ("progress", C.c_int),
-                ("debug_indefinite_mask", C.c_ulonglong)]
+                ("debug_indefinite_mask", C.c_ulonglong),
+                ("e_cap", _up), ("e_tag", _up)]
 
 
 class Iter(C.Structure):
@@ -177,7 +179,11 @@ def solve(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, cap_c
           tag_const=None, comm=None, **opts):
     """Run the oracle LM; returns (camera, cap, tag, summary_dict)."""
     A = _Arrays(camera, cap, tag, obs_cap, obs_tag, corners, camera_const, cap_const, tag_const)
+    # (elimination=ELIM_MIXED: e_cap / e_tag are the eliminated captures and tags, kept alive here)
+    keep = {k: np.ascontiguousarray(opts.pop(k), np.uint8) for k in ("e_cap", "e_tag") if k in opts}
     o = default_options(**opts)
+    for k, v in keep.items():
+        setattr(o, k, _p(v, _up))
     s = Summary()
     lib().or_solve(C.byref(A.prob), C.byref(o), C.byref(s), None if comm is None else C.byref(comm))
     return A.camera, A.cap, A.tag, summary_dict(s)

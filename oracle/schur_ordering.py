@@ -19,8 +19,10 @@ algorithm, so the e-block choice is parity-unpinned against Ceres.
 """
 
 
-def ceres_e_blocks(obs_cap, obs_tag, n_cap, n_tag, camera_const=False, cap_const=None, tag_const=None):
-    """Returns {captures, tags, camera, max_tag_obs} of Ceres' independent set."""
+def ceres_e_blocks(obs_cap, obs_tag, n_cap, n_tag, camera_const=False, cap_const=None, tag_const=None,
+                   members=False):
+    """Returns {captures, tags, camera, max_tag_obs} of Ceres' independent set (members: also
+    e_cap / e_tag, a 0/1 flag per capture and per tag, and e_cam)."""
     cap_free = [not (cap_const is not None and cap_const[c]) for c in range(n_cap)]
     tag_free = [not (tag_const is not None and tag_const[t]) for t in range(n_tag)]
     cam_free = not camera_const
@@ -57,6 +59,14 @@ def ceres_e_blocks(obs_cap, obs_tag, n_cap, n_tag, camera_const=False, cap_const
         for u in adj[v]:
             if color[u] == 0:
                 color[u] = 1
+    if members:
+        e_cap, e_tag = [0] * n_cap, [0] * n_tag
+        for v in taken:
+            if v[0] == "c":
+                e_cap[v[1]] = 1
+            elif v[0] == "t":
+                e_tag[v[1]] = 1
+        return dict(e_cap=e_cap, e_tag=e_tag, e_cam=int(("f",) in taken))
     return dict(captures=sum(1 for v in taken if v[0] == "c"),
                 tags=sum(1 for v in taken if v[0] == "t"),
                 camera=sum(1 for v in taken if v[0] == "f"),

@@ -78,3 +78,54 @@ def test_auto_side_by_config():
 def test_invalid_problem_rejected(L):
     with pytest.raises(L.LMError):
         L.debug_ceres_e_blocks([900.0, 0, 0], np.zeros((1, 6)), np.zeros((1, 6)), [1], [0])
+
+
+def _mixed_expected(g):
+    m = ceres_e_blocks(g.obs_cap, g.obs_tag, g.n_cap, g.n_tag, members=True)
+    ec, et = np.array(m["e_cap"], np.uint8), np.array(m["e_tag"], np.uint8)
+    direct = len({int(c) for c, t in zip(g.obs_cap, g.obs_tag) if not ec[c] and not et[t]})
+    return ec, et, direct
+
+
+@pytest.mark.parametrize("name", ["cfg1", "small", "medium", "wide", "cfg2", "cfg2[:300]"])
+def test_mixed_device_problem(L, name):
+    """ELIM_MIXED regroups the residuals by Ceres' exact set: one group per eliminated capture
+    and tag, one direct group per reduced-side capture with residuals joining two reduced-side
+    poses; every other capture and tag is a reduced-side block."""
+    g = synth.config_graph(name.split("[")[0])
+    if "[:" in name:
+        g = synth.prefix_graph(g, int(name.split("[:")[1][:-1]))
+    r = L.debug_mixed_groups(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag)
+    ec, et, direct = _mixed_expected(g)
+    assert (r["e_cap"] == ec).all() and (r["e_tag"] == et).all()
+    assert r["groups"] == ec.sum() + et.sum() + direct
+    assert r["direct"] == direct
+    assert r["f_blocks"] == g.n_cap + g.n_tag - ec.sum() - et.sum()
+
+
+def test_incremental_prefixes_mix(L):
+    """The reference's incremental flow on cfg2 solves mixed sets for most of its captures
+    (captures and tags both eliminated from ~220 captures on)."""
+    g = synth.config_graph("cfg2")
+    kinds = []
+    for k in (100, 300, 600, 1000):
+        m = ceres_e_blocks(*(lambda h: (h.obs_cap, h.obs_tag, h.n_cap, h.n_tag))(synth.prefix_graph(g, k)))
+        kinds.append((m["captures"] > 0, m["tags"] > 0))
+    assert kinds == [(False, True), (True, True), (True, True), (True, True)]
+
+
+@pytest.mark.parametrize("name", ["small", "medium", "wide"])
+def test_oracle_mixed_set_matches_capture_elimination(name):
+    """The oracle's DENSE_SCHUR over Ceres' mixed set (OR_ELIM_MIXED) is the same LM run as
+    over the captures: the same exact step, rounding apart."""
+    from oracle import oracle as O
+    O.build()
+    g = synth.config_graph(name)
+    ec, et, _ = _mixed_expected(g)
+    assert ec.sum() > 0 and et.sum() > 0
+    a = O.solve_graph(g)[3]
+    b = O.solve_graph(g, elimination=O.ELIM_MIXED, e_cap=ec, e_tag=et)[3]
+    assert (a["termination"], a["rule"], len(a["iterations"])) == (b["termination"], b["rule"], len(b["iterations"]))
+    for x, y in zip(a["iterations"], b["iterations"]):
+        assert abs(x["cost"] - y["cost"]) <= 1e-11 * x["cost"]
+

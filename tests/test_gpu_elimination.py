@@ -1,4 +1,5 @@
-"""GPU parity of the two elimination sides (arslam_lm_options.elimination).
+"""GPU parity of the elimination sides and of Ceres' exact mixed set
+(arslam_lm_options.elimination).
 
 DENSE_SCHUR eliminates Ceres' own e-block set (ar_slam_util.cpp:1011; Ceres
 2.0 ComputeStableSchurOrdering): mostly tags on the demo-sized cfg1 graph and
@@ -9,7 +10,9 @@ problem (captures become the reduced system).  Either side is the same exact
 solve of the same LM system, so both must reproduce the oracle's trace
 (capture elimination) to rounding: per-iteration cost 1e-9, final cost and
 focal 1e-8, same termination, every gauge-aligned capture and tag pose
-1e-6 m / 1e-7 rad (tests/gauge.py).
+1e-6 m / 1e-7 rad (tests/gauge.py).  ELIM_MIXED eliminates exactly
+Ceres' set, captures and tags together, and is checked against the
+oracle eliminating the same set (OR_ELIM_MIXED) at the same tolerances.
 """
 import json
 import os
@@ -102,6 +105,81 @@ def test_pointer_api_under_tag_elimination(lm):
     assert abs(s1["final_cost"] - s2["final_cost"]) <= 1e-9 * s1["final_cost"]
     np.testing.assert_allclose(c1, c2, rtol=1e-8)
     np.testing.assert_allclose(k1[:, :3] - k1[:, :3].mean(0), k2[:, :3] - k2[:, :3].mean(0), atol=1e-6)
+
+
+def _graph(name):
+    g = synth.config_graph(name.split("[")[0])
+    return synth.prefix_graph(g, int(name.split("[:")[1][:-1])) if "[:" in name else g
+
+
+def _ceres_set(g, **kw):
+    m = ceres_e_blocks(g.obs_cap, g.obs_tag, g.n_cap, g.n_tag, members=True, **kw)
+    return np.array(m["e_cap"], np.uint8), np.array(m["e_tag"], np.uint8)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "small", "medium", "wide", "cfg2[:300]"])
+def test_mixed_set_matches_oracle(lm, oracle, name):
+    """ELIM_MIXED eliminates exactly Ceres' set (captures and tags together; cfg1's is all
+    tags, the others mix), against the oracle eliminating the same set: the same trace at
+    the tolerances above, every gauge-aligned pose."""
+    g = _graph(name)
+    ec, et = _ceres_set(g)
+    ours = lm.solve_graph(g, elimination=lm.ELIM_MIXED)
+    if ec.sum() and et.sum():
+        ref = oracle.solve_graph(g, elimination=oracle.ELIM_MIXED, e_cap=ec, e_tag=et)
+        used = lm.ELIM_MIXED
+    else:
+        ref = oracle.solve_graph(g)
+        used = lm.ELIM_TAGS if et.sum() else lm.ELIM_CAPTURES
+    _compare(g, ours, ref)
+    s = ours[3]
+    assert s["elimination_used"] == used
+    assert (s["ceres_e_captures"], s["ceres_e_tags"]) == (int(ec.sum()), int(et.sum()))
+    # the reduced system: every capture and tag outside the set, and the camera
+    n_f = g.n_cap + len(np.unique(g.obs_tag)) - int(ec.sum()) - int(et.sum())
+    assert s["n_reduced"] >= 6 * n_f + 3
+
+
+def test_mixed_set_with_constant_blocks(lm, oracle):
+    """Constant captures and tags are not in Ceres' graph: the mixed set of what is left,
+    constant blocks on the reduced side (no rows), against the oracle."""
+    g = synth.config_graph("medium")
+    rng = np.random.default_rng(11)
+    cap_const = (rng.random(g.n_cap) < 0.1).astype(np.uint8)
+    tag_const = (rng.random(g.n_tag) < 0.1).astype(np.uint8)
+    kw = dict(cap_const=cap_const, tag_const=tag_const)
+    ec, et = _ceres_set(g, **kw)
+    assert ec.sum() and et.sum()
+    ours = lm.solve_graph(g, elimination=lm.ELIM_MIXED, **kw)
+    ref = oracle.solve_graph(g, elimination=oracle.ELIM_MIXED, e_cap=ec, e_tag=et, **kw)
+    _compare(g, ours, ref)
+    assert ours[3]["elimination_used"] == lm.ELIM_MIXED
+    np.testing.assert_array_equal(ours[1][cap_const == 1], g.cap[cap_const == 1])
+    np.testing.assert_array_equal(ours[2][tag_const == 1], g.tag[tag_const == 1])
+
+
+def test_pointer_api_under_mixed_elimination(lm):
+    """Caller-owned blocks are written back through the regrouping (eliminated captures and
+    tags, the reduced side's captures and tags); a re-solve reloads values only and ends
+    where a capture-eliminating solve ends."""
+    g = synth.config_graph("small")
+    outs = []
+    for elim in (lm.ELIM_CAPTURES, lm.ELIM_MIXED):
+        camera = g.camera.copy()
+        caps = [g.cap[c].copy() for c in range(g.n_cap)]
+        tags = [g.tag[t].copy() for t in range(g.n_tag)]
+        prob = lm.Problem(elimination=elim)
+        for b in range(g.n_obs):
+            prob.add_residual_block(g.corners[b], camera, caps[g.obs_cap[b]], tags[g.obs_tag[b]])
+        s = prob.solve()
+        assert s["elimination_used"] == elim
+        s2 = prob.solve()
+        assert s2["setup_kind"] == lm.SETUP_VALUES
+        outs.append((camera, np.stack(caps), np.stack(tags), s))
+    (c1, k1, t1, s1), (c2, k2, t2, s2) = outs
+    assert abs(s1["final_cost"] - s2["final_cost"]) <= 1e-9 * s1["final_cost"]
+    np.testing.assert_allclose(c1, c2, rtol=1e-8)
+    assert_poses_match(k2, t2, k1, t1, tags=np.arange(g.n_tag), caps=np.arange(g.n_cap))
 
 
 def test_invalid_elimination_rejected(lm):
