@@ -9,6 +9,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from ar_slam_amd import build, lm, synth  # noqa: E402
@@ -26,7 +28,9 @@ for c in range(2):
     w.solve_incremental()
 del w
 # (default options, as a drop-in user gets them; ARSLAM_PHASES=1: per-phase device times)
-s = lm.SlamSolver(phase_timing=int(os.environ.get("ARSLAM_PHASES", "0")))
+# (ARSLAM_ELIM: the elimination option, e.g. 3 = Ceres' exact mixed set)
+s = lm.SlamSolver(phase_timing=int(os.environ.get("ARSLAM_PHASES", "0")),
+                  elimination=int(os.environ.get("ARSLAM_ELIM", "0")))
 s.set_camera(g.camera)
 t0 = time.perf_counter()
 t_add = 0.0
@@ -62,6 +66,8 @@ print(json.dumps({"flow": f"solveIncremental, {name}: {g.n_cap} captures / {g.n_
                   "add_detections_ms_per_message": 1e3 * t_add / g.n_cap,
                   "device_phase_ms_per_solve": {k[2:-3]: round(v / n, 4) for k, v in ph.items()},
                   "setup_kinds": {"load": kinds[0], "values": kinds[1], "append": kinds[2]},
+                  "elimination_used": {str(k): int(v) for k, v in zip(*np.unique(
+                      [s.solve_summary(i)["elimination_used"] for i in range(n)], return_counts=True))},
                   "load_setup_phase_ms": {k: round(1e3 * v / max(1, kinds[0]), 4) for k, v in
                                           zip(("structure", "order", "plan", "upload", "rest"), phase)},
                   "final_rms_px": last["final_rms_px"], "final_termination": last["termination"],
