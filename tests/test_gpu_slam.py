@@ -25,9 +25,9 @@ def _detections(g, caps=None):
         yield f"cap{c}", [f"tag_{t}" for t in g.obs_tag[sel]], g.corners[sel]
 
 
-def _run_both(lm, g, driver, camera=None):
+def _run_both(lm, g, driver, camera=None, **opts):
     from oracle.driver import OracleSlam
-    s = lm.SlamSolver()
+    s = lm.SlamSolver(**opts)
     o = OracleSlam()
     if camera is not None:
         s.set_camera(camera)
@@ -80,6 +80,18 @@ def test_incremental_solve_matches_oracle_driver(lm):
     assert s.solve_order()[0] != 0            # begin() of the set, not the lowest index
     _compare(s, o)
     assert s.num_solves == g.n_cap          # every capture got connected and solved once
+
+
+def test_incremental_solve_with_ceres_exact_set(lm):
+    """The same flow with every Solve eliminating Ceres' exact e-block set (ELIM_MIXED): all
+    tags in its first solves, captures and tags together later on -- the same solves and the
+    same final state as the oracle's driver (which eliminates captures)."""
+    g = synth.config_graph("small")
+    s, o = _run_both(lm, g, "solve_incremental", camera=g.camera, elimination=lm.ELIM_MIXED)
+    assert s.solve_order() == o.solve_order
+    _compare(s, o)
+    used = {s.solve_summary(i)["elimination_used"] for i in range(s.num_solves)}
+    assert lm.ELIM_MIXED in used and lm.ELIM_TAGS in used
 
 
 def test_incremental_cfg2_batches_match_oracle_driver(lm):
