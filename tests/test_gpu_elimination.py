@@ -60,20 +60,23 @@ def test_both_sides_match_oracle(lm, oracle, name, side):
     assert s["n_reduced"] >= 6 * n_f + 1
 
 
+@pytest.mark.parametrize("side", ["tags", "mixed"])
 @pytest.mark.parametrize("name", ["tiny_reject", "small_reject", "tiny_failure", "small_parameter"])
-def test_control_traces_under_tag_elimination(lm, name):
-    """Rejected steps, invalid steps -> FAILURE and the parameter rule, with tags eliminated."""
+def test_control_traces_under_tag_elimination(lm, name, side):
+    """Rejected steps, invalid steps -> FAILURE and the parameter rule, with tags eliminated, and
+    with Ceres' exact set (all tags on tiny, captures and tags together on small)."""
     with open(os.path.join(GOLDEN, f"lm_ctl_{name}.json")) as f:
         gold = json.load(f)
     g = synth.config_graph(gold["config"], **gold["graph"])
     opts = dict(gold["options"])
     mask = opts.pop("debug_indefinite_mask", 0)
-    rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners,
-                            elimination=lm.ELIM_TAGS, **opts)
+    elim = lm.ELIM_TAGS if side == "tags" else lm.ELIM_MIXED
+    rp = lm.ResidentProblem(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners, elimination=elim, **opts)
     rp.debug_force_indefinite(mask)
     s = rp.solve()
     its = s["iterations"]
-    assert s["elimination_used"] == lm.ELIM_TAGS
+    ec, et = _ceres_set(g)
+    assert s["elimination_used"] == (lm.ELIM_TAGS if side == "tags" or not ec.sum() else lm.ELIM_MIXED)
     assert (s["termination"], s["rule"]) == (gold["termination"], gold["rule"])
     assert [it["step_is_valid"] for it in its] == gold["step_is_valid"]
     assert [it["step_is_successful"] for it in its] == gold["step_is_successful"]
