@@ -362,6 +362,9 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
 // (seq_done, seq > 0: with hout, the last block to finish also stores seq into
 // hout[kHostSeq] after every block's host words -- the LM loop's host polls that
 // word instead of an event; seq_done: a zeroed device int, left zero again)
+// x[0..n) into the page-locked dst; the last block stores seq into *word (page-locked,
+// after the data; seq_done: a zeroed device int, left zero again)
+void launch_copy_out(const double *src, long n, double *dst, int *seq_done, double *word, double seq, hipStream_t s);
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts,
                          double *out, hipStream_t s, const int *flag = nullptr,
                          double *hout = nullptr, int *seq_done = nullptr, double seq = 0.0);

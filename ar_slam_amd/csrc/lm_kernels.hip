@@ -1686,6 +1686,26 @@ void launch_cost(const DevProblem &P, const double *x, double *parts, hipStream_
   if (P.n_chunk_caps) hipLaunchKernelGGL(k_cost<true>, dim3(P.n_chunk_caps), dim3(kWave), 0, s, P, x, parts);
 }
 
+// The parameter download on one rank: a kernel stores x straight into the
+// page-locked host buffer and the last block to finish stores the sequence
+// number after every block's stores were made visible at system scope (the
+// host polls that word, as in the LM loop) -- no copy engine, no event.
+__global__ __launch_bounds__(256) void k_copy_out(const double *__restrict__ src, long n, double *__restrict__ dst,
+                                                  int *seq_done, double *word, double seq) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(seq_done, 1) == (int)gridDim.x - 1) {
+    atomicExch(seq_done, 0);
+    __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+void launch_copy_out(const double *src, long n, double *dst, int *seq_done, double *word, double seq, hipStream_t s) {
+  const unsigned blocks = (unsigned)std::min<long>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_copy_out, dim3(std::max(blocks, 1u)), dim3(256), 0, s, src, n, dst, seq_done, word, seq);
+}
+
 void launch_reduce_parts(const double *parts, int nc, const double *fparts, int nfparts, double *out,
                          hipStream_t s, const int *flag, double *hout, int *seq_done, double seq) {
   hipLaunchKernelGGL(k_reduce_parts, dim3(NPART + 2), dim3(1024), 0, s, parts, nc, fparts, nfparts, out, flag, hout,

@@ -1175,8 +1175,18 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
 }
 
 void arslam_lm::write_back(const double *d_src) {
-  h_x.alloc(n);   // page-locked: the parameter download is one DMA, no staging
-  HIP_CHECK(hipMemcpyAsync(h_x.p, d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+  h_x.alloc(n + 1);   // page-locked; [n]: the download's sequence word (one rank)
+  static const bool dma = std::getenv("ARSLAM_WRITE_BACK_DMA") != nullptr;   // debug A/B: the copy engine
+  if (nranks == 1 && !dma) {
+    // a kernel stores x into h_x and then the sequence word the host polls
+    // (the copy engine's download and an event behind it took ~70 us per
+    // Solve on the incremental flow)
+    const double seq = next_seq(h_x.p + n);
+    arslam::launch_copy_out(d_src, n, h_x.p, d_seq_done.p, h_x.p + n, seq, stream);
+    flag_sync(h_x.p + n, seq);
+  } else {
+    HIP_CHECK(hipMemcpyAsync(h_x.p, d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+  }
   if (nranks > 1) {
     // the camera and each tag from the rank holding it (the others hold stale
     // values of other ranks' subtree tags, and of the camera when its rows are
@@ -1190,7 +1200,7 @@ void arslam_lm::write_back(const double *d_src) {
     HIP_CHECK(hipMemcpyAsync(h_x.p, d_lx.p, 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipMemcpyAsync(h_x.p + t0, d_lx.p + 3, (n - t0) * sizeof(double), hipMemcpyDeviceToHost, stream));
   }
-  spin_sync();
+  if (nranks > 1 || dma) spin_sync();
   const double *h = h_x.p;
   std::memcpy(soa.camera, h, 3 * sizeof(double));
   if (elim_used == ARSLAM_ELIM_MIXED) {   // groups (not the direct ones: copies) and f-blocks to their blocks
