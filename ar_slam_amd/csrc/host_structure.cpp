@@ -989,8 +989,18 @@ SchurContrib gather_contrib(const SchurGather &G, const GatherItem &t) {
 }
 
 // the gather launch's work items: a destination per item, or its contributions
-// in chunks summed through partial slots (k_schur_combine)
-void gather_partition(SchurGather &G) {
+// in chunks summed through partial slots (k_schur_combine).  An item's wave
+// sums its contributions in G = 64 / (the block's elements) lane groups, so a
+// piece holds up to kSchurChunk contributions per group, 16 at least: a
+// 1-element block (camera, rhs) up to 1,024 -- the whole destination on
+// problems of up to 1,024 captures, and no combine launch there
+int gather_chunk(const SchurGather &G, int d, long nR, int cam_row) {
+  const int rX = G.dest_row[2L * d], rY = G.dest_row[2L * d + 1];
+  const int e = ((rX == nR || rX == cam_row) ? 1 : 6) * (rY == cam_row ? 1 : 6);
+  return std::max(kSchurChunk, 16 * (64 / e));
+}
+
+void gather_partition(SchurGather &G, long nR, int cam_row) {
   G.items.clear();
   G.splits.clear();
   G.n_pslots = 0;
@@ -999,14 +1009,15 @@ void gather_partition(SchurGather &G) {
   for (int d = 0; d < nd; ++d) {
     const int k0 = G.dest_start[d], k1 = G.dest_start[d + 1];
     G.max_contrib = std::max(G.max_contrib, k1 - k0);
-    if (k1 - k0 <= kSchurChunk) {
+    const int chunk = gather_chunk(G, d, nR, cam_row);
+    if (k1 - k0 <= chunk) {
       G.items.insert(G.items.end(), {d, k0, k1, -1});
       continue;
     }
-    const int pieces = (k1 - k0 + kSchurChunk - 1) / kSchurChunk;
+    const int pieces = (k1 - k0 + chunk - 1) / chunk;
     G.splits.insert(G.splits.end(), {d, G.n_pslots, pieces, 0});
     for (int q = 0; q < pieces; ++q)
-      G.items.insert(G.items.end(), {d, k0 + q * kSchurChunk, std::min(k1, k0 + (q + 1) * kSchurChunk), G.n_pslots + q});
+      G.items.insert(G.items.end(), {d, k0 + q * chunk, std::min(k1, k0 + (q + 1) * chunk), G.n_pslots + q});
     G.n_pslots += pieces;
   }
 }
@@ -1051,7 +1062,7 @@ SchurGather schur_gather_plan(const HostProblem &h, const ReducedLayout &L) {
     G.contrib.push_back(gather_contrib(G, items[i]));
   }
   G.dest_start.push_back((int)G.contrib.size());
-  gather_partition(G);
+  gather_partition(G, L.nR, L.cam_row);
   return G;
 }
 
@@ -1098,7 +1109,7 @@ void schur_gather_extend(SchurGather &G, const HostProblem &h, const ReducedLayo
   G.dest_row.swap(dest_row);
   G.dest_start.swap(dest_start);
   G.contrib.swap(contrib);
-  gather_partition(G);
+  gather_partition(G, L.nR, L.cam_row);
 }
 
 }  // namespace arslam

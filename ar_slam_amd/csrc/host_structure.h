@@ -188,7 +188,8 @@ ARSLAM_HD inline long schur_block_off(int U, int V, int nblk) {
   return R + (long)schur_blk_size(U, nblk) * schur_blk_start(V, nblk);
 }
 ARSLAM_HD inline long schur_slab_size(int nblk) { return 3 + 12L * nblk + 18L * nblk * (nblk + 1); }
-// A destination with more than kSchurChunk contributions is summed in pieces
+// A destination with more than kSchurChunk contributions per lane group of its
+// k_schur_gather wave (gather_partition) is summed in pieces
 // (work items writing partial sums, then one combine per split destination
 // adding the pieces in order), so no wave walks a long list serially.
 constexpr int kSchurChunk = 64;

@@ -910,24 +910,31 @@ __global__ __launch_bounds__(256) void k_schur_gather(DevProblem P, double *__re
   const int4 item = P.gather_items[it];
   const int2 rr = P.dest_row[item.x];
   const GatherLane g(P, rr, lane);
-  const int nk = item.z - item.y;   // <= 64
-  if (lane < nk) cts[w][lane] = P.contrib[item.y + lane];
+  const int nk = item.z - item.y;   // (gather_partition: <= 64, or <= 16 per lane group)
+  const bool staged = nk <= kWave;
+  if (staged && lane < nk) cts[w][lane] = P.contrib[item.y + lane];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   double s = 0.0;
-  if (g.grp < g.G) {
+  // (a long item -- a 1- or 6-element block summing up to 16 contributions
+  // per group -- reads its descriptors itself; the same order either way)
+  auto sum = [&](const SchurContrib *src) __attribute__((always_inline)) {
     for (int t0 = g.grp; t0 < nk; t0 += 8 * g.G) {
       double v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int t = min(t0 + u * g.G, nk - 1);   // clamped: always a valid address
-        const SchurContrib ct = cts[w][t];
+        const SchurContrib ct = src[t];
         v[u] = P.slab[ct.off + (ct.tr ? g.j * ct.ld + g.i : g.i * ct.ld + g.j)];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += (t0 + u * g.G < nk) ? v[u] : 0.0;
     }
+  };
+  if (g.grp < g.G) {
+    if (staged) sum(cts[w]);
+    else sum(P.contrib + item.y);
   }
   s = gather_groups(s, g, part[w], lane);
   if (lane >= g.E) return;
