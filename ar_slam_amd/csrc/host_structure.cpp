@@ -989,12 +989,13 @@ SchurContrib gather_contrib(const SchurGather &G, const GatherItem &t) {
 }
 
 // the gather launch's work items: a destination per item, or its contributions
-// in chunks summed through partial slots (k_schur_combine).  An item's wave
-// sums its contributions in G = 64 / (the block's elements) lane groups, so a
-// piece holds up to kSchurChunk contributions per group, 16 at least: a
-// 1-element block (camera, rhs) up to 1,024 -- the whole destination on
-// problems of up to 1,024 captures, and no combine launch there
-int gather_chunk(const SchurGather &G, int d, long nR, int cam_row) {
+// in chunks of kSchurChunk summed through partial slots (k_schur_combine).  An
+// item's wave sums its contributions in G = 64 / (the block's elements) lane
+// groups, so a destination stays one item up to 16 contributions per group (64
+// at least): a 1-element block (camera, rhs) up to 1,024 -- problems of up to
+// 1,024 captures need no combine launch.  Longer ones keep 64-contribution
+// pieces (a 1,024-contribution item's wave outlasts the rest of the gather)
+int gather_single_max(const SchurGather &G, int d, long nR, int cam_row) {
   const int rX = G.dest_row[2L * d], rY = G.dest_row[2L * d + 1];
   const int e = ((rX == nR || rX == cam_row) ? 1 : 6) * (rY == cam_row ? 1 : 6);
   return std::max(kSchurChunk, 16 * (64 / e));
@@ -1009,8 +1010,8 @@ void gather_partition(SchurGather &G, long nR, int cam_row) {
   for (int d = 0; d < nd; ++d) {
     const int k0 = G.dest_start[d], k1 = G.dest_start[d + 1];
     G.max_contrib = std::max(G.max_contrib, k1 - k0);
-    const int chunk = gather_chunk(G, d, nR, cam_row);
-    if (k1 - k0 <= chunk) {
+    const int chunk = kSchurChunk;
+    if (k1 - k0 <= gather_single_max(G, d, nR, cam_row)) {
       G.items.insert(G.items.end(), {d, k0, k1, -1});
       continue;
     }
