@@ -458,6 +458,7 @@ struct arslam_lm {
   // several ranks: the whole problem's capture count, this rank's captures
   // (ascending; the loaded problem's capture c is own_caps[c]) and its local arrays
   int nc_full = 0;
+  int nc_user = 0;   // the caller's capture count (the device problem's "captures" are tags or groups under TAGS / MIXED)
   std::vector<int> own_caps;
   std::vector<double> loc_cap, loc_corners;
   std::vector<int> loc_obs_cap, loc_obs_tag;
@@ -660,6 +661,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   std::vector<int> col_class;
   own_caps.clear();
   nc_full = p->n_cap;
+  nc_user = p_in->n_cap;
   if (nranks > 1) {
     // Several ranks: every rank holds the whole problem and computes the same
     // structure (deterministic host code, no exchange): the reduced layout,
@@ -1023,6 +1025,7 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   for (int &sl : lay.row_slot)
     if (sl >= 3) sl += 6 * (h.nc - nc);
   nc = h.nc;
+  nc_user = p->n_cap;
   nb = h.nb;
   n = h.n;
   nb_global = h.nb_global;
@@ -1699,7 +1702,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->ceres_e_captures = ceres_e_cap;
   s->ceres_e_tags = ceres_e_tag;
   s->n_ranks = nranks;
-  s->n_owned_captures = nc;
+  s->n_owned_captures = nranks > 1 ? nc : nc_user;   // (one rank: every capture, whichever side is eliminated)
   s->n_top_tiles = nranks > 1 ? plan.n_top_tiles : 0;
   s->split_top_work = split_top_work;
   s->split_max_rank_work = split_max_rank_work;
@@ -2010,7 +2013,7 @@ int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks, const unsigned char i
 int arslam_lm_owned_captures(const arslam_lm *h, int *out, int cap, int *n) {
   if (!h || !n || (cap > 0 && !out)) return ARSLAM_E_INVALID_ARG;
   if (!h->loaded) return ARSLAM_E_STATE;
-  const int k = h->nranks > 1 ? (int)h->own_caps.size() : h->nc;
+  const int k = h->nranks > 1 ? (int)h->own_caps.size() : h->nc_user;   // (one rank: every capture)
   for (int i = 0; i < k && i < cap; ++i) out[i] = h->nranks > 1 ? h->own_caps[i] : i;
   *n = k;
   return ARSLAM_OK;

@@ -137,6 +137,7 @@ def test_mixed_set_matches_oracle(lm, oracle, name):
     _compare(g, ours, ref)
     s = ours[3]
     assert s["elimination_used"] == used
+    assert s["n_owned_captures"] == g.n_cap   # (one rank: every capture, whatever the device groups)
     assert (s["ceres_e_captures"], s["ceres_e_tags"]) == (int(ec.sum()), int(et.sum()))
     # the reduced system: every capture and tag outside the set, and the camera
     n_f = g.n_cap + len(np.unique(g.obs_tag)) - int(ec.sum()) - int(et.sum())
