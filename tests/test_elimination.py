@@ -129,3 +129,23 @@ def test_oracle_mixed_set_matches_capture_elimination(name):
     for x, y in zip(a["iterations"], b["iterations"]):
         assert abs(x["cost"] - y["cost"]) <= 1e-11 * x["cost"]
 
+
+def test_mixed_device_problem_with_constant_blocks(L):
+    """Constant captures and tags are not in Ceres' graph: they stay on the reduced side (no
+    rows), and residuals joining two reduced-side poses -- constant ones included -- go to the
+    direct groups."""
+    g = synth.config_graph("medium")
+    rng = np.random.default_rng(11)
+    cap_const = (rng.random(g.n_cap) < 0.1).astype(np.uint8)
+    tag_const = (rng.random(g.n_tag) < 0.1).astype(np.uint8)
+    r = L.debug_mixed_groups(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, cap_const=cap_const,
+                             tag_const=tag_const)
+    m = ceres_e_blocks(g.obs_cap, g.obs_tag, g.n_cap, g.n_tag, cap_const=cap_const, tag_const=tag_const,
+                       members=True)
+    ec, et = np.array(m["e_cap"], np.uint8), np.array(m["e_tag"], np.uint8)
+    assert (r["e_cap"] == ec).all() and (r["e_tag"] == et).all()
+    assert not (ec & cap_const).any() and not (et & tag_const).any()   # constants are never e-blocks
+    direct = len({int(c) for c, t in zip(g.obs_cap, g.obs_tag) if not ec[c] and not et[t]})
+    assert r["groups"] == ec.sum() + et.sum() + direct and r["direct"] == direct
+    assert r["f_blocks"] == g.n_cap + g.n_tag - ec.sum() - et.sum()
+
