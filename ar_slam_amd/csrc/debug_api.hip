@@ -224,6 +224,7 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
       info->factor_flops = plan.total_factor_flops;
       info->scalar_flops = L.scalar_flops;
       info->n_dag_tasks = plan.n_dag_tasks;
+      info->fill_first_ok = plan.fill_first_ok ? 1 : 0;
       info->dag_valid = arslam::dag_check(plan) ? 1 : 0;
       if (const char *dump = std::getenv("ARSLAM_DAG_DUMP")) {   // debug: the task graph, for offline analysis
         if (FILE *f = std::fopen(dump, "wb")) {

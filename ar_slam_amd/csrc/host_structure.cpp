@@ -592,6 +592,8 @@ MixedProblem mixed_problem(const arslam_soa_problem &p, const std::vector<uint8_
                            const std::vector<uint8_t> &e_tag) {
   MixedProblem m;
   const int nc = p.n_cap, nt = p.n_tag, nb = p.n_obs;
+  m.src_n_cap = nc;
+  m.src_n_tag = nt;
   std::vector<int> cap_f(nc, -1), tag_f(nt, -1), cap_g(nc, -1), tag_g(nt, -1), cap_d(nc, -1);
   for (int t = 0; t < nt; ++t)
     if (!e_tag[t]) { tag_f[t] = (int)m.f_src.size(); m.f_src.push_back(t); m.f_is_cap.push_back(0); }

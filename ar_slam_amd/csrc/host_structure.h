@@ -114,6 +114,7 @@ struct MixedProblem {
   std::vector<unsigned char> f_is_cap;    // [f-blocks]
   std::vector<int> f_alias;               // [f-blocks] the direct group copying it, -1
   int n_direct = 0;
+  int src_n_cap = 0, src_n_tag = 0;       // the original problem's block counts (reload guard)
 };
 // p's observations regrouped by the e-set (e_cap / e_tag from ceres_schur_side)
 MixedProblem mixed_problem(const arslam_soa_problem &p, const std::vector<uint8_t> &e_cap,

@@ -490,6 +490,19 @@ void dag_build(LltPlan &plan) {
         plan.h_dag_ks_tiles[q] = make_int2(tid(tg.x, plan.h_ks[q]), tid(tg.y, plan.h_ks[q]));
     }
   }
+  // Fill tiles are not cleared on one rank: the first update of each stores
+  // 0 - acc instead of reading the tile (k_factor_dag, first_store).  That is
+  // only sound if every fill tile's first application (sequence 0) is an
+  // unfolded update item of the DAG: a tile with no update, or whose only
+  // update was folded into its POTRF, would be read uncleared.  Checked here,
+  // not assumed; the solver clears every tile when it fails.
+  {
+    plan.fill_first_ok = plan.n_phases == 1;
+    std::vector<char> first(nt, 0);
+    for (const int4 &tk : plan.h_dag_tasks)
+      if (tk.x == 2 && tk.z == 0) first[tk.w] = 1;
+    for (long t = plan.n_assembled; t < nt && plan.fill_first_ok; ++t) plan.fill_first_ok = first[t] != 0;
+  }
   long n_potrf = 0, n_trsm = 0;
   for (size_t t = 0; t < plan.h_dag_tasks.size(); ++t) {
     n_potrf += plan.h_dag_tasks[t].x == 0;

@@ -208,6 +208,7 @@ struct LltPlan {
   std::vector<int> h_tile_id;
   long n_tiles = 0;             // tiles of the factor (compact storage = n_tiles * 4096 doubles)
   long n_assembled = 0;         // tiles the Schur assembly writes (numbered first; multi-rank: = n_top_tiles)
+  bool fill_first_ok = false;   // every fill tile's first application is an unfolded update item (dag_build)
   // multi-rank plans (llt_plan_symbolic with column classes): phase 0 factors
   // this rank's subtree columns, phase 1 the replicated top columns after the
   // exchange of the top tiles (numbered first: tiles [0, n_top_tiles))

@@ -1346,7 +1346,10 @@ __device__ __forceinline__ void reduce_parts_block(int p, const double *__restri
     // this block's host words out of its XCD's L2 (the blocks span XCDs);
     // then the last block to finish stores the sequence number
     __threadfence_system();
-    if (seq_done && seq > 0.0 && atomicAdd(seq_done, 1) == (int)gridDim.x - 1) {
+    // acq_rel at system scope: the last block acquires every other block's
+    // fenced host stores before its release of the sequence word
+    if (seq_done && seq > 0.0 &&
+        __hip_atomic_fetch_add(seq_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == (int)gridDim.x - 1) {
       atomicExch(seq_done, 0);
       __hip_atomic_store(hout + kHostSeq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1702,7 +1705,8 @@ __global__ __launch_bounds__(256) void k_copy_out(const double *__restrict__ src
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
   __threadfence_system();
   __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(seq_done, 1) == (int)gridDim.x - 1) {
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(seq_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == (int)gridDim.x - 1) {
     atomicExch(seq_done, 0);
     __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }

@@ -408,19 +408,26 @@ struct arslam_lm {
 
   int cus_device = -1, cus = 0;   // the CU count, queried once per device
   // The thread and options device the handle's stream was last made ready
-  // for: a later load from the same thread with the same options makes no HIP
-  // call here.
+  // for: a later load from the same thread with the same options, while the
+  // thread's current device is still the handle's, makes one hipGetDevice (a
+  // thread-local read) and nothing else.  The current-device check matters
+  // when one thread drives handles on several devices: another handle's load
+  // may have switched it, and this handle's allocations must land on its own
+  // device.
   std::thread::id ready_thread{};
   int ready_opt_device = -2;
   void ensure_stream() {
-    if (stream && ready_thread == std::this_thread::get_id() && ready_opt_device == opt.device) {
+    int cur = -1;
+    HIP_CHECK(hipGetDevice(&cur));
+    if (stream && ready_thread == std::this_thread::get_id() && ready_opt_device == opt.device && cur == device) {
       return;
     }
-    HIP_CHECK(hipGetDevice(&device));
-    if (opt.device >= 0 && opt.device != device) {   // (set only when it differs)
-      HIP_CHECK(hipSetDevice(opt.device));
-      device = opt.device;
-    }
+    // the handle's device: the options device, else the one its stream lives on, else the current one
+    const int want = opt.device >= 0 ? opt.device : (stream ? device : cur);
+    fail_if(stream && want != device, ARSLAM_E_STATE,
+            "the handle's device changed after its stream was created (set options.device before the first load)");
+    if (want != cur) HIP_CHECK(hipSetDevice(want));   // (set only when it differs)
+    device = want;
     if (cus_device != device) {
       cus = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
@@ -885,7 +892,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
         for (int J = rY >> 6; J <= (rY + sy - 1) >> 6 && J <= I; ++J)
           fill_gathered = fill_gathered || plan.h_tile_id[(long)I * T + J] >= plan.n_assembled;
     }
-    if (!fill_gathered) n_clear = plan.n_assembled;
+    if (!fill_gathered && plan.fill_first_ok) n_clear = plan.n_assembled;
   }
   upload.commit(stream);
   d_xa.alloc(n); d_xb.alloc(n); d_xbest.alloc(n);
@@ -1049,7 +1056,8 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
 void arslam_lm::reload_values(const arslam_soa_problem *p_in) {
   const double t0 = now_s();
   if (elim_used == ARSLAM_ELIM_MIXED) {   // the regrouped slots from p_in's blocks
-    fail_if(!loaded || p_in->n_obs != (int)mx.obs_cap.size(), ARSLAM_E_STATE,
+    fail_if(!loaded || p_in->n_obs != (int)mx.obs_cap.size() || p_in->n_cap != mx.src_n_cap ||
+                p_in->n_tag != mx.src_n_tag, ARSLAM_E_STATE,
             "reload_values: structure differs from the loaded problem");
     arslam::mixed_values(mx, *p_in, x0.data());
     HIP_CHECK(hipMemcpyAsync(u_x0, x0.data(), n * sizeof(double), hipMemcpyHostToDevice, stream));
@@ -1799,6 +1807,9 @@ int arslam_lm_set_options(arslam_lm *h, const arslam_lm_options *opt) {
             "factor_executor must be 0 or 1");
     fail_if(opt->max_num_iterations < 0 || opt->max_num_iterations > ARSLAM_LM_MAX_ITERS,
             ARSLAM_E_INVALID_ARG, "max_num_iterations out of range");
+    // the stream and every device buffer live on the device of the first load
+    fail_if(h->stream && opt->device >= 0 && opt->device != h->device,
+            ARSLAM_E_INVALID_ARG, "a handle's device is fixed once it has loaded a problem: create a new handle");
     if (opt->device != h->opt.device || opt->reduced_ordering != h->opt.reduced_ordering ||
         opt->cholesky_skip_zero_tiles != h->opt.cholesky_skip_zero_tiles || opt->elimination != h->opt.elimination)
       h->loaded = false, h->pk_dirty = true;

@@ -514,7 +514,7 @@ class PlanInfo(C.Structure):
                 ("n_levels", C.c_int), ("n_assembled_tiles", C.c_long), ("n_factor_tiles", C.c_long),
                 ("n_update_tiles", C.c_long), ("n_update_items", C.c_long), ("n_split_targets", C.c_long),
                 ("update_flops", C.c_double), ("n_dag_tasks", C.c_long), ("dag_valid", C.c_int),
-                ("factor_flops", C.c_double), ("scalar_flops", C.c_double)]
+                ("factor_flops", C.c_double), ("scalar_flops", C.c_double), ("fill_first_ok", C.c_int)]
 
 
 def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False, cap_const=None,

@@ -292,24 +292,51 @@ def launch_ranks(args):
     if not args.launch_check:
         from ar_slam_amd import build
         build.build()
+    import tempfile
+    import time
     port = _free_port()
     procs = []
+    # rank 0's line goes to a file (no pipe to drain while the ranks are polled)
+    out0 = tempfile.TemporaryFile()
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, cwd=ROOT))
-    out = procs[0].stdout.read().decode()
+                                      stdout=out0 if r == 0 else sys.stderr, cwd=ROOT))
+    # Poll every rank: a rank that dies (a bad build, an init error before the
+    # rendezvous) would leave the others waiting in a collective forever, so
+    # the first non-zero exit ends the rest and is returned.
+    bad = 0
+    while [p.poll() for p in procs].count(None):   # (every rank polled: no short-circuit)
+        failed = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if failed:
+            bad = failed[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.2)
     rcs = [p.wait() for p in procs]
-    sys.stdout.write(out)
+    out0.seek(0)
+    sys.stdout.write(out0.read().decode())
     sys.stdout.flush()
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    if not bad:
+        nz = [rc for rc in rcs if rc != 0]
+        bad = nz[0] if nz else 0
+    return bad
 
 
 def launch_check(world, rank):
     """`--launch-check` (CPU, no GPU): the ranks meet over gloo and rank 0 prints who came -- the
     launcher and rendezvous of the multi-rank bench without a solve (tests/test_bench_launch.py)."""
+    if os.environ.get("ARSLAM_LAUNCH_CHECK_FAIL_RANK") == str(rank):   # (test: a rank dying before the rendezvous)
+        sys.exit(3)
     import torch
     import torch.distributed as dist
     t = torch.zeros(world, dtype=torch.int64)

@@ -60,6 +60,8 @@ typedef struct {
   double factor_flops;     /* flops of the tile plan per factorization (POTRF, TRSM, updates, inverses) */
   double scalar_flops;     /* flops of the scalar Cholesky of the real rows in this order (no padding,
                               no structurally zero entries inside tiles) */
+  int fill_first_ok;       /* 1: every fill tile's first application is an unfolded update item, so the
+                              solver leaves fill tiles uncleared and that update stores 0 - acc */
 } arslam_plan_info;
 
 /* diagnostic builds only (-DARSLAM_SCHUR_STAMPS): per-phase cycles of the

@@ -36,3 +36,16 @@ def test_gpus_flag_four_ranks():
 def test_one_gpu_starts_no_children():
     d = _run("--gpus", "1", "--launch-check")
     assert d["n_gpus"] == 1 and d["ranks"] == [0] and d["env"]["LOCAL_WORLD_SIZE"] is None
+
+
+def test_a_dead_rank_ends_the_launch():
+    """A rank that exits before the rendezvous must not leave rank 0 waiting in it forever: the
+    launcher polls every rank, ends the others at the first non-zero exit and returns that status."""
+    import time
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    e["ARSLAM_LAUNCH_CHECK_FAIL_RANK"] = "1"
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                         capture_output=True, text=True, timeout=120, env=e, cwd=ROOT)
+    assert out.returncode == 3, (out.returncode, out.stderr[-2000:])
+    assert time.time() - t0 < 60
