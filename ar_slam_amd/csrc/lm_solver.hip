@@ -340,6 +340,11 @@ struct arslam_lm {
   // ---- multi-GPU ----
   int rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
+  // debug (arslam_debug_force_multirank): take the multi-rank path -- the
+  // split, the two-phase factorization and every collective -- with one rank,
+  // so its RCCL calls run on a one-GPU box
+  bool force_multi = false;
+  bool multi() const { return nranks > 1 || force_multi; }
 
   ~arslam_lm() {
     for (auto &t : timers) t.destroy();
@@ -358,7 +363,7 @@ struct arslam_lm {
   // In-place all-reduce of a device buffer over the ranks (RCCL, or the
   // caller's callback).  Every rank issues the same sequence of calls.
   void allreduce_any(void *buf, size_t count, int dtype, int op) {
-    if (nranks <= 1 || count == 0) return;
+    if (!multi() || count == 0) return;
     const size_t bytes = count * (dtype == ARSLAM_DT_F64 ? sizeof(double) : 1);
     comm_bytes += (double)bytes;
     ++comm_calls;
@@ -372,7 +377,7 @@ struct arslam_lm {
       HIP_CHECK(hipStreamSynchronize(stream));
       return;
     }
-    fail_if(!comm, ARSLAM_E_STATE, "nranks > 1 without a communicator");
+    fail_if(!comm, ARSLAM_E_STATE, "the multi-rank path without a communicator");
     NCCL_CHECK(ncclAllReduce(buf, buf, count, dtype == ARSLAM_DT_F64 ? ncclDouble : ncclUint8,
                              op == ARSLAM_OP_SUM ? ncclSum : ncclMax, comm, stream));
   }
@@ -544,7 +549,7 @@ struct arslam_lm {
   PinnedBuf h_lin;   // [0..3] cost, fixed, g_f, col_f; [16..21] slot norms; [16 + kHostSeq] lin_seq
   double lin_seq = 0.0;   // (one rank) the last linearization's sequence number
   void lin_sync() {   // the linearization's host words (one rank: its flag; several: after the copies)
-    if (nranks == 1 && lin_seq > 0.0) flag_sync(h_lin.p + 16 + arslam::kHostSeq, lin_seq);
+    if (!multi() && lin_seq > 0.0) flag_sync(h_lin.p + 16 + arslam::kHostSeq, lin_seq);
     else spin_sync();
   }
   // host LM loop: the Jacobi scale of this solve is set, so each later
@@ -630,19 +635,19 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   const bool tags_fit = cs.max_tag_blk <= arslam::kMaxSchurBlocks, caps_fit = cs.max_cap_blk <= arslam::kMaxSchurBlocks;
   int side = opt.elimination;
   if (side == ARSLAM_ELIM_AUTO)
-    side = (nranks == 1 && tags_fit && (cs.e_tag > cs.e_cap || !caps_fit)) ? ARSLAM_ELIM_TAGS : ARSLAM_ELIM_CAPTURES;
+    side = (!multi() && tags_fit && (cs.e_tag > cs.e_cap || !caps_fit)) ? ARSLAM_ELIM_TAGS : ARSLAM_ELIM_CAPTURES;
   if (side == ARSLAM_ELIM_MIXED) {
     // Ceres' exact set: a whole side when it holds one kind only (then it is
     // every free block of that kind), the mixed device problem otherwise; the
     // camera joins it only in degenerate graphs (one residual), where the
     // device eliminates the captures instead
-    fail_if(nranks > 1, ARSLAM_E_UNSUPPORTED, "the mixed e-block set is single-rank only (the ranks own captures)");
+    fail_if(multi(), ARSLAM_E_UNSUPPORTED, "the mixed e-block set is single-rank only (the ranks own captures)");
     if (cs.e_cam || cs.e_tag == 0) side = ARSLAM_ELIM_CAPTURES;
     else if (cs.e_cap == 0) side = ARSLAM_ELIM_TAGS;
   }
-  fail_if(side == ARSLAM_ELIM_TAGS && nranks > 1, ARSLAM_E_UNSUPPORTED,
+  fail_if(side == ARSLAM_ELIM_TAGS && multi(), ARSLAM_E_UNSUPPORTED,
           "tag elimination is single-rank only (the ranks own captures)");
-  fail_if(nranks > 1 && opt.factor_executor != 1, ARSLAM_E_UNSUPPORTED,
+  fail_if(multi() && opt.factor_executor != 1, ARSLAM_E_UNSUPPORTED,
           "several ranks need the persistent executor (factor_executor = 1)");
   fail_if(side == ARSLAM_ELIM_TAGS && !tags_fit, ARSLAM_E_UNSUPPORTED,
           "tag elimination: a tag seen by more than 256 distinct captures");
@@ -669,7 +674,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   own_caps.clear();
   nc_full = p->n_cap;
   nc_user = p_in->n_cap;
-  if (nranks > 1) {
+  if (multi()) {
     // Several ranks: every rank holds the whole problem and computes the same
     // structure (deterministic host code, no exchange): the reduced layout,
     // then the subtree-to-rank split of the tile elimination tree, which
@@ -677,7 +682,15 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
     const arslam::HostProblem hf = arslam::host_problem(p, nullptr);   // validates p
     L = arslam::reduced_layout(hf, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
                                can_reuse ? &prev_tag_row : nullptr, prev_order_edges);
-    const arslam::RankSplit split = arslam::rank_split(hf, L, nranks);
+    arslam::RankSplit split = arslam::rank_split(hf, L, std::max(nranks, 2));
+    if (nranks == 1) {
+      // (forced multi-rank path on one rank: the two-rank split's replicated
+      // top, everything below it this rank's -- the exchange then carries the
+      // top tiles, as it would between ranks)
+      for (int &o : split.col_owner) o = o < 0 ? -1 : 0;
+      for (int &o : split.cap_owner) o = 0;
+      split.n_active = 1;
+    }
     col_class = split.col_class(rank);
     split_top_work = split.top_work;
     split_max_rank_work = split.max_rank_work;
@@ -753,7 +766,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   }
   prev_tag_row = L.tag_row;
   prev_order_edges = L.order_edges;
-  if (nranks == 1) covis_build(h, L);
+  if (!multi()) covis_build(h, L);
   prev_ordering = opt.reduced_ordering;
   prev_skip = opt.cholesky_skip_zero_tiles;
   tp[2] = now_s();
@@ -762,7 +775,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   has_f = nR > 0;
   if (has_f) {
     N = L.N;
-    arslam::llt_plan_build(plan, L.T, N, L.pattern, stream, nranks > 1 ? &col_class : nullptr);
+    arslam::llt_plan_build(plan, L.T, N, L.pattern, stream, multi() ? &col_class : nullptr);
   } else {
     N = 0;
     arslam::llt_plan_free(plan);
@@ -771,7 +784,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   tp[4] = now_s();
   upload_problem(h, L);
   tp[5] = now_s();
-  if (nranks == 1) lay = std::move(L);   // (try_extend: an appended problem keeps this layout and plan)
+  if (!multi()) lay = std::move(L);   // (try_extend: an appended problem keeps this layout and plan)
   setup_kind = ARSLAM_SETUP_LOAD;
   soa = side == ARSLAM_ELIM_MIXED ? *p_in : *p;   // (mixed: write_back maps the device slots to p_in's blocks)
   loaded = true;
@@ -831,7 +844,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   upload.add(&u_fslot_row, fslot_row.data(), fslot_row.size());
   // several ranks: the top tags' slots (their linearization sums ride with the top tiles)
   std::vector<int> top_slots;
-  if (nranks > 1 && has_f)
+  if (multi() && has_f)
     for (long sl = 3 + 6L * nc; sl < n; ++sl) {
       const int r = fslot_row[sl - 6L * nc];
       if (r >= 0 && plan.h_col_class[r / arslam::kTile] == 1) top_slots.push_back((int)sl);
@@ -842,7 +855,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   // rows; the top's rows, the camera and the tags outside the reduced system
   // on rank 0 (every rank holds the top, one counts it); capture slots all
   f_own.clear();
-  if (nranks > 1) {
+  if (multi()) {
     f_own.assign(n, 0);
     for (long sl = 3; sl < 3 + 6L * nc; ++sl) f_own[sl] = 1;
     for (long sl = 0; sl < n; ++sl) {
@@ -880,7 +893,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
     upload.add(&u_gather_splits, reinterpret_cast<const int4 *>(sg.splits.data()), n_splits);
   }
   n_clear = has_f ? plan.n_tiles : 0;
-  if (has_f && nranks == 1) {
+  if (has_f && !multi()) {
     // does the gather write into a fill tile (an appended problem's new
     // coupling; the plan is kept)?
     const int T = plan.T;
@@ -916,7 +929,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   if (has_f) {
     d_slab.alloc(std::max(sg.cap_off[nc], 1L));
     d_gather_part.alloc(36L * std::max(sg.n_pslots, 1));
-    s_pre = nranks > 1 ? round_up(top_tail_len(), 512) : 0;
+    s_pre = multi() ? round_up(top_tail_len(), 512) : 0;
     d_S.alloc((size_t)s_pre + (size_t)plan.n_tiles * 4096);   // (cleared by k_schur's extra blocks every step)
     Sp = d_S.p + s_pre;
     d_z.alloc(N);
@@ -946,8 +959,8 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.tag_start = u_tag_start; P.tag_obs = u_tag_obs; P.corners = u_corners;
   P.tag_row = u_tag_row; P.row_slot = u_row_slot;
   P.tile_id = plan.tile_id; P.T = plan.T;
-  P.tile_class = nranks > 1 && has_f ? plan.tile_class : nullptr;
-  P.f_own = nranks > 1 || mixed ? u_f_own : nullptr;
+  P.tile_class = multi() && has_f ? plan.tile_class : nullptr;
+  P.f_own = multi() || mixed ? u_f_own : nullptr;
   P.cap_kind = mixed ? u_cap_kind : nullptr;
   P.f_alias = mixed ? u_f_alias : nullptr;
   P.cap_off = u_cap_off; P.slab = d_slab.p; P.dest_row = u_dest_row; P.dest_start = u_dest_start;
@@ -971,7 +984,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
 // load() instead.  (summary.factor_scalar_flops keeps the loaded problem's
 // count: a new coupling inside a fill tile changes the scalar structure.)
 bool arslam_lm::try_extend(const arslam_soa_problem *p) {
-  if (!loaded || nranks > 1 || elim_used != ARSLAM_ELIM_CAPTURES || !has_f ||
+  if (!loaded || multi() || elim_used != ARSLAM_ELIM_CAPTURES || !has_f ||
       (opt.elimination != ARSLAM_ELIM_AUTO && opt.elimination != ARSLAM_ELIM_CAPTURES))
     return false;
   const double t0 = now_s();
@@ -1069,10 +1082,10 @@ void arslam_lm::reload_values(const arslam_soa_problem *p_in) {
   }
   const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
   const arslam_soa_problem *p = elim_used == ARSLAM_ELIM_TAGS ? &swapped : p_in;
-  fail_if(!loaded || p->n_cap != nc_full || p->n_tag != nt || (nranks == 1 && p->n_obs != nb), ARSLAM_E_STATE,
+  fail_if(!loaded || p->n_cap != nc_full || p->n_tag != nt || (!multi() && p->n_obs != nb), ARSLAM_E_STATE,
           "reload_values: structure differs from the loaded problem");
   std::memcpy(x0.data(), p->camera, 3 * sizeof(double));
-  if (nranks > 1) {
+  if (multi()) {
     for (int c = 0; c < nc; ++c) std::memcpy(x0.data() + 3 + 6L * c, p->cap + 6L * own_caps[c], 6 * sizeof(double));
   } else if (nc) {
     std::memcpy(x0.data() + 3, p->cap, 6L * nc * sizeof(double));
@@ -1091,12 +1104,12 @@ void arslam_lm::linearize_launch() {
   h_lin.alloc(32);
   // one rank: the reductions also store their results straight into the
   // page-locked h_lin (no copy launch); several: h_lin is copied after the exchanges
-  const bool direct = nranks == 1;
+  const bool direct = !multi();
   timers[PH_LIN].start(stream);
   arslam::launch_linearize(P, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
   arslam::launch_lin_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream,
                             direct ? h_lin.p : nullptr);
-  if (nranks > 1) {
+  if (multi()) {
     // this rank's partial sums: the cost and fixed cost saved (the step's
     // reductions reuse d_red) for the scalar exchange; the LM diagonal from
     // them is final for the capture slots and this rank's own subtree tags
@@ -1188,7 +1201,7 @@ void arslam_lm::linearize(double *x_cost, double *fixed_cost, double *gmax, doub
 void arslam_lm::write_back(const double *d_src) {
   h_x.alloc(n + 1);   // page-locked; [n]: the download's sequence word (one rank)
   static const bool dma = std::getenv("ARSLAM_WRITE_BACK_DMA") != nullptr;   // debug A/B: the copy engine
-  if (nranks == 1 && !dma) {
+  if (!multi() && !dma) {
     // a kernel stores x into h_x and then the sequence word the host polls
     // (the copy engine's download and an event behind it took ~70 us per
     // Solve on the incremental flow)
@@ -1198,7 +1211,7 @@ void arslam_lm::write_back(const double *d_src) {
   } else {
     HIP_CHECK(hipMemcpyAsync(h_x.p, d_src, n * sizeof(double), hipMemcpyDeviceToHost, stream));
   }
-  if (nranks > 1) {
+  if (multi()) {
     // the camera and each tag from the rank holding it (the others hold stale
     // values of other ranks' subtree tags, and of the camera when its rows are
     // not in the replicated top -- a split with one active rank and no top):
@@ -1211,7 +1224,7 @@ void arslam_lm::write_back(const double *d_src) {
     HIP_CHECK(hipMemcpyAsync(h_x.p, d_lx.p, 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipMemcpyAsync(h_x.p + t0, d_lx.p + 3, (n - t0) * sizeof(double), hipMemcpyDeviceToHost, stream));
   }
-  if (nranks > 1 || dma) spin_sync();
+  if (multi() || dma) spin_sync();
   const double *h = h_x.p;
   std::memcpy(soa.camera, h, 3 * sizeof(double));
   if (elim_used == ARSLAM_ELIM_MIXED) {   // groups (not the direct ones: copies) and f-blocks to their blocks
@@ -1222,7 +1235,7 @@ void arslam_lm::write_back(const double *d_src) {
     for (int f = 0; f < nt; ++f)
       std::memcpy((mx.f_is_cap[f] ? soa.cap : soa.tag) + 6L * mx.f_src[f], h + 3 + 6L * nc + 6L * f,
                   6 * sizeof(double));
-  } else if (nranks > 1) {   // this rank's captures into the whole problem's array
+  } else if (multi()) {   // this rank's captures into the whole problem's array
     for (int c = 0; c < nc; ++c) std::memcpy(soa.cap + 6L * own_caps[c], h + 3 + 6L * c, 6 * sizeof(double));
   } else if (nc) {
     std::memcpy(soa.cap, h + 3, 6L * nc * sizeof(double));
@@ -1252,7 +1265,7 @@ void arslam_lm::restore_patched_wait() {
 // Several ranks: every rank takes the same branch on the callbacks' answers
 // (MAX over the ranks of continue 0 < terminate successfully 1 < abort 2).
 int arslam_lm::agree_callback(int r) {
-  if (nranks <= 1) return r;
+  if (!multi()) return r;
   const double v = r == ARSLAM_SOLVER_ABORT ? 2.0 : r == ARSLAM_SOLVER_TERMINATE_SUCCESSFULLY ? 1.0 : 0.0;
   d_cb.alloc(1);
   HIP_CHECK(hipMemcpyAsync(d_cb.p, &v, sizeof(double), hipMemcpyHostToDevice, stream));
@@ -1311,7 +1324,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     }
   } restore_wait{this};
   any_iter_cb = iter_cb != nullptr;
-  if (nranks > 1) {   // a callback on any rank: every rank joins the per-iteration agreement
+  if (multi()) {   // a callback on any rank: every rank joins the per-iteration agreement
     const double mine = iter_cb ? 1.0 : 0.0;
     d_cb.alloc(1);
     HIP_CHECK(hipMemcpyAsync(d_cb.p, &mine, sizeof(double), hipMemcpyHostToDevice, stream));
@@ -1463,12 +1476,12 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       // (below).  k_schur's extra blocks clear S's tiles first.
       // (one rank on the persistent executor: the fill tiles the gather does
       // not write are left as they are -- their first update stores)
-      const bool fill_first_store = nranks == 1 && opt.factor_executor == 1;
-      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, Sp, stream, nranks == 1,
+      const bool fill_first_store = !multi() && opt.factor_executor == 1;
+      arslam::launch_schur(P, x, d_scale.p, d_diag.p, radius, Sp, stream, !multi(),
                            fill_first_store ? n_clear : plan.n_tiles, reset_in_schur ? &er : nullptr);
       const bool force_indefinite = dbg_indefinite_mask >> std::min(s->num_linear_solves - 1, 63) & 1ull;
       const long hook_row = P.cam_row >= 0 ? P.cam_row : nR - 1;   // (a top row with several ranks)
-      if (nranks > 1) arslam::launch_prep_reduced(P, d_diag.p, radius, Sp, stream, 0);
+      if (multi()) arslam::launch_prep_reduced(P, d_diag.p, radius, Sp, stream, 0);
       else if (force_indefinite) arslam::debug_set_reduced_diag(P, Sp, hook_row, -1.0, stream);   // test hook
       timers[PH_SCHUR].stop(stream);
       timers[PH_CHOL].start(stream);
@@ -1500,7 +1513,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
             std::fclose(f);
           }
           dag_traced = true;
-        } else if (nranks > 1) {
+        } else if (multi()) {
           // phase 0: this rank's subtree columns, and their updates of the top
           // tiles (its share of the top's Schur complement); then the top tiles
           // are summed over the ranks -- the step's one bulk exchange -- and
@@ -1561,7 +1574,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
         arslam::launch_dense_back_solve_dag(plan, Sp, nR, d_yF.p, d_flag.p, stream, dag_workgroups, false);
       else
         arslam::launch_dense_back_solve(plan, Sp, nR, d_z.p, d_yF.p, d_flag.p, stream);
-      if (nranks > 1) {
+      if (multi()) {
         // y of the top columns (identical on every rank) and of this rank's
         // own subtrees; no exchange: a rank's captures see only those tags
         // (a capture's tags lie on one root path of the elimination tree), so
@@ -1581,10 +1594,10 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     timers[PH_COST].start(stream);
     h_step.alloc(16);
     // (one rank: the scalars are also stored straight into the page-locked h_step)
-    const double step_seq = nranks == 1 ? next_seq(h_step.p + arslam::kHostSeq) : 0.0;
+    const double step_seq = !multi() ? next_seq(h_step.p + arslam::kHostSeq) : 0.0;
     arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p,
-                                nranks == 1 ? h_step.p : nullptr, d_seq_done.p, step_seq);
-    if (nranks > 1) {
+                                !multi() ? h_step.p : nullptr, d_seq_done.p, step_seq);
+    if (multi()) {
       // candidate cost, fixed, model change, capture step^2 by sum; the
       // non-finite flags, the f-side non-finite step, indefinite and executor
       // fault by max (every rank takes the same branch); with a pending
@@ -1598,7 +1611,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
       exchange_scalars(fl);
     }
     timers[PH_COST].stop(stream);
-    if (nranks > 1) {
+    if (multi()) {
       HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 5) * sizeof(double), hipMemcpyDeviceToHost, stream));
       spin_sync();
     } else {
@@ -1710,12 +1723,12 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->ceres_e_captures = ceres_e_cap;
   s->ceres_e_tags = ceres_e_tag;
   s->n_ranks = nranks;
-  s->n_owned_captures = nranks > 1 ? nc : nc_user;   // (one rank: every capture, whichever side is eliminated)
-  s->n_top_tiles = nranks > 1 ? plan.n_top_tiles : 0;
+  s->n_owned_captures = multi() ? nc : nc_user;   // (one rank: every capture, whichever side is eliminated)
+  s->n_top_tiles = multi() ? plan.n_top_tiles : 0;
   s->split_top_work = split_top_work;
   s->split_max_rank_work = split_max_rank_work;
   s->split_total_work = split_total_work;
-  s->n_active_ranks = nranks > 1 ? split_active : 1;
+  s->n_active_ranks = multi() ? split_active : 1;
 }
 
 // ===========================================================================
@@ -1991,12 +2004,13 @@ int arslam_comm_unique_id(unsigned char id[ARSLAM_COMM_ID_BYTES]) {
 }
 
 int arslam_lm_set_comm_callback(arslam_lm *h, int rank, int nranks, arslam_allreduce_fn fn, void *ctx) {
-  if (!h || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return ARSLAM_E_INVALID_ARG;
+  if (!h || nranks < 1 || rank < 0 || rank >= nranks || ((nranks > 1 || h->force_multi) && !fn))
+    return ARSLAM_E_INVALID_ARG;
   return guarded([&] {
     if (h->comm) { (void)ncclCommDestroy(h->comm); h->comm = nullptr; }
     h->rank = rank;
     h->nranks = nranks;
-    h->comm_cb = nranks > 1 ? fn : nullptr;
+    h->comm_cb = h->multi() ? fn : nullptr;
     h->comm_cb_ctx = ctx;
     h->loaded = false;
     h->pk_dirty = true;
@@ -2013,7 +2027,7 @@ int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks, const unsigned char i
     h->nranks = nranks;
     h->loaded = false;
     h->pk_dirty = true;
-    if (nranks > 1) {
+    if (h->multi()) {   // (one rank only under arslam_debug_force_multirank)
       ncclUniqueId u;
       std::memcpy(&u, id, sizeof(u));
       NCCL_CHECK(ncclCommInitRank(&h->comm, nranks, u, rank));
@@ -2024,8 +2038,8 @@ int arslam_lm_set_comm(arslam_lm *h, int rank, int nranks, const unsigned char i
 int arslam_lm_owned_captures(const arslam_lm *h, int *out, int cap, int *n) {
   if (!h || !n || (cap > 0 && !out)) return ARSLAM_E_INVALID_ARG;
   if (!h->loaded) return ARSLAM_E_STATE;
-  const int k = h->nranks > 1 ? (int)h->own_caps.size() : h->nc_user;   // (one rank: every capture)
-  for (int i = 0; i < k && i < cap; ++i) out[i] = h->nranks > 1 ? h->own_caps[i] : i;
+  const int k = h->multi() ? (int)h->own_caps.size() : h->nc_user;   // (one rank: every capture)
+  for (int i = 0; i < k && i < cap; ++i) out[i] = h->multi() ? h->own_caps[i] : i;
   *n = k;
   return ARSLAM_OK;
 }
@@ -2047,6 +2061,19 @@ int arslam_lm_debug_force_indefinite(arslam_lm *h, unsigned long long step_mask)
   if (!h) return ARSLAM_E_INVALID_ARG;
   h->dbg_indefinite_mask = step_mask;
   return ARSLAM_OK;
+}
+
+int arslam_lm_debug_force_multirank(arslam_lm *h, int on) {
+  if (!h || (on != 0 && on != 1)) return ARSLAM_E_INVALID_ARG;
+  return guarded([&] {
+    if (h->comm) { (void)ncclCommDestroy(h->comm); h->comm = nullptr; }
+    h->comm_cb = nullptr;
+    h->rank = 0;
+    h->nranks = 1;
+    h->force_multi = on != 0;
+    h->loaded = false;
+    h->pk_dirty = true;
+  });
 }
 
 int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken) {
@@ -2072,7 +2099,7 @@ int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken) {
 int arslam_lm_debug_tag_pair_tile(arslam_lm *h, const double *tag_a, const double *tag_b, int *status) {
   if (!h || !tag_a || !tag_b || !status) return ARSLAM_E_INVALID_ARG;
   return guarded([&] {
-    fail_if(!h->loaded || h->nranks > 1 || h->elim_used != ARSLAM_ELIM_CAPTURES || !h->has_f, ARSLAM_E_STATE,
+    fail_if(!h->loaded || h->multi() || h->elim_used != ARSLAM_ELIM_CAPTURES || !h->has_f, ARSLAM_E_STATE,
             "tag_pair_tile needs a pointer-keyed problem loaded with capture elimination on one rank");
     const auto ia = h->tag_of.find(const_cast<double *>(tag_a)), ib = h->tag_of.find(const_cast<double *>(tag_b));
     *status = -1;

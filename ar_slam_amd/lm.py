@@ -46,7 +46,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_set_iteration_callback", "arslam_lm_owned_captures",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
-           "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
+           "arslam_lm_debug_force_multirank", "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
            "arslam_debug_mixed_groups",
            "arslam_debug_dag_simulate", "arslam_debug_dag_fault_detail", "arslam_debug_box_fingerprint",
@@ -225,6 +225,7 @@ def lib():
     L.arslam_debug_ceres_e_blocks.argtypes = [C.POINTER(SoaProblem), _ip]
     L.arslam_debug_mixed_groups.argtypes = [C.POINTER(SoaProblem), _ip, C.POINTER(C.c_ubyte), C.POINTER(C.c_ubyte)]
     L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
+    L.arslam_lm_debug_force_multirank.argtypes = [C.c_void_p, C.c_int]
     L.arslam_lm_set_iteration_callback.argtypes = [C.c_void_p, ITER_CB, C.c_void_p]
     L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
     if hasattr(L, "arslam_lm_debug_tag_pair_tile"):   # (absent from older variant builds under A/B)
@@ -349,6 +350,11 @@ class _Handle:
         reduced system (camera diagonal -1), i.e. an invalid LM step."""
         _check(lib().arslam_lm_debug_force_indefinite(self._h, C.c_ulonglong(step_mask & (2**64 - 1))))
 
+    def debug_force_multirank(self, on=True):
+        """Test hook: the multi-rank path (split, two-phase factorization, every collective) with
+        one rank, so set_comm(0, 1, uid) makes a one-rank RCCL communicator on a one-GPU box."""
+        _check(lib().arslam_lm_debug_force_multirank(self._h, 1 if on else 0))
+
     def set_comm(self, rank, nranks, uid):
         """Join the ranks' exchange: ``uid`` is an RCCL unique id (bytes, one GPU per
         rank) or a host all-reduce ``fn(array, op)`` reducing a numpy array in place
@@ -380,8 +386,10 @@ class ResidentProblem(_Handle):
     """SoA problem uploaded once to HBM; ``solve()`` restarts from the loaded state."""
 
     def __init__(self, camera, cap, tag, obs_cap, obs_tag, corners, camera_const=False,
-                 cap_const=None, tag_const=None, comm=None, **opts):
+                 cap_const=None, tag_const=None, comm=None, force_multirank=False, **opts):
         super().__init__(**opts)
+        if force_multirank:
+            self.debug_force_multirank(True)
         if comm is not None:
             self.set_comm(*comm)
         self.A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners, camera_const, cap_const, tag_const)

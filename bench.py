@@ -363,6 +363,9 @@ def main():
     ap.add_argument("--no-localize", action="store_true", help="skip the cfg5 batched-localize side key")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--rccl-one-rank", action="store_true",
+                    help="(debug, one GPU) the multi-rank path with one rank over a one-rank RCCL communicator "
+                         "made through torch.distributed's nccl group: every collective of a multi-rank solve runs")
     ap.add_argument("--transport", choices=("rccl", "callback"), default="rccl",
                     help="multi-rank exchange: RCCL (one GPU per rank) or the host all-reduce callback over gloo "
                          "(test transport: every rank on the one GPU there is)")
@@ -397,9 +400,14 @@ def main():
     if callback:   # every rank on the one GPU there is (device_count does not initialise HIP here)
         device = local_rank % max(1, torch.cuda.device_count())
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    elif world > 1:
+    elif world > 1 or args.rccl_one_rank:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if world == 1:   # (--rccl-one-rank: a one-rank group, the same init and broadcast as N ranks)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     if args.config == "cfg5":
         bench_localize(args, world, rank)
@@ -416,7 +424,7 @@ def main():
         def allreduce(a, op):
             dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
         comm = (rank, world, allreduce)
-    elif world > 1:
+    elif world > 1 or args.rccl_one_rank:
         obj = [lm.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = (rank, world, obj[0])
@@ -437,7 +445,7 @@ def main():
     runtime_init_s = None if args.no_runtime_warmup else lm.warm_up(device)
     torch.cuda.synchronize()
     t_setup = time.perf_counter()
-    rp = lm.ResidentProblem(**part, comm=comm, phase_timing=0, **opts)
+    rp = lm.ResidentProblem(**part, comm=comm, phase_timing=0, force_multirank=args.rccl_one_rank, **opts)
     setup_wall_s = time.perf_counter() - t_setup
 
     def barrier():
@@ -545,7 +553,8 @@ def main():
                           active_ranks=last["n_active_ranks"]),
             "transport": ("host all-reduce callback over gloo, ranks sharing cuda:" + str(device) +
                           " (test transport: no scaling measurement)") if callback else
-                         ("RCCL, one GPU per rank" if world > 1 else None),
+                         ("RCCL, one GPU per rank" if world > 1 else
+                          "RCCL, one-rank communicator, multi-rank path forced (debug)" if args.rccl_one_rank else None),
             "phase_ms_per_solve": {k: phased[f"t_{k}_ms"] for k in
                                    ("linearize", "schur", "cholesky", "solve", "backsub", "cost")},
             "roofline": roofline,
@@ -573,7 +582,7 @@ def main():
             if args.config == "cfg3":   # plus the reference's own setting (Ceres num_threads = 1) on cfg2
                 out["cpu_baseline_cfg2_1_thread"] = cpu_baseline(synth.config_graph("cfg2"), 1, "cfg2")
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or args.rccl_one_rank:
         dist.destroy_process_group()
 
 

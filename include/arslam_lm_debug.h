@@ -81,6 +81,14 @@ int arslam_debug_schur_stamps(unsigned long long out[16]);
  * to repair. */
 int arslam_lm_debug_force_indefinite(arslam_lm *h, unsigned long long step_mask);
 int arslam_lm_debug_break_dependency(arslam_lm *h, long ticket, long *broken);
+/* force_multirank: on = 1 makes the handle take the multi-rank path with one
+ * rank -- the subtree split (the two-rank split's replicated top, everything
+ * below it this rank's), the two-phase factorization and every collective of
+ * a multi-rank solve -- so that arslam_lm_set_comm(h, 0, 1, id) creates a
+ * one-rank RCCL communicator and the solver issues its real ncclAllReduce
+ * calls (f64 SUM / MAX, u8 MAX) on its stream on a one-GPU box.  Resets the
+ * communicator (set it again after this call); 0 restores the one-rank path. */
+int arslam_lm_debug_force_multirank(arslam_lm *h, int on);
 /* tag_pair_tile: on a pointer-keyed problem loaded with capture elimination
  * on one rank, where the coupling of tag blocks a and b (and the pair's
  * mirror) falls in the reduced system: *status = 2 a tile assembled at the

@@ -201,3 +201,73 @@ def test_bench_launches_its_ranks():
     assert d["n_gpus"] == 2 and d["split"]["n_ranks"] == 2 and 1 <= d["split"]["active_ranks"] <= 2, d["split"]
     assert d["value"] > 0 and d["termination"].startswith("CONVERGENCE"), d
     assert "callback" in d["transport"], d["transport"]
+
+
+def _one_rank_worker(name, q):
+    """One process: the plain one-rank solve, then the forced multi-rank path on one rank through
+    the host callback (identity all-reduce) and through a one-rank RCCL communicator."""
+    try:
+        from ar_slam_amd import lm, synth
+        g = synth.config_graph(name)
+        part = dict(camera=g.camera, cap=g.cap, tag=g.tag, obs_cap=g.obs_cap, obs_tag=g.obs_tag,
+                    corners=g.corners)
+        out = {}
+        for mode in ("plain", "callback", "rccl"):
+            comm = None
+            if mode == "callback":
+                comm = (0, 1, lambda a, op: None)   # one rank: the all-reduce is the identity
+            elif mode == "rccl":
+                comm = (0, 1, lm.comm_unique_id())
+            rp = lm.ResidentProblem(**part, comm=comm, force_multirank=mode != "plain", device=0)
+            s = rp.solve()
+            out[mode] = (rp.camera.copy(), rp.cap.copy(), rp.tag.copy(), [it["cost"] for it in s["iterations"]],
+                         [it["trust_region_radius"] for it in s["iterations"]], s["termination"], s["rule"],
+                         s["comm_calls"], s["comm_bytes"], s["n_top_tiles"], s["n_ranks"])
+            rp.close()
+        q.put(out)
+    except Exception as e:   # noqa: BLE001 -- surface the failure in the parent
+        q.put(repr(e))
+
+
+def test_one_rank_rccl_path_runs_the_real_collectives():
+    """RCCL on hardware with one GPU: arslam_lm_debug_force_multirank makes the
+    handle take the multi-rank path with one rank -- the two-rank split's replicated top, the
+    two-phase factorization, the top-tile all-reduce, the all-gathered step scalars, the u8 MAX
+    flags, the split-hash check and the final tag gather -- and arslam_lm_set_comm(0, 1, id) then
+    runs ncclCommInitRank(nranks = 1) and every ncclAllReduce on the solver's stream.  A one-rank
+    all-reduce is the identity, so the RCCL solve is bit-identical to the same path through the host
+    callback; both agree with the plain one-rank solve to rounding (the two-phase factorization sums
+    a top tile's updates subtree-first, so the last bits may differ) and match it pose for pose."""
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_one_rank_worker, args=("cfg2", q))
+    p.start()
+    try:
+        out = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert isinstance(out, dict), out
+    plain, cb, rc = out["plain"], out["callback"], out["rccl"]
+    # the transport is all that differs: bit-identical
+    for a, b in zip(cb[:5], rc[:5]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    assert cb[5:] == rc[5:]
+    calls, xbytes, top_tiles, nr = rc[7:]
+    assert nr == 1 and calls > 0 and top_tiles > 0 and xbytes >= top_tiles * 32768, rc[7:]
+    assert plain[7] == 0   # the plain path makes no collective
+    # the multi-rank path on one rank against the plain solve
+    assert (rc[5], rc[6]) == (plain[5], plain[6])
+    assert len(rc[3]) == len(plain[3])
+    for a, b in zip(rc[3], plain[3]):
+        assert abs(a - b) <= 1e-9 * abs(b), (rc[3], plain[3])
+    np.testing.assert_allclose(rc[4], plain[4], rtol=1e-9)
+    assert abs(rc[0][0] - plain[0][0]) <= 1e-8 * plain[0][0]
+    assert_poses_match(rc[1], rc[2], plain[1], plain[2])
+    same = all(np.array_equal(np.asarray(a), np.asarray(b)) for a, b in zip(rc[:4], plain[:4]))
+    print(f"one-rank RCCL path: {calls} collectives, {xbytes / 1e6:.2f} MB, {top_tiles} top tiles; "
+          f"bit-identical to the plain solve: {same}")
