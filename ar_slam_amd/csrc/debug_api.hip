@@ -186,6 +186,11 @@ int simulate_all(const arslam::LltPlan &plan) {
     for (int pol = 0; pol < arslam::kDagSimPolicies; ++pol)
       for (unsigned seed = 1; seed <= (pol == 0 || pol == 3 ? 3u : 1u); ++seed)
         if (!arslam::dag_simulate(plan, wk, seed, pol)) return -(wk * 16 + pol);
+  // a 448-workgroup grid of which only k ever become resident (a GPU shared
+  // with another process, or several ranks' launches on one GPU)
+  for (int k : {1, 2, 7, 64})
+    for (int pol = 0; pol < arslam::kDagSimPolicies; ++pol)
+      if (!arslam::dag_simulate(plan, 448, 1u, pol, k)) return -(100000 * k + 448 * 16 + pol);
   return 1;
 }
 }  // namespace
@@ -279,6 +284,24 @@ extern "C" int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_work
   } catch (...) {
     return ARSLAM_E_INVALID_ARG;
   }
+}
+
+extern "C" int arslam_debug_dag_simulate_started(const arslam_soa_problem *p, int n_workers, int n_started,
+                                                 unsigned seed, int policy, int *ok) {
+  if (!p || !ok || n_workers < 1 || n_started < 0 || policy < 0) return ARSLAM_E_INVALID_ARG;
+  try {
+    *ok = arslam::dag_simulate(one_rank_plan(p), n_workers, seed, policy, n_started) ? 1 : 0;
+    return ARSLAM_OK;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}
+
+extern "C" int arslam_debug_dag_workgroup_limit(int k) {
+  arslam::set_dag_workgroup_limit(k);
+  return ARSLAM_OK;
 }
 
 extern "C" int arslam_debug_dag_fault_detail(const arslam_soa_problem *p, const int rec[9], char *buf, int len) {

@@ -766,11 +766,25 @@ __device__ __forceinline__ unsigned long long wait_clock() {
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
-// true once the wait that started at t0 has lasted kWaitCapTicks (checked on
-// every 16th poll) or kSpinCap polls
-__device__ __forceinline__ bool wait_expired(long spins, unsigned long long t0) {
-  return spins > kSpinCap || ((spins & 15) == 0 && wait_clock() - t0 > kWaitCapTicks);
-}
+// The time a wait has been *running*: the clock is read every 16th poll and
+// each interval counts at most kGapTicks (1 ms; 16 polls take microseconds),
+// so a wave descheduled by preemption (the hardware saves the whole dispatch's
+// waves and restores them later) does not count the time it was off the
+// machine, and a producer preempted with it is not reported as stuck.
+constexpr unsigned long long kGapTicks = 100000ull;   // 1 ms at 100 MHz
+struct WaitTimer {
+  unsigned long long last, run = 0;
+  __device__ __forceinline__ WaitTimer() : last(wait_clock()) {}
+  // true once the wait has run kWaitCapTicks (checked on every 16th poll) or kSpinCap polls
+  __device__ __forceinline__ bool expired(long spins) {
+    if (spins > kSpinCap) return true;
+    if ((spins & 15) != 0) return false;
+    const unsigned long long now = wait_clock(), d = now - last;
+    last = now;
+    run += d < kGapTicks ? d : kGapTicks;
+    return run > kWaitCapTicks;
+  }
+};
 // s_sleep units (64 cycles) between two polls of a dependency counter.  Every
 // poll is a device-scope atomic performed at the memory side; with a few
 // hundred update tasks waiting at once, polling every 64 cycles slowed the
@@ -1069,7 +1083,7 @@ __device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *
     const bool mine = w < w1;
     const int2 cv = mine ? waits[w] : make_int2(0, 0);
     long spins = 0;
-    const unsigned long long t0 = wait_clock();
+    WaitTimer tm;
     for (;;) {
       // (every lane re-polls each round: no loop-carried per-lane state)
       const int got = mine ? ld_acquire_relaxed(counters + cv.x) : 0;
@@ -1077,7 +1091,7 @@ __device__ bool dag_wait(int *counters, const int2 *waits, int w0, int w1, int *
       if (m == 0) break;
       if (chain) __builtin_amdgcn_s_sleep(kChainSleep);
       else __builtin_amdgcn_s_sleep(kPollSleep);
-      const bool exp = wait_expired(++spins, t0);
+      const bool exp = tm.expired(++spins);
       const bool give_up = exp || ((spins & 255) == 0 && __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) < 0);
       if (give_up) {
         *expired = exp;
@@ -1179,6 +1193,8 @@ struct DagArgs {
   // never clears them, and their first update stores 0 - acc instead of
   // reading the tile (INT_MAX: every tile is cleared and read-modify-written)
   int first_store;
+  int *started;               // workgroups of this launch that have started (the claim cap's base)
+  int wg_limit;               // debug: workgroups with blockIdx.x >= wg_limit return at once (INT_MAX: none)
 };
 
 // A ticket's 32-int record: two scalar loads in flight, one wait (the record
@@ -1235,8 +1251,18 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
   // EARLY waits are all drawn; its late waits may name undrawn tickets, so at
   // most half the grid may hold claimed targets: the other workgroups can
   // always draw the lowest unfinished ticket, whose producers are all done.
+  //
+  // "Half the grid" is not enough when fewer workgroups than the grid are
+  // resident (another process on the GPU, several ranks sharing one): every
+  // resident workgroup could then hold a claimed target while the ones that
+  // would draw never start.  So the cap is half the workgroups that have
+  // *started* (counted on entry, read at each claim): a started workgroup
+  // stays resident until every ticket is drawn, so at least half of the
+  // started ones hold no claimed target and can draw the lowest unfinished
+  // ticket (dag_simulate's started-k schedules).
   int *inflight = a.counters + 2 * a.n_tiles + kDagOffInflight;
-  const int cont_cap = (int)(gridDim.x / 2);
+  if ((int)blockIdx.x >= a.wg_limit) return;   // (debug: only wg_limit workgroups ever start)
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(a.started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // Per-CU "POTRF running" flags (performance only: a wrong or stale flag
   // costs a bounded pause, never a result).  The 64x64 POTRF is a chain of
   // dependent LDS/VALU steps on one wave; the other workgroup on its CU runs
@@ -1539,9 +1565,10 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         // stores (its target's early waits were polled beside the last POTRF
         // panel, sh[20..21]: a claimed target whose waits were seen met skips
         // its own poll).
-        int tk_seen = 0, infl_old = 0;
+        int tk_seen = 0, infl_old = 0, started_seen = 0;
         if (c >= 0 && tid == 0) {
           tk_seen = ld_acquire_relaxed(ticket);
+          started_seen = ld_acquire_relaxed(a.started);
           infl_old = atomicAdd(inflight, 1);
         }
         if (!pref) load_tile_wt(Ct, X, tid);
@@ -1559,7 +1586,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         // claim the continuation target before the tile is published: its
         // drawer waits for this tile, so it cannot have claimed it yet.  (The
         // CAS goes out here and is answered beside the last two steps.)
-        const bool want = c >= 0 && tid == 0 && a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < cont_cap;
+        const bool want = c >= 0 && tid == 0 && a.t_begin + tk_seen > r[kRecContMaxdep] && infl_old < started_seen / 2;
         int cas_old = 1;
         if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
         for (int st = max(s0, 2); st < 4; ++st) trsm_step(X, D, LTd, w, st, lane);
@@ -1718,10 +1745,10 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         if (tid == 0) {
           long spins = 0;
           int seen;
-          const unsigned long long t0 = wait_clock();
+          WaitTimer tm;
           while ((seen = ld_acquire_relaxed(applied + task.w)) < task.z) {
             __builtin_amdgcn_s_sleep(kPollSleep);
-            const bool exp = wait_expired(++spins, t0);
+            const bool exp = tm.expired(++spins);
             if (exp || (((spins & 255) == 0) && ld_acquire_relaxed(a.flag) < 0)) {
               dag_fault(a.flag, a.counters, a.n_tiles, ticket, 2, t, make_int3(a.n_tiles + task.w, seen, task.z), exp);
               break;
@@ -1901,7 +1928,7 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
         double yv = 0.0;
         bool mine = ri + lane < nR;
         long spins = 0;
-        const unsigned long long t0 = wait_clock();
+        WaitTimer tm;
         for (;;) {
           if (mine) {
             yv = ld_wt(yF + ri + lane);
@@ -1909,7 +1936,7 @@ __global__ __launch_bounds__(256) void k_bsolve_dag(const double *__restrict__ S
           }
           if (__builtin_amdgcn_ballot_w64(mine) == 0) break;
           __builtin_amdgcn_s_sleep(kBsolveSleep);
-          if (wait_expired(++spins, t0) || (((spins & 255) == 0) &&
+          if (tm.expired(++spins) || (((spins & 255) == 0) &&
                                      __builtin_amdgcn_readfirstlane(ld_acquire_relaxed(flag)) != 0)) {
             if (lane == 0) atomicCAS(flag, 0, -(4000000 + b));
             ok = false;
@@ -2037,6 +2064,9 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s, Lau
   }
 }
 
+static int g_dag_wg_limit = INT_MAX;   // debug (arslam_debug_dag_workgroup_limit), process-wide
+void set_dag_workgroup_limit(int k) { g_dag_wg_limit = k > 0 ? k : INT_MAX; }
+
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups, int *progress,
                           unsigned long long *trace, bool reset, int phase, long first_store) {
   const int t_begin = phase == 1 ? (int)P.phase_split : 0;
@@ -2050,7 +2080,8 @@ void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s,
   DagArgs a{S, P.T, P.ldiag, P.ldiag + 2L * P.T * T64 * T64, P.dag_rec, P.dag_ks_tiles, P.upd_ks, P.dag_claimed,
             P.dag_waits, P.dag_counters, (int)P.n_tiles, (int)P.n_dag_tasks, P.upd_part, P.upd_cnt, flag, t_begin, t_end,
             P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagOffTicket1 : kDagOffTicket0), progress, trace,
-            (int)std::min<long>(first_store, INT_MAX)};
+            (int)std::min<long>(first_store, INT_MAX),
+            P.dag_counters + 2 * P.n_tiles + (phase == 1 ? kDagOffStarted1 : kDagOffStarted0), g_dag_wg_limit};
   // A small task graph runs on fewer workgroups (a quarter of its tasks, at
   // least 64): its time is the elimination tree's chain, which runs faster
   // beside fewer co-resident update workgroups (cfg2, 580 tasks: 219.6 us on

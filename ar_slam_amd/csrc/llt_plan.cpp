@@ -874,8 +874,12 @@ bool dag_check(const LltPlan &plan) {
 //   3  draws first, then random.
 // policy | kDagSimNoCap (tests only) drops the in-flight cap on claimed
 // targets, which the protocol needs: the simulation must then find deadlocks.
-bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy) {
-  const bool no_cap = (policy & kDagSimNoCap) != 0;
+// n_started >= 0: only that many workgroups ever start (the rest of the grid is
+// never resident), each starting when the schedule picks it; the cap is half
+// the workgroups started so far (k_factor_dag), or half the grid under
+// policy | kDagSimGridCap (round 5's protocol, which these schedules break).
+bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy, int n_started) {
+  const bool no_cap = (policy & kDagSimNoCap) != 0, grid_cap = (policy & kDagSimGridCap) != 0;
   policy &= kDagSimNoCap - 1;
   const long nt = plan.n_tiles, n = plan.n_dag_tasks;
   std::vector<int> cnt(2 * nt + 1, 0), arrived(plan.h_split.size(), 0);
@@ -883,10 +887,16 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy)
   auto maxdep = [&](long t) { return has_cont ? plan.h_dag_maxdep[t] : -1; };
   std::vector<char> claimed(n, 0);
   enum { DRAW = 0, EARLY = 1, APPLY = 2, LATE = 3 };
-  struct W { long t = -1; int phase = DRAW; long next = -1; bool cont = false; };
-  std::vector<W> ws(n_workers);
+  struct W { long t = -1; int phase = DRAW; long next = -1; bool cont = false; bool up = true; };
+  const int n_res = n_started < 0 ? n_workers : std::min(n_started, n_workers);
+  std::vector<W> ws(n_res);
+  int started = n_res;
+  if (n_started >= 0) {
+    started = 0;
+    for (W &w : ws) w.up = false;
+  }
   long ticket = 0, finished = 0;
-  int inflight = 0;   // claimed continuations running: at most n_workers / 2 (as k_factor_dag)
+  int inflight = 0;   // claimed continuations running: at most started / 2 (as k_factor_dag)
   unsigned rng = seed ? seed : 1u;
   auto rnd = [&]() { rng = rng * 1664525u + 1013904223u; return rng >> 8; };
   auto met = [&](int q0, int q1) {
@@ -896,6 +906,7 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy)
   };
   auto early_end = [&](long t) { return plan.h_dag_sub[t].x >= 0 ? plan.h_dag_sub[t].y : plan.h_dag_wait_off[t + 1]; };
   auto movable = [&](const W &w) {
+    if (!w.up) return true;   // (start)
     switch (w.phase) {
       case DRAW: return w.next >= 0 || ticket < n;
       case EARLY: return met(plan.h_dag_wait_off[w.t], early_end(w.t));
@@ -907,7 +918,8 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy)
     ++finished;
     const int c = has_cont ? plan.h_dag_cont[w.t] : -1;
     w.next = -1;
-    if (c >= 0 && ticket > maxdep(c) && !claimed[c] && (no_cap || inflight < n_workers / 2)) {
+    const int cap = grid_cap ? n_workers / 2 : started / 2;
+    if (c >= 0 && ticket > maxdep(c) && !claimed[c] && (no_cap || inflight < cap)) {
       claimed[c] = 1;
       w.next = c;
       ++inflight;
@@ -916,6 +928,11 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy)
     w.phase = DRAW;
   };
   auto move = [&](W &w) {
+    if (!w.up) {
+      w.up = true;
+      ++started;
+      return;
+    }
     if (w.phase == DRAW) {
       if (w.next >= 0) {
         w.t = w.next;
@@ -962,7 +979,7 @@ bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy)
   while (finished < n) {
     cand.clear();
     bool draw = false;
-    for (int m = 0; m < n_workers; ++m)
+    for (int m = 0; m < n_res; ++m)
       if (movable(ws[m])) {
         if (policy != 0 && ws[m].phase == DRAW && !draw) {   // draws first: keep only draws
           draw = true;

@@ -41,7 +41,11 @@ enum DagFaultField {
   kFaultFirstStuck = 8,   // INT_MAX - the smallest ticket whose wait ran out of time (0: none)
   kDagFaultSlots = 9
 };
-constexpr int kDagCounterExtra = kDagOffFault + kDagFaultSlots;
+// workgroups of the phase-0 / phase-1 launch that have started (k_factor_dag's
+// claim cap is half of these, not half the grid: DESIGN §8b)
+constexpr int kDagOffStarted0 = kDagOffFault + kDagFaultSlots;
+constexpr int kDagOffStarted1 = kDagOffStarted0 + 1;
+constexpr int kDagCounterExtra = kDagOffStarted1 + 1;
 // k_factor_dag workgroups resident per CU (its launch bounds; 73 KB of LDS
 // each): a launch never asks for more than this times the CU count
 constexpr int kDagWorkgroupsPerCu = 2;
@@ -300,9 +304,12 @@ bool dag_check(const LltPlan &plan);
 // Randomised (policy 0) or adversarial interleavings of n_workers workgroups
 // running k_factor_dag's protocol; false on a reachable deadlock (dag_simulate
 // in llt_plan.cpp lists the policies).
-bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy = 0);
+// n_started >= 0: only that many of the n_workers workgroups ever start, one
+// at a time as the schedule picks them (fewer resident than the grid).
+bool dag_simulate(const LltPlan &plan, int n_workers, unsigned seed, int policy = 0, int n_started = -1);
 constexpr int kDagSimPolicies = 4;
 constexpr int kDagSimNoCap = 16;
+constexpr int kDagSimGridCap = 32;   // (tests) round 5's cap: half the grid, not half the started workgroups
 // The fault record of a timed-out executor wait (kDagFault*) in words: the
 // stuck task, the awaited counter, its producers and how far the launch drew.
 std::string dag_fault_detail(const LltPlan &plan, const int *rec);
@@ -444,6 +451,9 @@ void launch_dense_llt(const LltPlan &P, double *S, int *flag, hipStream_t s,
 // (first_store: the tiles from first_store on are fill tiles the Schur gather
 // does not write and S is not cleared for -- their first update stores
 // instead of reading the tile; LONG_MAX: none)
+// debug: only the first k workgroups of every k_factor_dag launch start (the
+// others return at once; k <= 0 restores all), process-wide
+void set_dag_workgroup_limit(int k);
 void launch_dense_llt_dag(const LltPlan &P, double *S, int *flag, hipStream_t s, int n_workgroups,
                           int *progress = nullptr, unsigned long long *trace = nullptr, bool reset = true,
                           int phase = -1, long first_store = LONG_MAX);

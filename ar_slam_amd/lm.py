@@ -49,7 +49,8 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_lm_debug_force_multirank", "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
            "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
            "arslam_debug_mixed_groups",
-           "arslam_debug_dag_simulate", "arslam_debug_dag_fault_detail", "arslam_debug_box_fingerprint",
+           "arslam_debug_dag_simulate", "arslam_debug_dag_simulate_started", "arslam_debug_dag_workgroup_limit",
+           "arslam_debug_dag_fault_detail", "arslam_debug_box_fingerprint",
            "arslam_debug_rank_split", "arslam_debug_gather_extend",
            "arslam_localize_many", "arslam_localizer_create", "arslam_localizer_destroy",
            "arslam_localizer_load", "arslam_localizer_solve",
@@ -226,6 +227,7 @@ def lib():
     L.arslam_debug_mixed_groups.argtypes = [C.POINTER(SoaProblem), _ip, C.POINTER(C.c_ubyte), C.POINTER(C.c_ubyte)]
     L.arslam_lm_debug_force_indefinite.argtypes = [C.c_void_p, C.c_ulonglong]
     L.arslam_lm_debug_force_multirank.argtypes = [C.c_void_p, C.c_int]
+    L.arslam_debug_dag_workgroup_limit.argtypes = [C.c_int]
     L.arslam_lm_set_iteration_callback.argtypes = [C.c_void_p, ITER_CB, C.c_void_p]
     L.arslam_lm_debug_break_dependency.argtypes = [C.c_void_p, C.c_long, C.POINTER(C.c_long)]
     if hasattr(L, "arslam_lm_debug_tag_pair_tile"):   # (absent from older variant builds under A/B)
@@ -545,14 +547,26 @@ def box_fingerprint(device=0):
             "pingpong_ns": out[3], "pingpong_xcc": [int(out[4]), int(out[5])]}
 
 
-def debug_dag_simulate(g, n_workers, seed=1, policy=0):
+def debug_dag_simulate(g, n_workers, seed=1, policy=0, started=None):
     """Host-only: one simulated interleaving of the persistent executor's protocol on g's one-rank
-    plan (policy 0 random, 1-3 adversarial; + 16 without the in-flight cap on claimed targets).
-    True if every task finished, False on a deadlock."""
+    plan (policy 0 random, 1-3 adversarial; + 16 without the in-flight cap on claimed targets;
+    + 32 with round 5's cap, half the grid).  started=k: only k of the n_workers workgroups ever
+    start.  True if every task finished, False on a deadlock."""
     A = _Soa(g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag, g.corners)
     ok = C.c_int(-1)
-    _check(lib().arslam_debug_dag_simulate(C.byref(A.s), int(n_workers), C.c_uint(seed), int(policy), C.byref(ok)))
+    if started is None:
+        _check(lib().arslam_debug_dag_simulate(C.byref(A.s), int(n_workers), C.c_uint(seed), int(policy),
+                                               C.byref(ok)))
+    else:
+        _check(lib().arslam_debug_dag_simulate_started(C.byref(A.s), int(n_workers), int(started), C.c_uint(seed),
+                                                       int(policy), C.byref(ok)))
     return bool(ok.value)
+
+
+def debug_dag_workgroup_limit(k):
+    """Process-wide test knob: later k_factor_dag launches let only their first k workgroups start
+    (as if only k were resident); k <= 0 restores the whole grid."""
+    _check(lib().arslam_debug_dag_workgroup_limit(int(k)))
 
 
 def debug_dag_fault_detail(g, rec):

@@ -118,6 +118,18 @@ int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int ski
  * flight, which the protocol relies on).  *ok = 1 if every task finished, 0 on
  * a deadlock. */
 int arslam_debug_dag_simulate(const arslam_soa_problem *p, int n_workers, unsigned seed, int policy, int *ok);
+/* The same with only n_started of the grid's n_workers workgroups ever
+ * starting (each when the schedule picks it): fewer workgroups resident than
+ * the grid.  The executor caps claimed continuations at half the workgroups
+ * started so far; policy + 32 simulates round 5's cap (half the grid), which
+ * such schedules deadlock. */
+int arslam_debug_dag_simulate_started(const arslam_soa_problem *p, int n_workers, int n_started, unsigned seed,
+                                      int policy, int *ok);
+/* Process-wide: every later k_factor_dag launch lets only its first k
+ * workgroups start (the others return at once), as if only k were resident;
+ * k <= 0 restores the whole grid.  The factorization's result does not depend
+ * on it (fixed summation order). */
+int arslam_debug_dag_workgroup_limit(int k);
 
 /* Host only: the message an executor fault carries for the one-rank plan of p
  * (nested dissection, sparse tiles) and a fault record rec[9] = {ticket, kind

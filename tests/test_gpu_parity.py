@@ -421,6 +421,25 @@ def test_executor_grid_size_does_not_change_the_result(lm, monkeypatch):
         assert np.array_equal(t2, tag) and np.array_equal(p2, cap) and np.array_equal(c2, cam), grid
 
 
+@pytest.mark.parametrize("name", ["cfg2", "cfg3"])
+def test_factorization_completes_with_few_resident_workgroups(lm, name):
+    """Progress independent of residency: the launch keeps its full grid (448
+    workgroups on cfg3) but only the first k workgroups ever start -- the rest return at once, as
+    when another process or other ranks hold the GPU.  The claim cap is half the workgroups that
+    have started (k = 1: no claims; 2: one; 7: three), so every factorization finishes, and the
+    fixed summation order makes the solve bit-identical to the whole grid's."""
+    g = synth.config_graph(name)
+    cam, cap, tag, ref = lm.solve_graph(g)
+    try:
+        for k in (1, 2, 7):
+            lm.debug_dag_workgroup_limit(k)
+            c2, p2, t2, s = lm.solve_graph(g)
+            assert [i["cost"] for i in s["iterations"]] == [i["cost"] for i in ref["iterations"]], k
+            assert np.array_equal(t2, tag) and np.array_equal(p2, cap) and np.array_equal(c2, cam), k
+    finally:
+        lm.debug_dag_workgroup_limit(0)
+
+
 @pytest.mark.parametrize("side", ["captures", "tags", "auto"])
 @pytest.mark.parametrize("name", ["kvar", "k24", "wall"])
 def test_large_captures_match_oracle(lm, oracle, name, side):

@@ -229,3 +229,18 @@ def test_fault_record_names_the_stuck_counter_and_its_producers(L):
     assert s3.endswith("smallest ticket timed out: 2205 (POTRF 69+TRSM)"), s3
     s2 = L.debug_dag_fault_detail(g, [2772, 1, 12625 * 0 + 2461 + 1620, 1, 2, 3000, 3, 17])
     assert "applied[1620] = 1 < 2" in s2 and "ticket 1981" in s2 and "ticket 2355" in s2, s2
+
+
+@pytest.mark.parametrize("name", ["small", "medium", "cfg2"])
+def test_claim_cap_follows_started_workgroups(L, name):
+    """Progress independent of residency.  A 448-workgroup grid of which only
+    k ever become resident: round 5's cap (half the grid) lets every resident workgroup hold a
+    claimed continuation whose late waits name tickets nobody is left to draw -- the simulation
+    finds that deadlock at k = 1; the kernel's cap (half the workgroups started so far) finishes
+    every schedule at k = 1, 2, 7 and 64."""
+    g = synth.config_graph(name)
+    GRID_CAP = 32
+    assert not any(L.debug_dag_simulate(g, 448, seed=1, policy=pol + GRID_CAP, started=1) for pol in range(4))
+    for k in (1, 2, 7, 64):
+        for pol in range(4):
+            assert L.debug_dag_simulate(g, 448, seed=3, policy=pol, started=k), (k, pol)
