@@ -156,18 +156,33 @@ __device__ __forceinline__ double bcast16(double v, int l) {
   }
 }
 
-// One wave: C(16x16) -= A(16 x K) B(16 x K)^T, operands in LDS (pitch LQ).
+// One wave: C(16x16) -= A(16 x K) B(16 x K)^T, operands in LDS (pitch LQ;
+// C never overlaps A or B).  C's four entries per lane are read before the
+// MFMA chain: read after it, hipcc issued each read-subtract-write as its own
+// LDS round trip (four in a row, ~300 cycles on the POTRF's chain per call).
 __device__ __forceinline__ void wave_gemm16_sub(double *C, const double *A, const double *B, int K,
                                                 int lane) {
   const int li = lane & 15, lk = lane >> 4;
+  double c[4];
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) c[reg] = C[(lk + 4 * reg) * LQ + li];
   dbl4 acc = {0, 0, 0, 0};
+#ifdef ARSLAM_GEMM_PF
+  if (K == 64 && A == B) {   // (variant) the fold: every operand read before the chain
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a[q] = A[li * LQ + 4 * q + lk];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], a[q], acc, 0, 0, 0);
+  } else
+#endif
   for (int k4 = 0; k4 < K; k4 += 4) {
     const double a = A[li * LQ + k4 + lk];
     const double b = B[li * LQ + k4 + lk];
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
   }
 #pragma unroll
-  for (int reg = 0; reg < 4; ++reg) C[(lk + 4 * reg) * LQ + li] -= acc[reg];
+  for (int reg = 0; reg < 4; ++reg) C[(lk + 4 * reg) * LQ + li] = c[reg] - acc[reg];
 }
 
 constexpr int LI = 18;   // LDS pitch of the 16x16 inverse diagonal blocks (conflict-free fragments)
@@ -320,7 +335,15 @@ __device__ __forceinline__ void diag16(double *D, int b0, double *inv, double *L
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const double piv = colx[i];
   if (!(piv > 0.0)) *bad = 1;
+#ifdef ARSLAM_D16_RSQ
+  // (variant) 1 / sqrt(piv) by v_rsq_f64 and two Newton steps, d = piv / sqrt(piv)
+  double rd = __builtin_amdgcn_rsq(piv);
+  rd = rd * __builtin_fma(-0.5 * piv * rd, rd, 1.5);
+  rd = rd * __builtin_fma(-0.5 * piv * rd, rd, 1.5);
+  const double d = piv * rd;
+#else
   const double d = sqrt(piv), rd = 1.0 / d;
+#endif
   // lane (g, i), column c = 4g+q:  L_{c,i} = U_i[c] / d_i (c > i),
   // (L^{-1})_{i,c} = Lu^{-1}_i[c] / d_i (c < i)
 #pragma unroll
@@ -425,26 +448,65 @@ __device__ __forceinline__ void lds_wait(const int *f, int v) {
 // fl[2] = update rounds done by waves 1-3 (round 0 the fold, round p+1 panel
 // p's trailing updates; three increments per round).  idle(p, w, lane) runs
 // on waves 1-3 after round p (as beside panel p in the barrier version).
+//
+// With the fold, wave 0's first apply and lookahead need only blocks (1, 0)
+// and (1, 1) folded -- the first blocks waves 1 and 2 fold -- not the whole
+// round 0 (wave 3's third block made wave 0 wait ~500 cycles after diag16(0)):
+// those two count in *fcnt, and waves 1-3 await the complete round 0
+// themselves before their first applies.
 template <class Idle>
 __device__ bool blocked_potrf64_async(double *D, double *inv, double *LTd, int *bad, int *fl, int tid,
-                                      double *colx, Idle &&idle, const double *F = nullptr, bool fold = false) {
+                                      double *colx, Idle &&idle, const double *F = nullptr, bool fold = false,
+                                      int *fcnt = nullptr) {
   const int w = tid >> 6, lane = tid & 63;
+  const bool early = fold && fcnt;
   if (tid == 0) {
     *bad = 0;
     fl[0] = fl[1] = fl[2] = fl[3] = 0;   // (fl[3]: the caller's prefetch count)
+    if (fcnt) *fcnt = 0;
   }
   __syncthreads();
   if (w == 0) {
+    STAMP(30);
     for (int p = 0; p < 4; ++p) {
       const int b0 = 16 * p;
       if (p == 0 && fold) wave_gemm16_sub(D, F, F, 64, lane);
-      if (p > 0) wave_gemm16_sub(D + b0 * LQ + b0, D + b0 * LQ + b0 - 16, D + b0 * LQ + b0 - 16, 16, lane);
-      if (p > 0) lds_wait(fl + 2, 3 * p);   // rounds 0 .. p-1: the fold and panels 0 .. p-2
+      // (p > 0: block (p, p) had panel p-1's lookahead update at the end of
+      // iteration p-1, and rounds 0 .. p-1 were awaited there)
+      STAMP(31 + 6 * p);
+      STAMP(32 + 6 * p);
       diag16(D, b0, inv, LTd + p * 16 * LI, bad, lane, colx);
+      STAMP(33 + 6 * p);
       if (p < 3) {
-        lds_wait(fl + 2, 3 * (p + 1));      // round p: block (p+1, p) has panel p-1's update
-        wave_apply_inv16(D + (b0 + 16) * LQ + b0, LTd + p * 16 * LI, lane);
+        if (p == 0 && early) lds_wait(fcnt, 2);   // blocks (1, 0) and (1, 1) folded
+        else lds_wait(fl + 2, 3 * (p + 1));      // round p: block (p+1, p) has panel p-1's update
+        STAMP(34 + 6 * p);
+        // The block below the diagonal solved transposed, Y = L_pp^{-1} A^T
+        // (the same products as A L_pp^{-T}, operands swapped: bit-identical),
+        // so each lane holds X[i][lk + 4 reg] -- the MFMA operand layout of
+        // X X^T: the next diagonal block's lookahead update runs from the
+        // registers, without reading X back from LDS.
+        const int li = lane & 15, lk = lane >> 4;
+        double *Cb = D + (b0 + 16) * LQ + b0, *Cd = Cb + 16;
+        const double *Linv = LTd + p * 16 * LI;
+        double a[4], cd[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = Cb[li * LQ + 4 * q + lk];
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) cd[reg] = Cd[(lk + 4 * reg) * LQ + li];
+        __builtin_amdgcn_wave_barrier();
+        dbl4 y = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y = __builtin_amdgcn_mfma_f64_16x16x4f64(Linv[li * LI + 4 * q + lk], a[q], y, 0, 0, 0);
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) Cb[li * LQ + lk + 4 * reg] = y[reg];
         lds_set(fl, p + 1);
+        STAMP(35 + 6 * p);
+        dbl4 g = {0, 0, 0, 0};
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) g = __builtin_amdgcn_mfma_f64_16x16x4f64(y[reg], y[reg], g, 0, 0, 0);
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) Cd[(lk + 4 * reg) * LQ + li] = cd[reg] - g[reg];
       }
     }
   } else {
@@ -455,12 +517,14 @@ __device__ bool blocked_potrf64_async(double *D, double *inv, double *LTd, int *
         while ((I + 1) * (I + 2) / 2 <= t) ++I;
         const int C = t - I * (I + 1) / 2;
         wave_gemm16_sub(D + 16 * I * LQ + 16 * C, F + 16 * I * LQ, F + 16 * C * LQ, 64, lane);
+        if (early && t <= 2) lds_add(fcnt, lane);   // (1, 0) by wave 1, (1, 1) by wave 2
       }
     }
     idle(0, w, lane);
     lds_add(fl + 2, lane);
     for (int p = 0; p < 3; ++p) {
       const int b0 = 16 * p;
+      if (p == 0 && early) lds_wait(fl + 2, 3);   // every block folded (wave 0 no longer awaits it)
       lds_wait(fl, p + 1);                  // L_pp's block inverse, block (p+1, p) applied
       if (w < 3 - p - 1 + 1 && p + 1 + w <= 3)   // blocks (p+2 .. 3, p): wave w takes p + 1 + w
         wave_apply_inv16(D + (b0 + 16 * (1 + w)) * LQ + b0, LTd + p * 16 * LI, lane);
@@ -1240,7 +1304,8 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
   // one LDS array carved per task type (POTRF: D, X, inv, LTd; GEMMs: sA, sB)
   __shared__ __attribute__((aligned(16))) double lds[2 * T64 * LQ + T64 + 4 * 16 * LI + 12 + 16 + T64];
   double *D = lds, *X = lds + T64 * LQ, *inv = X + T64 * LQ, *LTd = inv + T64;
-  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [12..15] fused solve steps done,
+  // [0] ticket, [1] bad, [2] ok, [3] last, [4] claimed continuation, [7] the POTRF fold's first blocks done,
+  // [12..15] fused solve steps done,
   // [6] its fetch requested, [8..10] the POTRF pipeline's flags, [11] thirds of that tile loaded,
   // [16..17] the continuation's A_kk halves in D, [20..21] its early waits seen met by waves 2-3
   int *sh = reinterpret_cast<int *>(LTd + 4 * 16 * LI);
@@ -1527,7 +1592,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
             if (wv == kPipeW2) sh[15] = sdone;
           }
         }
-      }, X, fold_in);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
+      }, X, fold_in, sh + 7);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();

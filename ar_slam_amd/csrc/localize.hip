@@ -195,9 +195,54 @@ struct Rows {
 // Residuals and capture-block Jacobian rows at x; wave-reduced cost, J'r,
 // column norms and the 21 upper entries of J'J.  Returns false if a residual
 // is not finite (uniform).
+// Per-query sums of 28 per-lane partials through LDS, instead of 28 butterfly
+// reductions (5 dependent DPP/permlane + add steps each, ~15 VALU
+// instructions per value): every lane writes its partials, lane v < 28 of the
+// query sums value v's LPQ partials by a fixed pairwise tree, and every lane
+// reads the 28 sums back -- the same bits on every lane of the query, so its
+// control flow stays uniform.  red: this query's [28][LPQ + 2] partials
+// (16-byte rows, bank-staggered by the pad) then [28] sums.
+template <int LPQ>
+__device__ __forceinline__ void query_sums28(double *red, int lane, double c, const double (&gl)[6],
+                                             const double (&hl)[21], double &cost, double (&g)[6], double (&H)[21]) {
+  constexpr int P = LPQ + 2;
+  red[lane] = c;
+#pragma unroll
+  for (int e = 0; e < 6; ++e) red[(1 + e) * P + lane] = gl[e];
+#pragma unroll
+  for (int e = 0; e < 21; ++e) red[(7 + e) * P + lane] = hl[e];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < 28) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2 *row = reinterpret_cast<const d2 *>(red + lane * P);
+    // pairwise: groups of 8 partials (three levels each), then the groups' sums
+    double gs[LPQ / 8];
+#pragma unroll
+    for (int gi = 0; gi < LPQ / 8; ++gi) {
+      const d2 a = row[4 * gi], b = row[4 * gi + 1], cc = row[4 * gi + 2], d = row[4 * gi + 3];
+      gs[gi] = ((a.x + a.y) + (b.x + b.y)) + ((cc.x + cc.y) + (d.x + d.y));
+    }
+#pragma unroll
+    for (int n = LPQ / 16; n >= 1; n >>= 1)
+#pragma unroll
+      for (int i = 0; i < n; ++i) gs[i] = gs[2 * i] + gs[2 * i + 1];
+    red[28 * P + lane] = gs[0];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  cost = 0.5 * red[28 * P];
+#pragma unroll
+  for (int e = 0; e < 6; ++e) g[e] = red[28 * P + 1 + e];
+#pragma unroll
+  for (int e = 0; e < 21; ++e) H[e] = red[28 * P + 7 + e];
+}
+
 template <int NCH, int LPQ>
 __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const double *x, int lane,
-                                  Rows<NCH> &rows, double &cost, double g[6], double H[21],
+                                  Rows<NCH> &rows, double &cost, double g[6], double H[21], double *red,
                                   const AngleAxis *ac_pre = nullptr) {
   double c = 0.0, gl[6] = {0, 0, 0, 0, 0, 0}, hl[21];
 #pragma unroll
@@ -237,11 +282,9 @@ __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const do
         for (int b = a; b < 6; ++b) hl[e++] += j6[a] * j6[b];
     }
   }
-  cost = 0.5 * wave_sum<LPQ>(c);
-#pragma unroll
-  for (int j = 0; j < 6; ++j) g[j] = wave_sum<LPQ>(gl[j]);
-#pragma unroll
-  for (int e = 0; e < 21; ++e) H[e] = wave_sum<LPQ>(hl[e]);
+  // the 28 per-lane partials (cost, J'r, J'J) summed per query through LDS
+  query_sums28<LPQ>(red, lane, c, gl, hl, cost, *reinterpret_cast<double(*)[6]>(g),
+                    *reinterpret_cast<double(*)[21]>(H));
   return wave_max<LPQ>(bad ? 1.0 : 0.0) == 0.0;
 }
 
@@ -275,6 +318,9 @@ template <int NCH, int LPQ>
 __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
   const int lane = threadIdx.x & (LPQ - 1);
   const int q = blockIdx.x * (64 / LPQ) + threadIdx.x / LPQ;
+  // (query_sums28's partials and sums, one region per query of the wave)
+  __shared__ __attribute__((aligned(16))) double red_all[(64 / LPQ) * (28 * (LPQ + 2) + 28)];
+  double *red = red_all + (threadIdx.x / LPQ) * (28 * (LPQ + 2) + 28);
   if (q >= p.nq) return;
   const int o0 = p.qs[q], k = p.qs[q + 1] - o0;
   arslam_localize_result res;
@@ -306,7 +352,7 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
   Rows<NCH> rows;
   double cost, g[6], H[21];   // (column norms squared = diag(H): HD(j))
   double x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-  bool finite = evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H);
+  bool finite = evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H, red);
   res.initial_cost = cost;
   if (!finite) {
     res.status = ARSLAM_FAILURE;
@@ -339,16 +385,17 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
       // (J~'J~ + D^2) y = J~'r, 6x6 Cholesky in every lane
       double A[21], y[6];
       {
+        // D^2 = diag / radius by one reciprocal (Ceres forms sqrt(diag / radius)
+        // and squares it: the same value to an ulp, twelve fewer sqrt / divide
+        // sequences per iteration)
+        const double rr = 1.0 / radius;
         int e = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
           for (int b = a; b < 6; ++b) {
             double v = scale[a] * scale[b] * H[e];
-            if (a == b) {
-              const double d = sqrt(diag[a] / radius);
-              v += d * d;
-            }
+            if (a == b) v += diag[a] * rr;
             A[e++] = v;
           }
       }
@@ -364,9 +411,12 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
 #pragma unroll
         for (int m = 0; m < j; ++m) s -= L_(j, m) * L_(j, m);
         lin_ok = lin_ok && s > 0.0;
-        const double ljj = sqrt(s);
-        L_(j, j) = ljj;
-        il[j] = 1.0 / ljj;   // one division per pivot; the column and both substitutions multiply
+        // 1 / L_jj = s^(-1/2): v_rsq_f64 and two Newton steps (the substitutions
+        // and the column only multiply by it; L_jj itself is never read)
+        double r = __builtin_amdgcn_rsq(s);
+        r = r * __builtin_fma(-0.5 * s * r, r, 1.5);
+        r = r * __builtin_fma(-0.5 * s * r, r, 1.5);
+        il[j] = r;
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
           double t = L_(i, j);
@@ -442,7 +492,7 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
 #pragma unroll
         for (int j = 0; j < 6; ++j) x[j] = xc[j];
         x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-        (void)evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H, &Fc.ac);
+        (void)evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H, red, &Fc.ac);
         gmax = 0.0;
 #pragma unroll
         for (int j = 0; j < 6; ++j) gmax = fmax(gmax, fabs(g[j]));

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void k_bench(const double *A, const double *Fg
     if (variant == 0) blocked_potrf64(D, inv, LTd, &bad, tid, colx);
     else if (variant == 1) blocked_potrf64_async(D, inv, LTd, &bad, fl, tid, colx, none);
     else if (variant == 2) blocked_potrf64_idle(D, inv, LTd, &bad, tid, colx, none, F);
-    else if (variant == 3) blocked_potrf64_async(D, inv, LTd, &bad, fl, tid, colx, none, F, true);
+    else if (variant == 3) blocked_potrf64_async(D, inv, LTd, &bad, fl, tid, colx, none, F, true, fl + 4);
     else if (tid < 64) {
       for (int p = 0; p < 4; ++p) diag16(D, 16 * p, inv, LTd + p * 16 * LI, &bad, tid, colx);
     }
