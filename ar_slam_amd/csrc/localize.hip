@@ -204,7 +204,7 @@ struct Rows {
 // (16-byte rows, bank-staggered by the pad) then [28] sums.
 template <int LPQ>
 __device__ __forceinline__ void query_sums28(double *red, int lane, double c, const double (&gl)[6],
-                                             const double (&hl)[21], double &cost, double (&g)[6], double (&H)[21]) {
+                                             const double (&hl)[21], double &cost) {
   constexpr int P = LPQ + 2;
   red[lane] = c;
 #pragma unroll
@@ -234,15 +234,17 @@ __device__ __forceinline__ void query_sums28(double *red, int lane, double c, co
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   cost = 0.5 * red[28 * P];
-#pragma unroll
-  for (int e = 0; e < 6; ++e) g[e] = red[28 * P + 1 + e];
-#pragma unroll
-  for (int e = 0; e < 21; ++e) H[e] = red[28 * P + 7 + e];
+  // (J'r and J'J stay in LDS, red + sums_off<LPQ>(): read where they are used,
+  // not held in 27 x 2 VGPRs across the LM loop)
 }
+
+// offset of query_sums28's sums in a query's LDS region: [0] cost x 2, [1..6] J'r, [7..27] J'J
+template <int LPQ>
+constexpr int sums_off() { return 28 * (LPQ + 2); }
 
 template <int NCH, int LPQ>
 __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const double *x, int lane,
-                                  Rows<NCH> &rows, double &cost, double g[6], double H[21], double *red,
+                                  double &cost, double *red,
                                   const AngleAxis *ac_pre = nullptr) {
   double c = 0.0, gl[6] = {0, 0, 0, 0, 0, 0}, hl[21];
 #pragma unroll
@@ -259,20 +261,15 @@ __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const do
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int R = lane + LPQ * ch;
-    rows.r[ch] = 0.0;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) rows.J[ch][j] = 0.0;
     if (R < nrow) {
       const int o = o0 + (R >> 3), row = R & 7;
       double j6[6];
       const double r = loc_row(F, x, p.aw + 4L * (4 * p.ot[o] + (row >> 1)), p.cam[0], row & 1,
                                p.corners[8L * o + row], j6);
       bad = bad || !isfinite(r);
-      rows.r[ch] = r;
       c += r * r;
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
-        rows.J[ch][j] = j6[j];
         gl[j] += j6[j] * r;
       }
       int e = 0;
@@ -283,8 +280,7 @@ __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const do
     }
   }
   // the 28 per-lane partials (cost, J'r, J'J) summed per query through LDS
-  query_sums28<LPQ>(red, lane, c, gl, hl, cost, *reinterpret_cast<double(*)[6]>(g),
-                    *reinterpret_cast<double(*)[21]>(H));
+  query_sums28<LPQ>(red, lane, c, gl, hl, cost);
   return wave_max<LPQ>(bad ? 1.0 : 0.0) == 0.0;
 }
 
@@ -349,10 +345,11 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
   const int nrow = 8 * k;
 
   // ---- iteration 0 ----
-  Rows<NCH> rows;
-  double cost, g[6], H[21];   // (column norms squared = diag(H): HD(j))
+  double cost;
+  // J'r and J'J of the last linearization, in LDS (column norms squared = diag(H): HD(j))
+  const double *g = red + sums_off<LPQ>() + 1, *H = red + sums_off<LPQ>() + 7;
   double x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-  bool finite = evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H, red);
+  bool finite = evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, cost, red);
   res.initial_cost = cost;
   if (!finite) {
     res.status = ARSLAM_FAILURE;
@@ -448,19 +445,28 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
       }
 #undef L_
 #undef UP
-      // step = -y; model cost change m = -sum mr (r + mr/2), mr = J~ step
+      // step = -y; model cost change m = -(r'J~ step + step' J~'J~ step / 2),
+      // from J'r and J'J (LDS) -- in exact arithmetic the same as Ceres'
+      // -sum mr (r + mr/2), mr = J~ step, over the rows, without keeping the
+      // rows in registers or reducing over the lanes
       double model = 0.0;
       bool valid = false;
       if (lin_ok) {
-        double mcc = 0.0;
+        double st[6];
 #pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
-          double mr = 0.0;
+        for (int j = 0; j < 6; ++j) st[j] = scale[j] * (-y[j]);   // the unscaled step
+        double lin = 0.0, quad = 0.0;
 #pragma unroll
-          for (int j = 0; j < 6; ++j) mr += rows.J[ch][j] * scale[j] * (-y[j]);
-          mcc += mr * (rows.r[ch] + mr / 2.0);   // padding rows contribute 0
+        for (int j = 0; j < 6; ++j) lin += g[j] * st[j];
+        int e = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          double row = 0.0;
+#pragma unroll
+          for (int b = a; b < 6; ++b) row += (b == a ? 0.5 : 1.0) * H[e++] * st[b];
+          quad += st[a] * row;
         }
-        model = -wave_sum<LPQ>(mcc);
+        model = -(lin + quad);
         valid = model > 0.0;
       }
       if (!valid) {
@@ -492,7 +498,7 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
 #pragma unroll
         for (int j = 0; j < 6; ++j) x[j] = xc[j];
         x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-        (void)evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, rows, cost, g, H, red, &Fc.ac);
+        (void)evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, cost, red, &Fc.ac);
         gmax = 0.0;
 #pragma unroll
         for (int j = 0; j < 6; ++j) gmax = fmax(gmax, fabs(g[j]));
