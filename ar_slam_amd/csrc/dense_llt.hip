@@ -90,6 +90,15 @@ __device__ __forceinline__ void store_tile64(double *__restrict__ g, long lda, c
   }
 }
 
+// A fast continuation (-DARSLAM_FAST_CONT, round 6, measured and not kept:
+// DESIGN §9): a claimed continuation whose A_kk is in registers starts on
+// waves 0, 2, 3 while wave 1 still waits for the solved tile's store
+// acknowledgements -- no closing barriers, no start barriers
+#ifdef ARSLAM_FAST_CONT
+constexpr bool kFastCont = true;
+#else
+constexpr bool kFastCont = false;
+#endif
 constexpr int LQ = 66;   // LDS pitch of the blocked panel kernel (16-lane row access and MFMA
                          // fragment reads both conflict-free)
 
@@ -454,18 +463,28 @@ __device__ __forceinline__ void lds_wait(const int *f, int v) {
 // round 0 (wave 3's third block made wave 0 wait ~500 cycles after diag16(0)):
 // those two count in *fcnt, and waves 1-3 await the complete round 0
 // themselves before their first applies.
+//
+// fsync (a fast continuation, k_factor_dag): the caller reset the flags
+// before its last barrier and the waves arrive at different times, so there
+// is no reset and no barrier here; fsync[0] = 1 once the flags are reset,
+// fsync[1] = 2 once waves 2-3 have moved A_kk into D.
 template <class Idle>
 __device__ bool blocked_potrf64_async(double *D, double *inv, double *LTd, int *bad, int *fl, int tid,
                                       double *colx, Idle &&idle, const double *F = nullptr, bool fold = false,
-                                      int *fcnt = nullptr) {
+                                      int *fcnt = nullptr, const int *fsync = nullptr) {
   const int w = tid >> 6, lane = tid & 63;
   const bool early = fold && fcnt;
-  if (tid == 0) {
-    *bad = 0;
-    fl[0] = fl[1] = fl[2] = fl[3] = 0;   // (fl[3]: the caller's prefetch count)
-    if (fcnt) *fcnt = 0;
+  if (fsync) {
+    lds_wait(fsync, 1);
+    lds_wait(fsync + 1, 2);
+  } else {
+    if (tid == 0) {
+      *bad = 0;
+      fl[0] = fl[1] = fl[2] = fl[3] = 0;   // (fl[3]: the caller's prefetch count)
+      if (fcnt) *fcnt = 0;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (w == 0) {
     STAMP(30);
     for (int p = 0; p < 4; ++p) {
@@ -1353,6 +1372,10 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
   // workgroup that drew the target claims and runs it once its waits are met.
   int next = -1, prev_k = -1;
   bool next_met = false;   // a claimed continuation whose early waits were already seen met
+  // A fast continuation: its predecessor's waves went straight on to it
+  // without the predecessor's closing barriers (wave 1 still waiting for the
+  // solved tile's store acknowledgements) -- see the end of the POTRF task.
+  bool fast_next = false;
   for (;;) {
     // thread coordinates re-derived per task from a laundered threadIdx: the
     // per-lane LDS/tile addresses of every task type are then computed where
@@ -1372,9 +1395,11 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
     const int t = __builtin_amdgcn_readfirstlane(next);
     const int pk = prev_k;   // a claimed continuation: the predecessor's column (its L_{k,pk} is in X)
     const bool premet = cont && next_met;   // (only for the claimed target it was polled for)
+    const bool fast = cont && fast_next;
     next = -1;
     prev_k = -1;
     next_met = false;
+    fast_next = false;
     DAG_PROGRESS(0, t);
     DAG_PROGRESS(1, 1);
     if (t >= a.t_end) break;
@@ -1396,8 +1421,10 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         sh[2] = (cont || r[kRecMaxdep] < 0 || atomicCAS(a.claimed + t, 0, 1) == 0) ? 1 : 0;
       }
     }
-    __syncthreads();
-    if (!sh[2]) continue;
+    if (!fast) {
+      __syncthreads();
+      if (!sh[2]) continue;
+    }
     DAG_PROGRESS(1, 2);
     if (a.trace && tid == 0) a.trace[8L * t + 1] = realtime();
     // the chain tasks (POTRF, TRSM) win SIMD arbitration over co-resident updates
@@ -1478,7 +1505,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
       } else {
         load_tile_wt(a.S + (long)task.w * (T64 * T64), D, tid);
       }
-      __syncthreads();
+      if (!fast) __syncthreads();
       if (a.trace && tid == 0) a.trace[8L * t + 4] = realtime();
       // The fused TRSM's tile: wave 1 fetches it into X while wave 0 factors
       // the first diagonal block, if its late waits are already met;
@@ -1492,7 +1519,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
       // a third each, beside the next panel: on the late elimination-tree chain
       // the tile's last update lands a few microseconds into the POTRF
       // (cfg3 k_factor_dag 758 -> 736 us).
-      if (tid == 0) {
+      if (tid == 0 && !fast) {   // (a fast continuation: reset by its predecessor)
         sh[6] = 0;
         sh[12] = sh[13] = sh[14] = sh[15] = 0;   // the fused solve's column steps done per row block
       }
@@ -1592,7 +1619,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
             if (wv == kPipeW2) sh[15] = sdone;
           }
         }
-      }, X, fold_in, sh + 7);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
+      }, X, fold_in, sh + 7, fast ? sh + 22 : nullptr);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
       if (tid == 0)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
@@ -1655,6 +1682,84 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         int cas_old = 1;
         if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
         for (int st = max(s0, 2); st < 4; ++st) trsm_step(X, D, LTd, w, st, lane);
+#ifdef ARSLAM_FAST_CONT
+        // whether A_kk comes in D, before the barrier; the claim's answer (the
+        // CAS issued beside steps 1-2) is read by tid 0 after it, while wave 1
+        // issues the tile's stores and waves 2-3 move A_kk, and published in
+        // sh[5] (1 + claimed target, 0 until then)
+        if (tid == 0) sh[5] = sh[22] = sh[23] = 0;   // (a fast continuation's start flags, below)
+        if (w >= 2 && lane == 0) sh[16 + w - 2] = ap_ok ? 1 : 0;
+        __syncthreads();
+        if (tid == 0) {
+          const int cl = want && cas_old == 0 ? c : -1;
+          if (c >= 0 && cl < 0) atomicSub(inflight, 1);
+          sh[4] = cl;
+          lds_set(sh + 5, 1);
+        }
+        // A fast continuation (the claimed target's early waits were seen met,
+        // its A_kk is in registers, and it folds this task's column alone): the
+        // waves go straight on to it.  Wave 1 stores the solved tile, waits
+        // for the acknowledgements and publishes the tile -- at the time the
+        // barrier version would -- while wave 0 starts the target's fold and
+        // first diagonal block: the acknowledgement round trip and the two
+        // closing barriers, the target's start barriers and its flag resets
+        // leave the chain.  Waves 2-3 move A_kk into D (L_kk's last reader was
+        // the solve) and count themselves in sh[23]; tid 0 resets the target's
+        // POTRF flags now (every reader of them is past the barrier) and sets
+        // sh[22].  Wave 1's first fold block, (1, 0), is needed only after wave
+        // 0's first diagonal block.
+        // wave 1 stores the solved tile, waves 2-3 move the continuation's
+        // A_kk into D (free: L_kk's last reader was the solve)
+        if (w == 1) store_tile_wt<64>(Ct, X, tid - 64, false);
+        lds_wait(sh + 5, 1);
+        const int claim = sh[4];
+        const bool fc = kFastCont && claim >= 0 && sh[20] && sh[21] && sh[16] && sh[17] && sh_rec[kRecZ] >= 0 &&
+                        sh_rec[kRecQ1] - sh_rec[kRecQ0] == 1 && sh_rec[kRecFoldK0] == k;
+        if (w >= 2) {
+          if (ap_ok) {
+            ld_wt16x16_wait(apv);
+            const int t2 = tid - 128;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int e = u * 128 + t2, row = e >> 5, c2 = (e & 31) * 2;
+              *reinterpret_cast<dbl2 *>(D + row * LQ + c2) = apv[u];
+            }
+          }
+          if (fc) lds_add(sh + 23, lane);
+        }
+        // (wave 1 alone waits for the stores' acknowledgements; releasing
+        // the tile from the continuation instead was measured slower)
+        if (w == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (fc) {
+          if (w == 1 && lane == 0) {
+            __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a.trace) a.trace[8L * t + 7] = realtime();
+          }
+          if (tid == 0) {
+            sh[1] = 0;                                   // the target POTRF's bad flag
+            sh[7] = sh[8] = sh[9] = sh[10] = sh[11] = 0;   // its fold count and pipeline flags
+            sh[6] = 0;
+            sh[12] = sh[13] = sh[14] = sh[15] = 0;
+            if (a.trace) a.trace[8L * t + 3] = blockIdx.x | ((unsigned long long)(1 | 2 | (pref ? 4 : 0) | 8 | 16 | 32) << 32);
+            lds_set(sh + 22, 1);
+          }
+          fast_next = true;
+        } else {
+          __syncthreads();
+          if (tid == 0) __hip_atomic_fetch_add(ready + sub.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (a.trace && tid == 0) {
+            a.trace[8L * t + 7] = realtime();
+            // (debug flags above the workgroup: premet, A_kk prefetched into D, fused tile prefetched,
+            // the continuation's early waits seen met, claimed)
+            const unsigned long long fl = (premet ? 1 : 0) | (akk_in_d ? 2 : 0) | (pref ? 4 : 0) |
+                                          (sh[20] && sh[21] ? 8 : 0) | (sh[4] >= 0 ? 16 : 0);
+            a.trace[8L * t + 3] = blockIdx.x | (fl << 32);
+          }
+          __syncthreads();
+        }
+        next = claim;
+        next_met = next >= 0 && sh[20] && sh[21];
+#else
         __syncthreads();
         // wave 1 stores the solved tile, waves 2-3 move the continuation's
         // A_kk into D (free: L_kk's last reader was the solve)
@@ -1693,6 +1798,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         __syncthreads();
         next = sh[4];
         next_met = next >= 0 && sh[20] && sh[21];
+#endif
         if (next >= 0) prev_k = k;
       }
     } else if (task.x == 3) {
