@@ -243,7 +243,7 @@ template <int LPQ>
 constexpr int sums_off() { return 28 * (LPQ + 2); }
 
 template <int NCH, int LPQ>
-__device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const double *x, int lane,
+__device__ bool evaluate_jacobian(const LocParams &p, const double *rc, int nrow, const double *x, int lane,
                                   double &cost, double *red,
                                   const AngleAxis *ac_pre = nullptr) {
   double c = 0.0, gl[6] = {0, 0, 0, 0, 0, 0}, hl[21];
@@ -262,10 +262,9 @@ __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const do
   for (int ch = 0; ch < NCH; ++ch) {
     const int R = lane + LPQ * ch;
     if (R < nrow) {
-      const int o = o0 + (R >> 3), row = R & 7;
+      const double *rr = rc + 4 * R;   // (the row's corner world point and observation, LDS)
       double j6[6];
-      const double r = loc_row(F, x, p.aw + 4L * (4 * p.ot[o] + (row >> 1)), p.cam[0], row & 1,
-                               p.corners[8L * o + row], j6);
+      const double r = loc_row(F, x, rr, p.cam[0], R & 1, rr[3], j6);
       bad = bad || !isfinite(r);
       c += r * r;
 #pragma unroll
@@ -285,7 +284,7 @@ __device__ bool evaluate_jacobian(const LocParams &p, int o0, int nrow, const do
 }
 
 template <int NCH, int LPQ>
-__device__ double evaluate_cost(const LocParams &p, int o0, int nrow, const double *x, int lane, bool &finite,
+__device__ double evaluate_cost(const LocParams &p, const double *rc, int nrow, const double *x, int lane, bool &finite,
                               CapFrame &F) {
   cap_frame(x, F, false);
   double c = 0.0;
@@ -294,9 +293,8 @@ __device__ double evaluate_cost(const LocParams &p, int o0, int nrow, const doub
   for (int ch = 0; ch < NCH; ++ch) {
     const int R = lane + LPQ * ch;
     if (R < nrow) {
-      const int o = o0 + (R >> 3), row = R & 7;
-      const double r = loc_row(F, x, p.aw + 4L * (4 * p.ot[o] + (row >> 1)), p.cam[0], row & 1,
-                               p.corners[8L * o + row], nullptr);
+      const double *rr = rc + 4 * R;
+      const double r = loc_row(F, x, rr, p.cam[0], R & 1, rr[3], nullptr);
       bad = bad || !isfinite(r);
       c += r * r;
     }
@@ -317,6 +315,11 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
   // (query_sums28's partials and sums, one region per query of the wave)
   __shared__ __attribute__((aligned(16))) double red_all[(64 / LPQ) * (28 * (LPQ + 2) + 28)];
   double *red = red_all + (threadIdx.x / LPQ) * (28 * (LPQ + 2) + 28);
+  // each row's corner world point and observation, gathered once per query
+  // (obs_tag -> the tag's corner points: two dependent global loads per row
+  // that every cost and Jacobian evaluation repeated)
+  __shared__ __attribute__((aligned(16))) double rc_all[(64 / LPQ) * NCH * LPQ * 4];
+  double *rc = rc_all + (threadIdx.x / LPQ) * NCH * LPQ * 4;
   if (q >= p.nq) return;
   const int o0 = p.qs[q], k = p.qs[q + 1] - o0;
   arslam_localize_result res;
@@ -343,13 +346,27 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
   if (p.init_from_map)
     init_capture_pose(p.corners + 8L * res.init_obs, p.cam, p.tag + 6L * p.ot[res.init_obs], x);
   const int nrow = 8 * k;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int R = lane + LPQ * ch;
+    if (R < nrow) {
+      const int o = o0 + (R >> 3), row = R & 7;
+      const double *a = p.aw + 4L * (4 * p.ot[o] + (row >> 1));
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      reinterpret_cast<d2 *>(rc + 4 * R)[0] = d2{a[0], a[1]};
+      reinterpret_cast<d2 *>(rc + 4 * R)[1] = d2{a[2], p.corners[8L * o + row]};
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
   // ---- iteration 0 ----
   double cost;
   // J'r and J'J of the last linearization, in LDS (column norms squared = diag(H): HD(j))
   const double *g = red + sums_off<LPQ>() + 1, *H = red + sums_off<LPQ>() + 7;
   double x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-  bool finite = evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, cost, red);
+  bool finite = evaluate_jacobian<NCH, LPQ>(p, rc, nrow, x, lane, cost, red);
   res.initial_cost = cost;
   if (!finite) {
     res.status = ARSLAM_FAILURE;
@@ -487,7 +504,7 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
       }
       bool cfin = true;
       CapFrame Fc;
-      double cand = evaluate_cost<NCH, LPQ>(p, o0, nrow, xc, lane, cfin, Fc);
+      double cand = evaluate_cost<NCH, LPQ>(p, rc, nrow, xc, lane, cfin, Fc);
       if (!cfin) cand = DBL_MAX;
       // ParameterToleranceReached / FunctionToleranceReached
       if (sqrt(sq) <= p.ptol * (x_norm + p.ptol)) { res.status = ARSLAM_CONVERGENCE; res.rule = ARSLAM_RULE_PARAMETER; break; }
@@ -498,7 +515,7 @@ __global__ __launch_bounds__(64, 2) void k_localize(LocParams p) {
 #pragma unroll
         for (int j = 0; j < 6; ++j) x[j] = xc[j];
         x_norm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
-        (void)evaluate_jacobian<NCH, LPQ>(p, o0, nrow, x, lane, cost, red, &Fc.ac);
+        (void)evaluate_jacobian<NCH, LPQ>(p, rc, nrow, x, lane, cost, red, &Fc.ac);
         gmax = 0.0;
 #pragma unroll
         for (int j = 0; j < 6; ++j) gmax = fmax(gmax, fabs(g[j]));

@@ -237,8 +237,8 @@ def load_pmc_localize():
 # the PMC passes of the commit this bench line measures (each profile round writes its own
 # directory; these name the latest): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md,
 # tools/pmc_bench.sh) and the dominant kernel's MFMA utilisation (tools/pmc_mfma.sh)
-PMC_PROFILE = os.path.join("profiles", "r05", "pmc_hbm_bytes.json")
-PMC_MFMA = os.path.join("profiles", "r05", "pmc_mfma.json")
+PMC_PROFILE = os.path.join("profiles", "r06", "pmc_hbm_bytes.json")
+PMC_MFMA = os.path.join("profiles", "r06", "pmc_mfma.json")
 
 
 def _load_json(rel):
