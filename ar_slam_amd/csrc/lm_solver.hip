@@ -459,6 +459,7 @@ struct arslam_lm {
   void upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L, int extend_from = -1);
   arslam::SchurGather sg;   // the loaded problem's Schur gather plan
   bool try_extend(const arslam_soa_problem *p);
+  bool try_extend_mixed(const arslam_soa_problem *p);
   arslam::ReducedLayout lay;      // the loaded layout (one rank), kept for try_extend
   bool pk_appended_only = false;  // since the last load only residual blocks of known tags were added
   int setup_kind = ARSLAM_SETUP_LOAD;
@@ -984,8 +985,10 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
 // load() instead.  (summary.factor_scalar_flops keeps the loaded problem's
 // count: a new coupling inside a fill tile changes the scalar structure.)
 bool arslam_lm::try_extend(const arslam_soa_problem *p) {
+  // (ARSLAM_ELIM_MIXED whose set was every capture: new captures join it, as in try_extend_mixed)
   if (!loaded || multi() || elim_used != ARSLAM_ELIM_CAPTURES || !has_f ||
-      (opt.elimination != ARSLAM_ELIM_AUTO && opt.elimination != ARSLAM_ELIM_CAPTURES))
+      (opt.elimination != ARSLAM_ELIM_AUTO && opt.elimination != ARSLAM_ELIM_CAPTURES &&
+       opt.elimination != ARSLAM_ELIM_MIXED))
     return false;
   const double t0 = now_s();
   if (opt.elimination == ARSLAM_ELIM_AUTO) {   // the side Ceres would eliminate may change as the graph grows
@@ -1061,6 +1064,127 @@ bool arslam_lm::try_extend(const arslam_soa_problem *p) {
   if (prof)
     std::fprintf(stderr, "arslam append: nc %d side %.3f host %.3f check %.3f upload %.3f ms\n", nc,
                  1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2), 1e3 * (now_s() - t3));
+  return true;
+}
+
+// ARSLAM_ELIM_MIXED on a grown pointer-keyed problem (the reference's
+// solveIncremental, ar_slam_util.cpp:629-742: new captures, each with
+// residual blocks of known tags).  A fresh load would recompute Ceres' set
+// (ComputeStableSchurOrdering) and rebuild the layout, plan and gather plan;
+// here the set only grows: every new capture whose tags are all on the
+// reduced side joins it as an eliminated group, appended after the loaded
+// groups (so the loaded groups, the f-blocks and the gather plan's summation
+// order are kept, and the plan is extended as for captures), and tags never
+// leave the reduced side -- a new capture that sees an eliminated tag, a new
+// tag or a residual on an old capture reloads.  The set is then the loaded
+// problem's Ceres set plus the new captures: an independent set (a new
+// capture is adjacent only to its tags, all reduced), not necessarily the
+// one Ceres would pick on the grown graph; the step is the same exact solve.
+bool arslam_lm::try_extend_mixed(const arslam_soa_problem *p) {
+  if (!loaded || multi() || elim_used != ARSLAM_ELIM_MIXED || !has_f || opt.elimination != ARSLAM_ELIM_MIXED)
+    return false;
+  const double t0 = now_s();
+  const long nb_old = (long)mx.obs_cap.size();
+  const int ng_old = (int)mx.kind.size(), nf = (int)mx.f_src.size();
+  if (p->n_tag != mx.src_n_tag || p->n_cap < mx.src_n_cap || p->n_obs <= nb_old) return false;
+  // the f-block of each original tag (-1: eliminated or not a parameter)
+  std::vector<int> tag_f(p->n_tag, -1);
+  for (int f = 0; f < nf; ++f)
+    if (!mx.f_is_cap[f]) tag_f[mx.f_src[f]] = f;
+  // the new residuals: on new captures only, every tag on the reduced side
+  for (long b = nb_old; b < p->n_obs; ++b)
+    if (p->obs_cap[b] < mx.src_n_cap || tag_f[p->obs_tag[b]] < 0) return false;
+  arslam::MixedProblem m = mx;
+  const int nc_new = p->n_cap - mx.src_n_cap;
+  std::vector<int> cap_g(nc_new, -1);
+  for (long b = nb_old; b < p->n_obs; ++b) {
+    const int c = p->obs_cap[b], q = c - mx.src_n_cap;
+    if (cap_g[q] < 0) {
+      cap_g[q] = (int)m.kind.size();
+      m.kind.push_back(arslam::kMixCap);
+      m.group_src.push_back(c);
+      m.cap_const.push_back(p->cap_const ? p->cap_const[c] : 0);
+    }
+    m.obs_cap.push_back(cap_g[q]);
+    m.obs_tag.push_back(tag_f[p->obs_tag[b]]);
+  }
+  for (int q = 0; q < nc_new; ++q)
+    if (cap_g[q] < 0) return false;   // (a capture without residual blocks: not a block of Ceres' problem)
+  const int ng = (int)m.kind.size();
+  m.src_n_cap = p->n_cap;
+  m.cap.resize(6L * ng);
+  m.soa = *p;
+  m.soa.n_cap = ng;
+  m.soa.n_tag = nf;
+  m.soa.cap = m.cap.data();
+  m.soa.tag = m.tag.data();
+  m.soa.obs_cap = m.obs_cap.data();
+  m.soa.obs_tag = m.obs_tag.data();
+  m.soa.cap_const = m.cap_const.data();
+  m.soa.tag_const = m.tag_const.data();
+  std::vector<double> xv(3 + 6L * ng + 6L * nf);
+  arslam::mixed_values(m, *p, xv.data());
+  std::memcpy(m.cap.data(), xv.data() + 3, 6L * ng * sizeof(double));
+  if (nf) std::memcpy(m.tag.data(), xv.data() + 3 + 6L * ng, 6L * nf * sizeof(double));
+  const double t1 = now_s();
+  arslam::HostProblem h = arslam::host_problem(&m.soa, nullptr);
+  arslam::mixed_patch(h, m, *p);
+  const double t2 = now_s();
+  // the same free f-blocks and camera (the same reduced rows)
+  if ((lay.cam_row >= 0) != (h.slot_free[0] != 0)) return false;
+  for (int f = 0; f < nf; ++f)
+    if ((lay.tag_row[f] >= 0) != (h.slot_free[3 + 6L * h.nc + 6L * f] != 0)) return false;
+  // every new group's tiles pairwise in the loaded factor's tiles
+  const int T = lay.T;
+  std::vector<int> ts;
+  for (int g = ng_old; g < ng; ++g) {
+    ts.clear();
+    if (lay.cam_row >= 0) {
+      ts.push_back(lay.cam_row / 64);
+      ts.push_back((lay.cam_row + 2) / 64);
+    }
+    for (int a = h.cap_blk_start[g]; a < h.cap_blk_start[g + 1]; ++a) {
+      const int r0 = lay.tag_row[h.blk_tag[a]];
+      if (r0 < 0) continue;
+      ts.push_back(r0 / 64);
+      ts.push_back((r0 + 5) / 64);
+    }
+    for (size_t a = 0; a < ts.size(); ++a)
+      for (size_t b = 0; b < ts.size(); ++b)
+        if (ts[a] >= ts[b] && plan.h_tile_id[(size_t)ts[a] * T + ts[b]] < 0) return false;
+  }
+  for (int g = ng_old; g < ng; ++g) covis_add(h, lay, g);
+  if (covis_nt && 10 * covis_edges > 11 * prev_order_edges) return false;
+  if (4L * h.nc > 5L * prev_order_nc) return false;   // (a quarter more groups: a fresh order)
+  // the f-block slots move with the group count
+  for (int &sl : lay.row_slot)
+    if (sl >= 3) sl += 6 * (h.nc - nc);
+  mx = std::move(m);
+  mx.soa.cap = mx.cap.data();   // (the moved vectors keep their buffers; re-pointed for clarity)
+  mx.soa.tag = mx.tag.data();
+  mx.soa.obs_cap = mx.obs_cap.data();
+  mx.soa.obs_tag = mx.obs_tag.data();
+  mx.soa.cap_const = mx.cap_const.data();
+  mx.soa.tag_const = mx.tag_const.data();
+  ceres_e_cap += nc_new;
+  nc = h.nc;
+  nc_full = h.nc;
+  nc_user = p->n_cap;
+  nb = h.nb;
+  n = h.n;
+  nb_global = h.nb_global;
+  slot_free = h.slot_free;
+  x0 = h.x0;
+  const double t3 = now_s();
+  upload_problem(h, lay, ng_old);
+  soa = *p;
+  pk_appended_only = true;
+  setup_kind = ARSLAM_SETUP_APPEND;
+  setup_s = now_s() - t0;
+  static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
+  if (prof)
+    std::fprintf(stderr, "arslam append (mixed): groups %d host %.3f check %.3f upload %.3f ms\n", ng,
+                 1e3 * (t2 - t1), 1e3 * (t3 - t2), 1e3 * (now_s() - t3));
   return true;
 }
 
@@ -1926,7 +2050,7 @@ int arslam_lm_solve(arslam_lm *h, arslam_lm_summary *summary) {
     } stage_guard{h};
     if (h->loaded && h->pk_loaded && !h->pk_dirty) {
       h->reload_values(&p);   // same problem, new values: no host rebuild, no re-upload of observations
-    } else if (h->loaded && h->pk_loaded && h->pk_appended_only && h->try_extend(&p)) {
+    } else if (h->loaded && h->pk_loaded && h->pk_appended_only && (h->try_extend(&p) || h->try_extend_mixed(&p))) {
       h->pk_dirty = false;    // appended residual blocks within the loaded tile pattern: layout and plan kept
     } else {
       h->reuse_order = h->pk_loaded;   // a grown pointer-keyed problem (not the first load)

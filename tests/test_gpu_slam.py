@@ -92,6 +92,40 @@ def test_incremental_solve_with_ceres_exact_set(lm):
     _compare(s, o)
     used = {s.solve_summary(i)["elimination_used"] for i in range(s.num_solves)}
     assert lm.ELIM_MIXED in used and lm.ELIM_TAGS in used
+    # (round 6) a grown mixed problem whose new captures see only reduced tags is appended: the set
+    # grows by them, the layout, plan and gather plan are kept
+    appended = [i for i in range(s.num_solves) if s.solve_summary(i)["elimination_used"] == lm.ELIM_MIXED
+                and s.solve_summary(i)["setup_kind"] == lm.SETUP_APPEND]
+    assert appended, [(s.solve_summary(i)["elimination_used"], s.solve_summary(i)["setup_kind"])
+                      for i in range(s.num_solves)]
+
+
+def test_incremental_cfg2_prefix_under_mixed_set_appends(lm):
+    """The reference's solveIncremental on the first 300 captures of cfg2 under ELIM_MIXED: from about
+    the 220th capture Ceres' set mixes captures and tags; new captures that see only reduced tags
+    join the set and append (setup_kind APPEND) instead of a full load, and the flow ends in the
+    state the same flow reaches eliminating the captures -- the same exact solves, rounding apart."""
+    g = synth.config_graph("cfg2")
+    runs = {}
+    for elim in (lm.ELIM_CAPTURES, lm.ELIM_MIXED):
+        s = lm.SlamSolver(elimination=elim)
+        s.set_camera(g.camera)
+        for uid, ids, corners in _detections(g, range(300)):
+            s.add_detections(uid, ids, corners)
+        s.solve_incremental()
+        runs[elim] = s
+    a, m = runs[lm.ELIM_CAPTURES], runs[lm.ELIM_MIXED]
+    assert m.solve_order() == a.solve_order() and m.num_solves == a.num_solves
+    la, lmx = a.last_summary(), m.last_summary()
+    assert lmx["termination"] == la["termination"]
+    assert abs(lmx["final_cost"] - la["final_cost"]) <= 1e-6 * la["final_cost"]
+    np.testing.assert_allclose(m.capture_poses(), a.capture_poses(), atol=1e-5)
+    np.testing.assert_allclose(m.aruco_poses(), a.aruco_poses(), atol=1e-5)
+    sums = [m.solve_summary(i) for i in range(m.num_solves)]
+    mixed = [d["setup_kind"] for d in sums if d["elimination_used"] == lm.ELIM_MIXED]
+    n_app, n_load = mixed.count(lm.SETUP_APPEND), mixed.count(lm.SETUP_LOAD)
+    print(f"cfg2[:300] under ELIM_MIXED: {len(mixed)} mixed solves, {n_app} appended, {n_load} loaded")
+    assert n_app > 0
 
 
 def test_incremental_cfg2_batches_match_oracle_driver(lm):
