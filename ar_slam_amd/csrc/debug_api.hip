@@ -262,6 +262,54 @@ extern "C" int arslam_debug_reduced_plan(const arslam_soa_problem *p, int orderi
   }
 }
 
+extern "C" int arslam_debug_reduced_plan_side(const arslam_soa_problem *p, int elimination, arslam_plan_info *info) {
+  if (!p || !info || elimination < ARSLAM_ELIM_CAPTURES || elimination > ARSLAM_ELIM_MIXED) return ARSLAM_E_INVALID_ARG;
+  try {
+    std::memset(info, 0, sizeof(*info));
+    // the device problem of that side, as arslam_lm's load builds it (one rank)
+    std::vector<uint8_t> e_cap, e_tag;
+    arslam::MixedProblem mx;
+    const arslam_soa_problem swapped = arslam::swap_roles(*p);
+    const arslam_soa_problem *q = p;
+    int side = elimination;
+    if (side == ARSLAM_ELIM_MIXED) {
+      const arslam::SchurSide cs = arslam::ceres_schur_side(p, &e_cap, &e_tag);
+      if (cs.e_cam || cs.e_tag == 0) side = ARSLAM_ELIM_CAPTURES;
+      else if (cs.e_cap == 0) side = ARSLAM_ELIM_TAGS;
+      else mx = arslam::mixed_problem(*p, e_cap, e_tag), q = &mx.soa;
+    }
+    if (side == ARSLAM_ELIM_TAGS) q = &swapped;
+    arslam::HostProblem h = arslam::host_problem(q, nullptr);
+    if (side == ARSLAM_ELIM_MIXED) arslam::mixed_patch(h, mx, *p);
+    arslam::ReducedLayout L = arslam::reduced_layout(h, 2, true, nullptr, nullptr);
+    info->n_reduced = L.nR;
+    info->n_padded = L.N;
+    info->pad_rows = L.pad_rows;
+    info->tiles_per_side = L.T;
+    info->n_parts = L.n_parts;
+    info->camera_row = L.cam_row;
+    info->scalar_flops = L.scalar_flops;
+    if (L.nR > 0) {
+      arslam::LltPlan plan;
+      arslam::llt_plan_symbolic(plan, L.T, L.N, L.pattern);
+      info->n_levels = plan.nlev;
+      info->n_assembled_tiles = plan.n_assembled;
+      info->n_factor_tiles = plan.n_tiles;
+      info->n_update_tiles = plan.total_upd_tiles;
+      info->n_update_items = (long)plan.h_items.size();
+      info->update_flops = plan.total_upd_flops;
+      info->factor_flops = plan.total_factor_flops;
+      info->n_dag_tasks = plan.n_dag_tasks;
+      info->dag_valid = arslam::dag_check(plan) ? 1 : 0;
+    }
+    return side;
+  } catch (const arslam::ApiError &e) {
+    return e.code;
+  } catch (...) {
+    return ARSLAM_E_INVALID_ARG;
+  }
+}
+
 namespace {
 arslam::LltPlan one_rank_plan(const arslam_soa_problem *p) {
   const arslam::HostProblem h = arslam::host_problem(p, nullptr);

@@ -695,6 +695,22 @@ void mixed_patch(HostProblem &h, const MixedProblem &m, const arslam_soa_problem
     const bool fr = (m.f_is_cap[f] ? used_c[o] : used_t[o]) && !m.tag_const[f];
     for (int j = 0; j < 6; ++j) h.slot_free[3 + 6L * ng + 6L * f + j] = fr;
   }
+  // the f-blocks' places for the ordering: a tag's translation; a capture's
+  // the mean translation of the tags it sees (its own translation is minus the
+  // camera centre, a mirror image of the tags' frame)
+  std::vector<double> cap_xyz(3L * p.n_cap, 0.0);
+  std::vector<int> cap_n(p.n_cap, 0);
+  for (int b = 0; b < p.n_obs; ++b) {
+    const int c = p.obs_cap[b];
+    for (int a = 0; a < 3; ++a) cap_xyz[3L * c + a] += p.tag[6L * p.obs_tag[b] + a];
+    cap_n[c]++;
+  }
+  h.nd_xyz.assign(3L * nf, 0.0);
+  for (int f = 0; f < nf; ++f) {
+    const int o = m.f_src[f];
+    for (int a = 0; a < 3; ++a)
+      h.nd_xyz[3L * f + a] = m.f_is_cap[f] ? (cap_n[o] ? cap_xyz[3L * o + a] / cap_n[o] : 0.0) : p.tag[6L * o + a];
+  }
 }
 
 HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_deg_sum) {
@@ -786,7 +802,8 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
 
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
                              const ReduceMaxU8 &pattern_max,
-                             const std::vector<int> *reuse_tag_row, long reuse_edges, bool fast_order) {
+                             const std::vector<int> *reuse_tag_row, long reuse_edges, bool fast_order,
+                             bool reuse_by_identity) {
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: layout phases
   auto clk = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   double tl[5] = {prof ? clk() : 0.0, 0, 0, 0, 0};
@@ -847,9 +864,11 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   if (prof) tl[1] = clk();
   // (tags past the earlier order's -- new parameter blocks are appended --
   // are placed after its rows, at the end of its last part: below)
+  // (by identity: an entry per tag, -1 for a tag without an earlier row)
   const int n_old = reuse_tag_row ? std::min((int)reuse_tag_row->size(), nt) : 0;
   bool reuse = reuse_tag_row && (int)reuse_tag_row->size() <= std::max(nt, 1) && 10 * L.n_edges <= 11 * reuse_edges;
-  for (int t = 0; reuse && t < n_old; ++t) reuse = ((*reuse_tag_row)[t] >= 0) == (tfree[t] != 0);
+  if (reuse_by_identity) reuse = reuse && (int)reuse_tag_row->size() == nt;
+  for (int t = 0; reuse && !reuse_by_identity && t < n_old; ++t) reuse = ((*reuse_tag_row)[t] >= 0) == (tfree[t] != 0);
   L.order_edges = reuse ? reuse_edges : L.n_edges;
   L.order_reused = reuse;
   std::vector<std::vector<int>> parts;
@@ -859,7 +878,8 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
     // tag positions (initial values) embed the co-visibility graph for geometric separators
     std::vector<double> xyz(3L * nt);
     for (int t = 0; t < nt; ++t)
-      for (int a = 0; a < 3; ++a) xyz[3L * t + a] = h.x0[3 + 6L * nc + 6L * t + a];
+      for (int a = 0; a < 3; ++a)
+        xyz[3L * t + a] = h.nd_xyz.empty() ? h.x0[3 + 6L * nc + 6L * t + a] : h.nd_xyz[3L * t + a];
     // leaves of up to 32 tags (192 rows = 3 whole tiles): a smaller dissection
     // would not shorten the elimination tree, only add padding and parts
     // (debug sweeps; clamped to [1, 4096])
@@ -874,7 +894,9 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
   }
   long row = 0, real = 0;
   if (reuse) {
-    for (int t = 0; t < n_old; ++t) L.tag_row[t] = (*reuse_tag_row)[t];
+    // (by identity: a tag whose earlier row is no longer a parameter leaves
+    // those rows as padding, identity rows like the alignment padding)
+    for (int t = 0; t < n_old; ++t) L.tag_row[t] = tfree[t] ? (*reuse_tag_row)[t] : -1;
     for (int t = 0; t < n_old; ++t)
       if (L.tag_row[t] >= 0) {
         row = std::max(row, (long)L.tag_row[t] + 6);
@@ -884,8 +906,8 @@ ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, co
     // root separator): a valid order whatever they couple to, since every
     // part's elimination path ends there; the caller recomputes the order
     // once the tile elimination tree grows taller than a fresh one
-    for (int t = n_old; t < nt; ++t)
-      if (tfree[t]) {
+    for (int t = 0; t < nt; ++t)
+      if (tfree[t] && (t >= n_old || L.tag_row[t] < 0)) {
         L.tag_row[t] = (int)row;
         row += 6;
         real += 6;

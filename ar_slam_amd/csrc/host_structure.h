@@ -58,6 +58,10 @@ struct HostProblem {
   std::vector<unsigned char> slot_free, obs_active;
   std::vector<double> x0;           // [n] initial slots
   long nb_global = 0;
+  // [3 nt] the reduced blocks' places for the geometric separators (empty: the
+  // tag translations in x0); a mixed set's reduced captures sit at the mean of
+  // the tags they see (a capture's translation slot is minus its centre)
+  std::vector<double> nd_xyz;
 };
 
 // Reverse Cuthill-McKee order of an undirected graph (adjacency lists).
@@ -155,10 +159,15 @@ double scalar_cholesky_flops(const std::vector<std::vector<int>> &adj, const std
 // ordering) when the set of free tags is unchanged and the graph has grown by
 // at most a tenth since -- an incremental solve that only added captures
 // keeps its elimination order until the fill it was made for is outdated.
+// reuse_by_identity: reuse_tag_row has one entry per tag of h (the earlier
+// row of the same block, -1 for a block new to the reduced side) -- a mixed
+// set re-chosen on a grown graph (ARSLAM_ELIM_MIXED), whose reduced blocks are
+// renumbered; earlier rows of blocks gone from the reduced side stay padding,
+// the new blocks go to the end of the last part.
 ReducedLayout reduced_layout(const HostProblem &h, int ordering, bool sparse, const ReduceMaxU8 &adj_max,
                              const ReduceMaxU8 &pattern_max,
                              const std::vector<int> *reuse_tag_row = nullptr, long reuse_edges = 0,
-                             bool fast_order = false);
+                             bool fast_order = false, bool reuse_by_identity = false);
 
 // Deterministic Schur assembly.  k_schur stores capture c's local reduced
 // system at slab + cap_off[c] block-packed: local blocks U = 0 (f, 1 row),

@@ -507,6 +507,10 @@ struct arslam_lm {
   }
   bool reuse_order = false;  // load(): keep the previous tag order when the free tags are unchanged
   std::vector<int> prev_tag_row;
+  // ARSLAM_ELIM_MIXED: the rows of the last layout by original block (tag /
+  // capture id, -1 off the reduced side), for a reload whose re-chosen set
+  // renumbers the reduced blocks (reduced_layout by identity)
+  std::vector<int> prev_mx_tag_row, prev_mx_cap_row;
   int prev_ordering = -1, prev_skip = -1;
   long prev_order_edges = 0;
   // the capture count the order was computed at: nested dissection cuts along
@@ -515,6 +519,7 @@ struct arslam_lm {
   // its co-visibility graph barely changed (incremental cfg2: an order kept
   // from the first load gave 18 elimination-tree levels, a fresh one 10)
   int prev_order_nc = 0;
+  bool last_order_reused = false;   // summary.order_reused
   int prev_order_height = 0;   // tile elimination-tree height of the layout the order was computed for
   static int etree_height(const arslam::ReducedLayout &L) {
     std::vector<uint8_t> P = L.pattern;
@@ -654,12 +659,24 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
           "tag elimination: a tag seen by more than 256 distinct captures");
   fail_if(side == ARSLAM_ELIM_CAPTURES && !caps_fit, ARSLAM_E_UNSUPPORTED,
           "capture elimination: a capture sees more than 256 distinct tags");
-  // (the f-side changed, or is a mixed set of its own: no order to reuse)
+  // (the f-side changed, or is a mixed set of its own: no order to reuse by
+  // index; a mixed set after a mixed set maps the earlier rows by block)
+  const bool was_mixed = elim_used == ARSLAM_ELIM_MIXED;
   if (side != elim_used || side == ARSLAM_ELIM_MIXED) prev_tag_row.clear();
   elim_used = side;
   const arslam_soa_problem swapped = arslam::swap_roles(*p_in);
   if (side == ARSLAM_ELIM_MIXED) mx = arslam::mixed_problem(*p_in, e_cap, e_tag);
   else mx = arslam::MixedProblem{};
+  static const bool mx_fresh = std::getenv("ARSLAM_MIXED_FRESH_ORDER") != nullptr;   // debug A/B: round 6's first cut
+  const bool by_identity = side == ARSLAM_ELIM_MIXED && was_mixed && reuse_order && !mx_fresh && !mx.f_src.empty() &&
+                           (!prev_mx_tag_row.empty() || !prev_mx_cap_row.empty());
+  if (by_identity) {
+    prev_tag_row.assign(mx.f_src.size(), -1);
+    for (size_t f = 0; f < mx.f_src.size(); ++f) {
+      const std::vector<int> &m = mx.f_is_cap[f] ? prev_mx_cap_row : prev_mx_tag_row;
+      if (mx.f_src[f] < (int)m.size()) prev_tag_row[f] = m[mx.f_src[f]];
+    }
+  }
   const arslam_soa_problem *p = side == ARSLAM_ELIM_TAGS ? &swapped : side == ARSLAM_ELIM_MIXED ? &mx.soa : p_in;
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
   double tp[6] = {now_s(), 0, 0, 0, 0, 0};
@@ -743,7 +760,7 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
     t_host = now_s();
     // (a grown pointer-keyed problem: a fresh order takes the faster separator search)
     L = arslam::reduced_layout(h, opt.reduced_ordering, opt.cholesky_skip_zero_tiles != 0, nullptr, nullptr,
-                               can_reuse ? &prev_tag_row : nullptr, prev_order_edges, reuse_order);
+                               can_reuse ? &prev_tag_row : nullptr, prev_order_edges, reuse_order, by_identity);
     // A kept order whose tile elimination tree grew taller than the fresh
     // order's by more than a level (new co-visibility across its separators:
     // 10 -> 14 -> 20 levels within a few loads of the incremental cfg2 flow)
@@ -761,12 +778,21 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
   nb_global = h.nb_global;
   slot_free = h.slot_free;
   x0 = h.x0;
+  last_order_reused = L.order_reused;
   if (!L.order_reused) {
     prev_order_nc = h.nc;
     prev_order_height = L.nR > 0 ? etree_height(L) : 0;
   }
   prev_tag_row = L.tag_row;
   prev_order_edges = L.order_edges;
+  prev_mx_tag_row.clear();
+  prev_mx_cap_row.clear();
+  if (side == ARSLAM_ELIM_MIXED) {
+    prev_mx_tag_row.assign(p_in->n_tag, -1);
+    prev_mx_cap_row.assign(p_in->n_cap, -1);
+    for (size_t f = 0; f < mx.f_src.size(); ++f)
+      (mx.f_is_cap[f] ? prev_mx_cap_row : prev_mx_tag_row)[mx.f_src[f]] = L.tag_row[f];
+  }
   if (!multi()) covis_build(h, L);
   prev_ordering = opt.reduced_ordering;
   prev_skip = opt.cholesky_skip_zero_tiles;
@@ -1853,6 +1879,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
   s->split_max_rank_work = split_max_rank_work;
   s->split_total_work = split_total_work;
   s->n_active_ranks = multi() ? split_active : 1;
+  s->order_reused = last_order_reused ? 1 : 0;
 }
 
 // ===========================================================================
@@ -2080,6 +2107,8 @@ int arslam_lm_reset(arslam_lm *h) {
     h->pk_dirty = true;
     h->pk_loaded = false;
     h->prev_tag_row.clear();
+    h->prev_mx_tag_row.clear();
+    h->prev_mx_cap_row.clear();
   });
 }
 

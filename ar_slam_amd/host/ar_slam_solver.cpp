@@ -464,10 +464,12 @@ void ArSlamSolver::localizeMany(unsigned first_loc_cap_idx) {   // :888-901, eac
 void ArSlamSolver::optimize(const Capture &capture) {   // :1001-1018
   arslam_lm_options o = options_;
   o.max_num_iterations = 50;                      // :1004
-  // DENSE_SCHUR (:1011): captures unless the caller asked for a side or for
-  // Ceres' exact (mixed) set -- one side keeps the appended-plan path of the
-  // growing problem
-  if (o.elimination == ARSLAM_ELIM_AUTO) o.elimination = ARSLAM_ELIM_CAPTURES;
+  // DENSE_SCHUR (:1011) eliminates Ceres' own e-block set: ARSLAM_ELIM_MIXED
+  // unless the caller asked for a side (round 6: a grown problem whose new
+  // captures see only reduced tags appends to the set, and a reload keeps the
+  // earlier order by block -- the cfg2 flow 1.16x the all-captures one,
+  // DESIGN.md §2, §7b)
+  if (o.elimination == ARSLAM_ELIM_AUTO) o.elimination = ARSLAM_ELIM_MIXED;
   o.minimizer_progress_to_stdout = verbose_ ? 1 : 0;
   check(arslam_lm_set_options(problem_, &o));
   SolveRecord rec;

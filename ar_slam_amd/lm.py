@@ -47,7 +47,7 @@ EXPORTS = ["arslam_lm_options_init", "arslam_lm_create", "arslam_lm_destroy",
            "arslam_debug_residual_jacobian", "arslam_debug_dense_llt", "arslam_debug_dense_llt_ex",
            "arslam_debug_angle_axis_rotate", "arslam_lm_debug_force_indefinite",
            "arslam_lm_debug_force_multirank", "arslam_lm_debug_break_dependency", "arslam_lm_debug_tag_pair_tile",
-           "arslam_debug_reduced_plan", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
+           "arslam_debug_reduced_plan", "arslam_debug_reduced_plan_side", "arslam_debug_schur_stamps", "arslam_debug_ceres_e_blocks",
            "arslam_debug_mixed_groups",
            "arslam_debug_dag_simulate", "arslam_debug_dag_simulate_started", "arslam_debug_dag_workgroup_limit",
            "arslam_debug_dag_fault_detail", "arslam_debug_box_fingerprint",
@@ -132,7 +132,8 @@ class Summary(C.Structure):
                 ("split_total_work", C.c_double), ("t_factor_own_ms", C.c_double),
                 ("t_factor_top_ms", C.c_double),
                 ("n_iters", C.c_int), ("iters", Iteration * (MAX_ITERS + 1)),
-                ("setup_phase_s", C.c_double * 5), ("comm_calls", C.c_long), ("n_active_ranks", C.c_int)]
+                ("setup_phase_s", C.c_double * 5), ("comm_calls", C.c_long), ("n_active_ranks", C.c_int),
+                ("order_reused", C.c_int)]
 
     def to_dict(self):
         its = [{f: getattr(self.iters[i], f) for f, _ in Iteration._fields_}
@@ -536,6 +537,18 @@ def debug_reduced_plan(camera, cap, tag, obs_cap, obs_tag, corners, camera_const
     _check(lib().arslam_debug_reduced_plan(C.byref(A.s), ordering, skip_zero_tiles, C.byref(info),
                                            tag_row.ctypes.data_as(_ip)))
     return {f: getattr(info, f) for f, _ in PlanInfo._fields_}, tag_row[:A.tag.shape[0]]
+
+
+def debug_reduced_plan_side(camera, cap, tag, obs_cap, obs_tag, corners=None, elimination=ELIM_CAPTURES):
+    """Host-only: the reduced layout and tile plan of a fresh one-rank load under elimination
+    (ELIM_CAPTURES, ELIM_TAGS or ELIM_MIXED).  Returns (side used, info dict)."""
+    if corners is None:
+        corners = np.zeros((len(obs_cap), 8))
+    A = _Soa(camera, cap, tag, obs_cap, obs_tag, corners, False, None, None)
+    info = PlanInfo()
+    side = lib().arslam_debug_reduced_plan_side(C.byref(A.s), elimination, C.byref(info))
+    _check(min(side, 0))
+    return side, {f: getattr(info, f) for f, _ in PlanInfo._fields_}
 
 
 def box_fingerprint(device=0):

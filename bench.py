@@ -101,6 +101,10 @@ def bench_incremental(name="cfg2"):
             "wall_s": wall, "solves": n, "lm_iterations": sum(d["num_linear_solves"] for d in sums),
             "setup_ms_per_solve": 1e3 * setup / n, "minimizer_ms_per_solve": 1e3 * mini / n,
             "setup_kinds": {"full load": kinds[0], "values only": kinds[1], "appended (plan kept)": kinds[2]},
+            # (the mirror's default: Ceres' own e-block set, ARSLAM_ELIM_MIXED -- all tags, then mixed)
+            "elimination_used": {name: sum(d["elimination_used"] == e for d in sums)
+                                 for e, name in ((lm.ELIM_CAPTURES, "captures"), (lm.ELIM_TAGS, "tags"),
+                                                 (lm.ELIM_MIXED, "mixed"))},
             "final_rms_px": sums[-1]["final_rms_px"]}
 
 

@@ -168,6 +168,8 @@ typedef struct {
   long comm_calls;              /* multi-rank: collectives this rank made during the solve */
   int n_active_ranks;           /* ranks that own subtrees of the split (the others own only captures that
                                    see top tags alone); 1 on one rank */
+  int order_reused;             /* the last full load kept the earlier elimination order (an incremental
+                                   reload: 1) or computed a fresh one (0) */
 } arslam_lm_summary;
 
 /* Whole problem in struct-of-arrays form (bulk / benchmark path). */

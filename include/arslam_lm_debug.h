@@ -111,6 +111,11 @@ int arslam_debug_mixed_groups(const arslam_soa_problem *p, int out[4], unsigned 
 
 int arslam_debug_reduced_plan(const arslam_soa_problem *p, int ordering, int skip_zero_tiles,
                               arslam_plan_info *info, int *tag_row);
+/* Host only: the reduced layout (nested dissection, sparse tiles) and tile plan
+ * of p's device problem under elimination (ARSLAM_ELIM_CAPTURES, _TAGS or
+ * _MIXED: Ceres' set), built as a fresh one-rank load builds it.  Returns the
+ * side used (MIXED falls back to a whole side as the load does) or an error. */
+int arslam_debug_reduced_plan_side(const arslam_soa_problem *p, int elimination, arslam_plan_info *info);
 
 /* Host only: one simulated interleaving of n_workers workgroups running the
  * persistent executor's protocol on the one-rank plan of p (policy 0 random,

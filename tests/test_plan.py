@@ -80,6 +80,23 @@ def test_nested_dissection_beats_band_on_cfg3(L):
     assert again == nd                               # deterministic
 
 
+@pytest.mark.parametrize("k", [600, 1000])
+def test_mixed_set_layout_is_as_shallow_as_captures(L, k):
+    """Ceres' mixed set on a cfg2 prefix (ELIM_MIXED): its reduced side holds tags and the
+    captures next to eliminated tags, about as many rows as eliminating every capture.  The
+    geometric separators place those captures at the mean of the tags they see -- at their own
+    translation slot (minus the camera centre) the cuts were of a mirrored cloud and the tree
+    grew taller (round 6: cfg2[:1000] 13 levels / 272 tiles against 11 / 205)."""
+    g = synth.prefix_graph(synth.config_graph("cfg2"), k)
+    args = (g.camera, g.cap, g.tag, g.obs_cap, g.obs_tag)
+    side_c, c = L.debug_reduced_plan_side(*args, elimination=L.ELIM_CAPTURES)
+    side_m, m = L.debug_reduced_plan_side(*args, elimination=L.ELIM_MIXED)
+    assert (side_c, side_m) == (L.ELIM_CAPTURES, L.ELIM_MIXED)
+    assert c["dag_valid"] and m["dag_valid"]
+    assert m["n_levels"] <= c["n_levels"] + 1
+    assert m["n_factor_tiles"] <= 1.3 * c["n_factor_tiles"] * m["n_reduced"] / c["n_reduced"]
+
+
 def test_invalid_problem_rejected_on_host(L):
     g = synth.config_graph("tiny")
     bad = g.obs_tag.copy()

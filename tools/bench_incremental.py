@@ -59,6 +59,13 @@ for i in range(n):
     mini += d["minimizer_time_s"]
     iters += d["num_linear_solves"]
 last = s.last_summary()
+if os.environ.get("ARSLAM_INC_DUMP"):   # debug: one line per Solve
+    with open(os.environ["ARSLAM_INC_DUMP"], "w") as f:
+        for i in range(n):
+            d = s.solve_summary(i)
+            f.write(json.dumps({k: d[k] for k in ("elimination_used", "setup_kind", "setup_time_s", "minimizer_time_s",
+                                                  "num_linear_solves", "n_factor_tiles", "n_levels", "n_reduced",
+                                                  "order_reused", "t_cholesky_ms")}) + "\n")
 print(json.dumps({"flow": f"solveIncremental, {name}: {g.n_cap} captures / {g.n_tag} tags, one message per capture",
                   "wall_s": wall, "solves": n, "lm_iterations": iters,
                   "setup_ms_per_solve": 1e3 * setup / n, "minimizer_ms_per_solve": 1e3 * mini / n,
