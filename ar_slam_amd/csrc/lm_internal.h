@@ -53,6 +53,14 @@ constexpr int kDagWorkgroupsPerCu = 2;
 constexpr int kWave = 64;
 constexpr int kTile = 64;          // reduced-system Cholesky tile
 constexpr int kRowStride = 14;     // LDS row: 13 Jacobian entries + residual
+// The stored copy of a row (DevProblem::jrows): 11 values.  The capture- and
+// tag-translation columns of a row are the same three numbers (d/dt_c =
+// d/dt_t = P M_c: the point is R_t corner + t_t + t_c), so columns 7..9 are
+// not stored; column j of the row is stored column jrow_col(j).
+constexpr int kJStored = 11;
+__host__ __device__ constexpr int jrow_col(int j) {
+  return j <= 6 ? j : j <= 9 ? j - 6 : j <= 12 ? j - 3 : 10;
+}
 // The per-capture kernels take a capture's observations through LDS in
 // chunks of kObsChunk (8 observations = one wave's 64 residual rows), so
 // k_linearize, k_backsub and the cost take any number of observations per
@@ -150,7 +158,8 @@ struct DevProblem {
   // (x^2, the f-side step) count each slot on one rank, and the final tag
   // values are gathered from these
   const unsigned char *f_own = nullptr;
-  double *jrows;             // [8 nb kRowStride] unscaled Jacobian rows + residual at the linearization point
+  double *jrows;             // [8 nb kJStored] unscaled Jacobian rows + residual at the linearization point
+                             // (column-major per capture: (row, jrow_col(j)) at 8 o0 kJStored + jrow_col(j) 8k + row)
   double *cap_ui;            // [36 nc] (U_c + D_c^2)^{-1} of the current step (k_schur -> k_backsub)
 };
 

@@ -74,9 +74,9 @@ __device__ __forceinline__ double lm_d2(const double *diag, long slot, double ra
 // (nrows rows in all, observations from o0): 13 Jacobian entries (scaled by
 // the Jacobi scale if scale != nullptr) and the residual in column 13.
 // With gout, the unscaled rows are also stored there column-major per capture
-// (entry (row, j) at gout + 8 o0 kRowStride + j nrows + row): the Schur and
-// back-substitution passes at the same point reload them instead of
-// re-evaluating the projection.
+// (entry (row, j) at gout + 8 o0 kJStored + jrow_col(j) nrows + row, the
+// translation columns once): the Schur and back-substitution passes at the
+// same point reload them instead of re-evaluating the projection.
 __device__ __forceinline__ void fill_rows(const DevProblem &P, const double *x, const double *scale, int c,
                           int o0, int row0, int nr, int nrows, double *rows, double *gout = nullptr) {
   const double *cam = x;
@@ -117,10 +117,11 @@ __device__ __forceinline__ void fill_rows(const DevProblem &P, const double *x, 
     }
     dst[13] = r;
     if (gout) {
-      double *g = gout + 8L * o0 * kRowStride + row;
+      double *g = gout + 8L * o0 * kJStored + row;
 #pragma unroll
-      for (int j = 0; j < 13; ++j) g[(long)j * nrows] = J[j];
-      g[13L * nrows] = r;
+      for (int j = 0; j < 13; ++j)
+        if (j < 7 || j > 9) g[(long)jrow_col(j) * nrows] = J[j];
+      g[(long)jrow_col(13) * nrows] = r;
     }
   }
 }
@@ -136,12 +137,14 @@ __device__ __forceinline__ void load_rows_q(const DevProblem &P, const double *s
   const double *sc = scale + slot_cap(P, c);
   for (int lr = threadIdx.x; lr < nr; lr += kWave) {
     const int row = row0 + lr;
-    const double *g = P.jrows + 8L * o0 * kRowStride + row;
+    const double *g = P.jrows + 8L * o0 * kJStored + row;
     const int t = P.obs_tag[o0 + (row >> 3)];
     const int tr = P.tag_row[t];
-    double v[14];
+    double u[kJStored], v[14];
 #pragma unroll
-    for (int j = 0; j < 14; ++j) v[j] = g[(long)j * nrows];
+    for (int j = 0; j < kJStored; ++j) u[j] = g[(long)j * nrows];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) v[j] = u[jrow_col(j)];
     const double *st = scale + slot_tag(P, t);
     double yt[6];
 #pragma unroll
@@ -165,6 +168,31 @@ __device__ __forceinline__ void load_rows_q(const DevProblem &P, const double *s
     qv[lr] = q;
   }
 }
+
+#ifdef ARSLAM_BACKSUB_RECOMPUTE
+// load_rows_q's rows evaluated again at x instead of read back (the same
+// products in the same order: fill_rows scales J as load_rows_q scales the
+// stored copy, and q is formed from the row as there)
+__device__ __forceinline__ void eval_rows_q(const DevProblem &P, const double *x, const double *scale, const double *yF,
+                                            double yf, int c, int o0, int row0, int nr, int nrows, double *rows,
+                                            double *qv) {
+  fill_rows(P, x, scale, c, o0, row0, nr, nrows, rows);
+  for (int lr = threadIdx.x; lr < nr; lr += kWave) {
+    const int row = row0 + lr;
+    const int tr = P.tag_row[P.obs_tag[o0 + (row >> 3)]];
+    const double *d = rows + (long)lr * kRowStride;
+    double q = d[0] * yf;
+    if (tr >= 0) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) q += d[7 + j] * yF[tr + j];
+    }
+    qv[lr] = q;
+  }
+}
+#define ARSLAM_BACKSUB_ROWS(...) eval_rows_q(P, x, __VA_ARGS__)
+#else
+#define ARSLAM_BACKSUB_ROWS(...) load_rows_q(P, __VA_ARGS__)
+#endif
 
 // (a,b) of the e-th entry of the upper triangle of a 6x6 matrix, row-major
 __device__ __forceinline__ void upper6(int e, int &a, int &b) {
@@ -498,13 +526,15 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
   // tag scales), so the two latencies overlap
   const int li = lane & 15, lk = lane >> 4;
   const bool valid = li < 14;
-  const double *jb = P.jrows + 8L * o0 * kRowStride;
+  // (column li of the row is stored column jrow_col(li): lanes 7..9 read the
+  // translation column lanes 1..3 read)
+  const double *jb = P.jrows + 8L * o0 * kJStored + (long)jrow_col(min(li, 13)) * nrows;
   double jv[16];
 #pragma unroll
   for (int u = 0; u < 8; ++u)
 #pragma unroll
     for (int st = 0; st < 2; ++st)
-      jv[2 * u + st] = (valid && u < k) ? jb[(long)li * nrows + 8 * u + 4 * st + lk] : 0.0;
+      jv[2 * u + st] = (valid && u < k) ? jb[8 * u + 4 * st + lk] : 0.0;
   static_assert(kObsChunk == 8, "k_schur's operand registers hold eight observations");
   // the tag scales and blocks of a chunk of kObsChunk observations (reloaded
   // beside the operand registers in the Gram loop)
@@ -569,7 +599,7 @@ __global__ __launch_bounds__(kWave) void k_schur(DevProblem P, const double *__r
         for (int u = 0; u < 8; ++u)
 #pragma unroll
           for (int st = 0; st < 2; ++st)
-            jv[2 * u + st] = (valid && q + u < k) ? jb[(long)li * nrows + 8 * (q + u) + 4 * st + lk] : 0.0;
+            jv[2 * u + st] = (valid && q + u < k) ? jb[8 * (q + u) + 4 * st + lk] : 0.0;
         stage_chunk(q);   // (the previous iteration ended at a wave barrier: its reads are done)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1121,7 +1151,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
   // chunks in LDS (U, v), nothing held in registers across the row loads
   auto chunk = [&](int r0) __attribute__((always_inline)) {
     const int nr = min(kChunkRows, nrows - r0);
-    load_rows_q(P, scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
+    ARSLAM_BACKSUB_ROWS(scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
     __syncthreads();
     const int va = reuse_ui ? lane - 32 : lane - 21;
     if (!reuse_ui && lane < 21) {
@@ -1195,7 +1225,7 @@ __global__ __launch_bounds__(kWave) void k_backsub(DevProblem P, const double *_
     for (int r0 = 0; r0 < nrows; r0 += kChunkRows) {
       const int nr = min(kChunkRows, nrows - r0);
       __syncthreads();
-      load_rows_q(P, scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
+      ARSLAM_BACKSUB_ROWS(scale, yF, yf, c, o0, r0, nr, nrows, rows, qv);
       __syncthreads();
       model(nr);
     }

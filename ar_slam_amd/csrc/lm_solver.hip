@@ -938,7 +938,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   d_xa.alloc(n); d_xb.alloc(n); d_xbest.alloc(n);
   d_g.alloc(n); d_colnorm.alloc(n); d_scale.alloc(n); d_diag.alloc(n);
   d_obs_tg.alloc(std::max(12L * nb, 1L));
-  d_jrows.alloc(std::max(8L * arslam::kRowStride * nb, 1L));
+  d_jrows.alloc(std::max(8L * arslam::kJStored * nb, 1L));
   d_cap_ui.alloc(std::max(36L * nc, 1L));
   d_parts.alloc((size_t)arslam::NPART * std::max(nc, 1));
   n_fparts = (int)((std::max(nR, 1L) + 255) / 256);

@@ -39,6 +39,8 @@ def test_residual_jacobian_matches_oracle(lm, oracle):
         np.testing.assert_allclose(r[i], ro, rtol=1e-12, atol=1e-9)
         scale = np.abs(Jo).max(axis=1, keepdims=True) + 1e-300
         assert np.max(np.abs(J[i] - Jo) / scale) < 1e-12
+    # the capture- and tag-translation columns are the same numbers (the stored Jacobian keeps them once)
+    assert np.array_equal(J[..., 3:6], J[..., 9:12])   # ([f, 0, 0, t_c, w_c, t_t, w_t])
 
 
 @pytest.mark.parametrize("executor", [0, 1])

@@ -20,7 +20,8 @@ def child(cfg, steps):
     g = synth.config_graph(cfg)
     lm.warm_up()
     rp = lm.ResidentProblem(camera=g.camera, cap=g.cap, tag=g.tag, obs_cap=g.obs_cap, obs_tag=g.obs_tag,
-                            corners=g.corners, kernel_timing=1, phase_timing=0)
+                            corners=g.corners, kernel_timing=1,
+                            phase_timing=int(os.environ.get("AB_PHASES", "0")))   # (AB_PHASES=1: per-phase device ms)
     rp.solve()
     t0 = time.perf_counter()
     ss = [rp.solve() for _ in range(steps)]
@@ -30,8 +31,10 @@ def child(cfg, steps):
     h = hashlib.sha256(np.ascontiguousarray(rp.camera).tobytes() + np.ascontiguousarray(rp.cap).tobytes() +
                        np.ascontiguousarray(rp.tag).tobytes()).hexdigest()[:12]
     li = lm.library_info()
+    ph = {k[2:-3]: round(sum(s[k] for s in ss) / len(ss), 4) for k in
+          ("t_linearize_ms", "t_schur_ms", "t_cholesky_ms", "t_solve_ms", "t_backsub_ms")}
     print(json.dumps({"factor_us": dom * 1e3, "it_s": it / el, "cost": repr(ss[-1]["final_cost"]), "digest": h,
-                      "lib": f"{li['file']} sha {li['sha256']}", "build": li["build"]}))
+                      "lib": f"{li['file']} sha {li['sha256']}", "build": li["build"], "phases": ph}))
 
 
 def main():
@@ -56,7 +59,8 @@ def main():
             d = json.loads(out.stdout.strip().splitlines()[-1])
             res[n].append(d)
             print(f"round {r} {n:12s} factor {d['factor_us']:7.1f} us  {d['it_s']:7.1f} it/s  cost {d['cost']}  {d['digest']}"
-                  f"  [{d['lib']}, build {d['build']}]", flush=True)
+                  f"  [{d['lib']}, build {d['build']}]" + (f"  phases {d['phases']}" if os.environ.get("AB_PHASES") else ""),
+                  flush=True)
     for n in names:
         if not res[n]:
             continue
