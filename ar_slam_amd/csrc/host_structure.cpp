@@ -765,11 +765,15 @@ HostProblem host_problem(const arslam_soa_problem *p, const ReduceSumF64 &tag_de
   // tag CSR over the capture-major order
   h.tag_start.assign(nt + 1, 0);
   h.tag_obs.resize(nb);
+  h.obs_tpos.resize(nb);
   for (int q = 0; q < nb; ++q) h.tag_start[h.obs_tag[q] + 1]++;
   for (int t = 0; t < nt; ++t) h.tag_start[t + 1] += h.tag_start[t];
   {
     std::vector<int> fill(h.tag_start.begin(), h.tag_start.end() - 1);
-    for (int q = 0; q < nb; ++q) h.tag_obs[fill[h.obs_tag[q]]++] = q;
+    for (int q = 0; q < nb; ++q) {
+      h.obs_tpos[q] = fill[h.obs_tag[q]]++;
+      h.tag_obs[h.obs_tpos[q]] = q;
+    }
   }
   // free slots (global tag use over ranks)
   std::vector<double> tag_deg(nt + 1, 0.0);

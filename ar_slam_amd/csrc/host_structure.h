@@ -54,6 +54,7 @@ struct HostProblem {
   std::vector<int> blk_tag;         // tag of each (capture, local block)
   std::vector<int> tag_start;       // [nt+1] tag CSR over the capture-major order
   std::vector<int> tag_obs;         // [nb]
+  std::vector<int> obs_tpos;        // [nb] position of observation q in the tag CSR (tag_obs[obs_tpos[q]] = q)
   std::vector<double> corners;      // [8 nb] capture-major
   std::vector<unsigned char> slot_free, obs_active;
   std::vector<double> x0;           // [n] initial slots

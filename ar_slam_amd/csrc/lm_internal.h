@@ -132,7 +132,8 @@ struct DevProblem {
   const unsigned char *obs_active;   // [nb]
   const unsigned char *slot_free;    // [n]
   const int *tag_start;      // [nt+1]  CSR of observations by tag (capture-major order inside)
-  const int *tag_obs;        // [nb]
+  const int *obs_tpos;       // [nb]    position of each observation in that CSR: k_linearize's per-observation
+                             //         tag sums are stored tag-major (obs_tg), so a tag's are contiguous
   const double *corners;     // [nb*8]
   const int *tag_row;        // [nt]    first reduced row of tag t (6 rows), -1 if not free
   const int *row_slot;       // [nR]    parameter slot of a reduced row, -1 for padding rows

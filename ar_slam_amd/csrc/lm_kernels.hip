@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4, 8))) v
 #pragma unroll
       for (int rr = 0; rr < 8; ++rr) s += rq[rr * kRowStride + ca] * rq[rr * kRowStride + cb];
       if (it == 0) ocost[q] = 0.5 * s;
-      else obs_tg[12L * (o0 + q0 + q) + (it - 1)] = s;
+      else obs_tg[12L * P.obs_tpos[o0 + q0 + q] + (it - 1)] = s;   // (tag-major: k_lin_reduce reads a tag's at once)
     }
     // per capture: capture gradient (6: E'r), capture column norms (6), f gradient, f column norm
     if (lane < 14) {
@@ -368,13 +368,12 @@ __device__ __forceinline__ void tag_reduce_elem(const DevProblem &P, const doubl
   const int t = (int)(e / 12), j = (int)(e % 12);
   double s = 0.0;
   const int qa = P.tag_start[t], qb = P.tag_start[t + 1];
-  for (int q0 = qa; q0 < qb; q0 += 32) {   // 32 gathers in flight; summed in observation order
-    int o[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) o[u] = P.tag_obs[min(q0 + u, qb - 1)];
+  // (obs_tg is tag-major: the tag's observations, in observation order, are
+  // contiguous -- no index load in front of the sums' loads)
+  for (int q0 = qa; q0 < qb; q0 += 32) {   // 32 loads in flight; summed in observation order
     double v[32];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) v[u] = obs_tg[12L * o[u] + j];
+    for (int u = 0; u < 32; ++u) v[u] = obs_tg[12L * min(q0 + u, qb - 1) + j];
 #pragma unroll
     for (int u = 0; u < 32; ++u) s += (q0 + u < qb) ? v[u] : 0.0;
   }

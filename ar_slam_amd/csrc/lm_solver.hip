@@ -260,7 +260,7 @@ struct arslam_lm {
   // uploaded arrays (pointers into `upload`, re-laid out by every load)
   UploadArena upload;
   int *u_cap_start = nullptr, *u_obs_tag = nullptr, *u_obs_lblk = nullptr, *u_cap_blk_start = nullptr,
-      *u_blk_tag = nullptr, *u_tag_start = nullptr, *u_tag_obs = nullptr, *u_tag_row = nullptr,
+      *u_blk_tag = nullptr, *u_tag_start = nullptr, *u_obs_tpos = nullptr, *u_tag_row = nullptr,
       *u_row_slot = nullptr, *u_fslot_row = nullptr, *u_dest_start = nullptr, *u_big_caps = nullptr;
   unsigned char *u_f_own = nullptr;
   unsigned char *u_cap_kind = nullptr;   // ARSLAM_ELIM_MIXED: DevProblem::cap_kind, f_alias
@@ -861,7 +861,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   upload.add(&u_cap_blk_start, h.cap_blk_start.data(), nc + 1);
   upload.add(&u_blk_tag, h.blk_tag.data(), h.blk_tag.size());
   upload.add(&u_tag_start, h.tag_start.data(), nt + 1);
-  upload.add(&u_tag_obs, h.tag_obs.data(), nb);
+  upload.add(&u_obs_tpos, h.obs_tpos.data(), nb);
   upload.add(&u_obs_active, h.obs_active.data(), nb);
   upload.add(&u_slot_free, h.slot_free.data(), n);
   upload.add(&u_corners, h.corners.data(), 8L * nb);
@@ -983,7 +983,7 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   P.cap_start = u_cap_start; P.obs_tag = u_obs_tag; P.obs_lblk = u_obs_lblk;
   P.cap_blk_start = u_cap_blk_start; P.blk_tag = u_blk_tag;
   P.obs_active = u_obs_active; P.slot_free = u_slot_free;
-  P.tag_start = u_tag_start; P.tag_obs = u_tag_obs; P.corners = u_corners;
+  P.tag_start = u_tag_start; P.obs_tpos = u_obs_tpos; P.corners = u_corners;
   P.tag_row = u_tag_row; P.row_slot = u_row_slot;
   P.tile_id = plan.tile_id; P.T = plan.T;
   P.tile_class = multi() && has_f ? plan.tile_class : nullptr;
