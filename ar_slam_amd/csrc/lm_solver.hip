@@ -6,6 +6,7 @@
 // (ar_slam_util.cpp:1001-1018).  Only scalars cross
 // PCIe per step (cost, model cost change, norms, the Cholesky flag); the
 // problem, the parameters and the reduced system stay resident in HBM.
+#include "host_threads.h"
 #include "lm_internal.h"
 #include "arslam_lm.h"
 #include "arslam_lm_debug.h"
@@ -458,6 +459,7 @@ struct arslam_lm {
   // problem, the others unchanged: the gather plan is extended, not rebuilt)
   void upload_problem(const arslam::HostProblem &h, const arslam::ReducedLayout &L, int extend_from = -1);
   arslam::SchurGather sg;   // the loaded problem's Schur gather plan
+  bool sg_ready = false;    // load(): sg was built beside the tile plan (upload_problem keeps it)
   bool try_extend(const arslam_soa_problem *p);
   bool try_extend_mixed(const arslam_soa_problem *p);
   arslam::ReducedLayout lay;      // the loaded layout (one rank), kept for try_extend
@@ -793,17 +795,32 @@ void arslam_lm::load(const arslam_soa_problem *p_in) {
     for (size_t f = 0; f < mx.f_src.size(); ++f)
       (mx.f_is_cap[f] ? prev_mx_cap_row : prev_mx_tag_row)[mx.f_src[f]] = L.tag_row[f];
   }
-  if (!multi()) covis_build(h, L);
   prev_ordering = opt.reduced_ordering;
   prev_skip = opt.cholesky_skip_zero_tiles;
   tp[2] = now_s();
   scalar_flops = L.scalar_flops;
   nR = L.nR;
   has_f = nR > 0;
-  if (has_f) {
+  sg_ready = false;
+  if (has_f && !multi()) {
+    // the Schur gather plan (host only, from h and L) on a second thread while
+    // this one builds and uploads the tile plan (its HIP calls stay on the
+    // thread whose device is current) and does the co-visibility bookkeeping
+    N = L.N;
+    arslam::SchurGather sg_new;
+    arslam::host_fork2(
+        true, [&] { sg_new = arslam::schur_gather_plan(h, L); },
+        [&] {
+          arslam::llt_plan_build(plan, L.T, N, L.pattern, stream, nullptr);
+          covis_build(h, L);
+        });
+    sg = std::move(sg_new);
+    sg_ready = true;
+  } else if (has_f) {
     N = L.N;
     arslam::llt_plan_build(plan, L.T, N, L.pattern, stream, multi() ? &col_class : nullptr);
   } else {
+    if (!multi()) covis_build(h, L);
     N = 0;
     arslam::llt_plan_free(plan);
   }
@@ -850,8 +867,10 @@ void arslam_lm::upload_problem(const arslam::HostProblem &h, const arslam::Reduc
   static const bool prof = std::getenv("ARSLAM_SETUP_PROFILE") != nullptr;   // debug: setup phases
   const double tu0 = prof ? now_s() : 0.0;
   if (!has_f) sg = arslam::SchurGather{};
+  else if (sg_ready) {}   // (load: built beside the tile plan)
   else if (extend_from >= 0 && (int)sg.cap_off.size() == extend_from + 1) arslam::schur_gather_extend(sg, h, L, extend_from);
   else sg = arslam::schur_gather_plan(h, L);
+  sg_ready = false;
   const double tu1 = prof ? now_s() : 0.0;
   const int n_dest = has_f ? (int)sg.dest_start.size() - 1 : 0;
   const int n_items = (int)sg.items.size() / 4, n_splits = (int)sg.splits.size() / 4;

@@ -77,14 +77,14 @@ def cpu_baseline(g, threads, name):
                       f"{dt:.1f} s"}
 
 
-def bench_incremental(name="cfg2"):
+def bench_incremental(name="cfg2", elimination=0):
     """The reference's real flow (ArSlamSolver::solveIncremental, ar_slam_util.cpp:629-742): one
     Detections message per capture, each followed by a full Solve of the problem so far (:736),
     through the C++ host mirror and the pointer-keyed C-ABI (the drop-in path, host buffers, setup
     included).  Reported beside the headline line, never as `value`."""
     from ar_slam_amd import lm, synth
     g = synth.config_graph(name)
-    s = lm.SlamSolver()
+    s = lm.SlamSolver(elimination=elimination)   # (0: the mirror's default, Ceres' exact set)
     s.set_camera(g.camera)
     t0 = time.perf_counter()
     for c in range(g.n_cap):
@@ -570,6 +570,8 @@ def main():
         if world == 1 and not args.no_incremental and args.config == "cfg3":
             print("bench: incremental cfg2 flow", file=sys.stderr, flush=True)
             out["incremental_cfg2"] = bench_incremental("cfg2")
+            # the same flow eliminating every capture (rounds 3-5's default)
+            out["incremental_cfg2_captures"] = bench_incremental("cfg2", elimination=1)
         if world == 1 and args.config == "cfg3" and not args.no_localize:
             print("bench: cfg5 localize batch", file=sys.stderr, flush=True)
             out["localize_cfg5"] = bench_localize(args, world, rank, side=True)
