@@ -606,8 +606,9 @@ struct arslam_localizer {
     if (opt.device >= 0 && opt.device != cur) hip_check(hipSetDevice(opt.device), "hipSetDevice");
     if (!stream) {
       hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
-      hip_check(hipEventCreate(&ev0), "hipEventCreate");
-      hip_check(hipEventCreate(&ev1), "hipEventCreate");
+      // (timing only: no system-scope fence at the records)
+      hip_check(hipEventCreateWithFlags(&ev0, hipEventDisableSystemFence), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&ev1, hipEventDisableSystemFence), "hipEventCreate");
     }
   }
 
