@@ -338,8 +338,10 @@ void launch_linearize(const DevProblem &P, const double *x, double *g, double *c
                       double *obs_tg, double *parts, hipStream_t s);
 // k_linearize's reductions in one launch: the per-capture partials into
 // out[0..NPART+1] (launch_reduce_parts without fparts) and the tag slots' g and colnorm
+// (save: also the cost and fixed cost, out[P_COST], out[P_FIXED], into save[0..1])
 void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
-                       const double *parts, double *out, hipStream_t s, double *hout = nullptr);
+                       const double *parts, double *out, hipStream_t s, double *hout = nullptr,
+                       double *save = nullptr);
 struct LmDiagArgs;
 // (ld: also the LM diagonal from the new scale, ld->diag / dmin / dmax)
 void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale,
@@ -420,7 +422,25 @@ struct AgFields {
   }
 };
 void launch_ag_put(const double *src, const AgFields &fl, double *ag, int nranks, int rank, hipStream_t s);
-void launch_ag_reduce(const double *ag, const AgFields &fl, double *dst, int nranks, hipStream_t s);
+// (several ranks) device ranges stored into page-locked host words by the
+// all-gather's combining launch itself, then the sequence number the host
+// polls (as one rank's reductions do): no copy launches, no event
+struct HostOut {
+  const double *src[3] = {};
+  double *dst[3] = {};
+  int len[3] = {};
+  int n = 0;
+  double *seq_word = nullptr;
+  double seq = 0.0;
+  void add(const double *s, double *d, int l) {
+    if (n >= 3) throw std::logic_error("HostOut: more than 3 ranges");
+    src[n] = s;
+    dst[n] = d;
+    len[n++] = l;
+  }
+};
+void launch_ag_reduce(const double *ag, const AgFields &fl, double *dst, int nranks, hipStream_t s,
+                      const HostOut *ho = nullptr);
 // The camera slots of g and colnorm from the reduced partials red (P_GF, P_CF),
 // then the norms over free parameter slots: out[0..2] = max|g|, sum g^2, sum x^2
 // over capture slots, out[3..5] the same over camera + tag slots.  out[7] is

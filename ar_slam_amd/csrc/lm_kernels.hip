@@ -1331,7 +1331,8 @@ __device__ __forceinline__ void reduce_parts_block(int p, const double *__restri
                                                    const double *__restrict__ fparts, int nfparts,
                                                    double *__restrict__ out, const int *__restrict__ flag,
                                                    double *red, double *__restrict__ hout,
-                                                   int *seq_done = nullptr, double seq = 0.0) {
+                                                   int *seq_done = nullptr, double seq = 0.0,
+                                                   double *__restrict__ save = nullptr) {
   const int t = threadIdx.x;
   const bool is_max = (p == P_YBAD || p == P_CBAD || p == NPART + 1);
   const double *src = p < NPART ? parts + (long)p * nc : fparts;
@@ -1359,6 +1360,7 @@ __device__ __forceinline__ void reduce_parts_block(int p, const double *__restri
     if (t == 0) {
       out[p] = r;
       if (hout) hout[p] = r;
+      if (save && p < 2) save[p] = r;   // (P_COST, P_FIXED)
     }
   }
   if (flag && p == 0 && t == 0) {   // rides along the step's one host read
@@ -1400,10 +1402,10 @@ __global__ __launch_bounds__(1024) void k_reduce_parts(const double *__restrict_
 __global__ __launch_bounds__(1024) void k_lin_reduce(DevProblem P, const double *__restrict__ obs_tg,
                                                      double *__restrict__ g, double *__restrict__ colnorm,
                                                      const double *__restrict__ parts, double *__restrict__ out,
-                                                     double *__restrict__ hout) {
+                                                     double *__restrict__ hout, double *__restrict__ save) {
   __shared__ double red[1024];
   if ((int)blockIdx.x < NPART + 2)
-    reduce_parts_block(blockIdx.x, parts, P.nc, nullptr, 0, out, nullptr, red, hout);
+    reduce_parts_block(blockIdx.x, parts, P.nc, nullptr, 0, out, nullptr, red, hout, nullptr, 0.0, save);
   else
     tag_reduce_elem(P, obs_tg, (long)(blockIdx.x - (NPART + 2)) * 1024 + threadIdx.x, g, colnorm);
 }
@@ -1551,16 +1553,27 @@ __global__ void k_ag_put(const double *__restrict__ src, AgFields fl, double *__
 
 // ... and their combination in rank order (sum, or max where fl.max bit f is
 // set), the same bits on every rank, written back to dst[idx[f]]
-__global__ void k_ag_reduce(const double *__restrict__ ag, AgFields fl, double *__restrict__ dst, int nranks) {
+__global__ void k_ag_reduce(const double *__restrict__ ag, AgFields fl, double *__restrict__ dst, int nranks,
+                            HostOut ho) {
   const int f = threadIdx.x;
-  if (f >= fl.n) return;
-  const bool mx = (fl.max >> f) & 1u;
-  double v = ag[f];
-  for (int r = 1; r < nranks; ++r) {
-    const double w = ag[r * kAgFields + f];
-    v = mx ? fmax(v, w) : v + w;
+  if (f < fl.n) {
+    const bool mx = (fl.max >> f) & 1u;
+    double v = ag[f];
+    for (int r = 1; r < nranks; ++r) {
+      const double w = ag[r * kAgFields + f];
+      v = mx ? fmax(v, w) : v + w;
+    }
+    dst[fl.idx[f]] = v;
   }
-  dst[fl.idx[f]] = v;
+  if (!ho.seq_word) return;
+  // the host's words (after every combined value: one block), fenced at
+  // system scope, then the sequence number the host polls
+  __syncthreads();
+  for (int q = 0; q < ho.n; ++q)
+    for (int e = f; e < ho.len[q]; e += blockDim.x) ho.dst[q][e] = ho.src[q][e];
+  __threadfence_system();
+  __syncthreads();
+  if (f == 0) __hip_atomic_store(ho.seq_word, ho.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // one thread per (observation, row): residual and 15-column Jacobian row
@@ -1617,10 +1630,10 @@ void launch_linearize(const DevProblem &P, const double *x, double *g, double *c
 }
 
 void launch_lin_reduce(const DevProblem &P, const double *obs_tg, double *g, double *colnorm,
-                       const double *parts, double *out, hipStream_t s, double *hout) {
+                       const double *parts, double *out, hipStream_t s, double *hout, double *save) {
   const unsigned tag_blocks = (unsigned)((12L * P.nt + 1023) / 1024);
   hipLaunchKernelGGL(k_lin_reduce, dim3(NPART + 2 + tag_blocks), dim3(1024), 0, s, P, obs_tg, g, colnorm, parts,
-                     out, hout);
+                     out, hout, save);
 }
 
 void launch_scale(const DevProblem &P, const double *colnorm, int jacobi, double *scale, hipStream_t s,
@@ -1778,8 +1791,9 @@ void launch_ag_put(const double *src, const AgFields &fl, double *ag, int nranks
                      nranks, rank);
 }
 
-void launch_ag_reduce(const double *ag, const AgFields &fl, double *dst, int nranks, hipStream_t s) {
-  hipLaunchKernelGGL(k_ag_reduce, dim3(1), dim3(kAgFields), 0, s, ag, fl, dst, nranks);
+void launch_ag_reduce(const double *ag, const AgFields &fl, double *dst, int nranks, hipStream_t s,
+                      const HostOut *ho) {
+  hipLaunchKernelGGL(k_ag_reduce, dim3(1), dim3(kAgFields), 0, s, ag, fl, dst, nranks, ho ? *ho : HostOut{});
 }
 
 void debug_residual_jacobian(int n, const double *cam, const double *cap, const double *tag,

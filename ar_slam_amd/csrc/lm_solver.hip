@@ -553,7 +553,7 @@ struct arslam_lm {
   static constexpr int kLinSave = 16 + 8 + 6 * arslam::kNormBlocks;   // d_red[kLinSave..+1]: the linearization's cost, fixed
   void complete_pending_lin();
   void lin_norms();   // k_slot_norms once the linearization's sums are final
-  void exchange_scalars(arslam::AgFields fl);   // (+ the pending norms), into d_red
+  void exchange_scalars(arslam::AgFields fl, arslam::HostOut *ho = nullptr);   // (+ the pending norms), into d_red
   void exchange_norms() {
     if (norms_pending) exchange_scalars(arslam::AgFields{});
   }
@@ -1279,17 +1279,14 @@ void arslam_lm::linearize_launch() {
   const bool direct = !multi();
   timers[PH_LIN].start(stream);
   arslam::launch_linearize(P, x, d_g.p, d_colnorm.p, d_obs_tg.p, d_parts.p, stream);
+  // (several ranks: this rank's partial cost and fixed cost also saved, the
+  // step's reductions reuse d_red, for the scalar exchange; the LM diagonal
+  // from the partial sums is final for the capture slots and this rank's own
+  // subtree tags -- all their observations are this rank's -- the rest
+  // follows the exchange, lin_norms)
   arslam::launch_lin_reduce(P, d_obs_tg.p, d_g.p, d_colnorm.p, d_parts.p, d_red.p, stream,
-                            direct ? h_lin.p : nullptr);
-  if (multi()) {
-    // this rank's partial sums: the cost and fixed cost saved (the step's
-    // reductions reuse d_red) for the scalar exchange; the LM diagonal from
-    // them is final for the capture slots and this rank's own subtree tags
-    // (all their observations are this rank's), the rest follows the
-    // exchange (lin_norms)
-    HIP_CHECK(hipMemcpyAsync(d_red.p + kLinSave, d_red.p, 2 * sizeof(double), hipMemcpyDeviceToDevice, stream));
-    lin_xpending = true;
-  }
+                            direct ? h_lin.p : nullptr, multi() ? d_red.p + kLinSave : nullptr);
+  if (multi()) lin_xpending = true;
   const arslam::LmDiagArgs ld{n, d_scale.p, d_colnorm.p, opt.min_lm_diagonal, opt.max_lm_diagonal, d_diag.p};
   lin_seq = direct ? next_seq(h_lin.p + 16 + arslam::kHostSeq) : 0.0;
   arslam::launch_slot_norms(P, d_red.p, d_g.p, d_colnorm.p, x, d_norms_p, stream, direct ? h_lin.p + 16 : nullptr,
@@ -1326,7 +1323,7 @@ void arslam_lm::complete_pending_lin() {
 // linearization's norms are pending, its capture-slot norms, all-gathered in
 // one SUM all-reduce and combined in rank order (k_ag_put / k_ag_reduce: the
 // same bits on every rank); the norms then go to h_lin like the rest of it.
-void arslam_lm::exchange_scalars(arslam::AgFields fl) {
+void arslam_lm::exchange_scalars(arslam::AgFields fl, arslam::HostOut *ho) {
   const bool with_norms = norms_pending;
   if (with_norms) {
     // the norms over the slots each rank holds (captures; its f-side slots)
@@ -1335,14 +1332,21 @@ void arslam_lm::exchange_scalars(arslam::AgFields fl) {
     fl.add(kLinSave, false);       // the linearization's cost
     fl.add(kLinSave + 1, false);   // ... and fixed cost
   }
-  if (fl.n == 0) return;
+  if (fl.n == 0 && !ho) return;   // (with ho the combining launch still stores the host words)
   d_ag.alloc((size_t)nranks * arslam::kAgFields);
   arslam::launch_ag_put(d_red.p, fl, d_ag.p, nranks, rank, stream);
   allreduce(d_ag.p, (size_t)nranks * arslam::kAgFields, ARSLAM_OP_SUM);
-  arslam::launch_ag_reduce(d_ag.p, fl, d_red.p, nranks, stream);
+  if (with_norms && ho) {   // (the combining launch stores them with the step's words)
+    h_lin.alloc(32);
+    ho->add(d_norms_p, h_lin.p + 16, 6);
+    ho->add(d_red.p + kLinSave, h_lin.p, 2);
+  }
+  arslam::launch_ag_reduce(d_ag.p, fl, d_red.p, nranks, stream, ho);
   if (with_norms) {
-    HIP_CHECK(hipMemcpyAsync(h_lin.p + 16, d_norms_p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p + kLinSave, 2 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    if (!ho) {
+      HIP_CHECK(hipMemcpyAsync(h_lin.p + 16, d_norms_p, 6 * sizeof(double), hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipMemcpyAsync(h_lin.p, d_red.p + kLinSave, 2 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    }
     norms_pending = false;
   }
 }
@@ -1766,7 +1770,7 @@ void arslam_lm::solve(arslam_lm_summary *s) {
     timers[PH_COST].start(stream);
     h_step.alloc(16);
     // (one rank: the scalars are also stored straight into the page-locked h_step)
-    const double step_seq = !multi() ? next_seq(h_step.p + arslam::kHostSeq) : 0.0;
+    double step_seq = !multi() ? next_seq(h_step.p + arslam::kHostSeq) : 0.0;
     arslam::launch_reduce_parts(d_parts.p, nc, d_fparts.p, n_fparts, d_red.p, stream, d_flag.p,
                                 !multi() ? h_step.p : nullptr, d_seq_done.p, step_seq);
     if (multi()) {
@@ -1780,15 +1784,17 @@ void arslam_lm::solve(arslam_lm_summary *s) {
         fl.add(f, false);
       for (int f : {(int)arslam::P_YBAD, (int)arslam::P_CBAD, arslam::NPART + 1, arslam::NPART + 2, arslam::NPART + 3})
         fl.add(f, true);
-      exchange_scalars(fl);
+      // the step's words (and a pending linearization's norms) stored to the
+      // host by the combining launch, then its sequence number
+      arslam::HostOut ho;
+      ho.add(d_red.p, h_step.p, arslam::NPART + 5);
+      step_seq = next_seq(h_step.p + arslam::kHostSeq);
+      ho.seq_word = h_step.p + arslam::kHostSeq;
+      ho.seq = step_seq;
+      exchange_scalars(fl, &ho);
     }
     timers[PH_COST].stop(stream);
-    if (multi()) {
-      HIP_CHECK(hipMemcpyAsync(h_step.p, d_red.p, (arslam::NPART + 5) * sizeof(double), hipMemcpyDeviceToHost, stream));
-      spin_sync();
-    } else {
-      flag_sync(h_step.p + arslam::kHostSeq, step_seq);
-    }
+    flag_sync(h_step.p + arslam::kHostSeq, step_seq);
     const double *red = h_step.p;
     // A stuck dependency wait of a persistent executor is a device fault, not
     // an indefinite system: fail loudly instead of shrinking the radius.
