@@ -1620,7 +1620,11 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
           }
         }
       }, X, fold_in, sh + 7, fast ? sh + 22 : nullptr);   // (a flag, not a nullable LDS pointer: hipcc mis-selects that null check)
-      if (tid == 0)
+      // A fused solve whose tile is already in X has no wait: the CU's flag
+      // stays up through it too (the solve is the link's next stretch of the
+      // chain; cfg3 k_factor_dag 621.9 -> 604.2 us, same-box A/B)
+      const bool keep_flag = sub.x >= 0 && sh[11] >= 3;
+      if (tid == 0 && !keep_flag)
         __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.trace && tid == 0) a.trace[8L * t + 5] = realtime();
       if (!ok && tid == 0) {
@@ -1682,6 +1686,8 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         int cas_old = 1;
         if (want) cas_old = atomicCAS(a.claimed + c, 0, 1);
         for (int st = max(s0, 2); st < 4; ++st) trsm_step(X, D, LTd, w, st, lane);
+        if (keep_flag && tid == 0)
+          __hip_atomic_store(cu_flag + cu_key, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef ARSLAM_FAST_CONT
         // whether A_kk comes in D, before the barrier; the claim's answer (the
         // CAS issued beside steps 1-2) is read by tid 0 after it, while wave 1
