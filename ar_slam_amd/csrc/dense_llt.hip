@@ -1522,6 +1522,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
       if (tid == 0 && !fast) {   // (a fast continuation: reset by its predecessor)
         sh[6] = 0;
         sh[12] = sh[13] = sh[14] = sh[15] = 0;   // the fused solve's column steps done per row block
+        sh[18] = 0;                              // beside the last panel: wave 1's take / skip (1 / 2)
       }
       // sh[11]: thirds of the tile loaded into X (3: all; set to 0 by the
       // pipeline's start).  Each wave decides for its own third: a wave that
@@ -1551,14 +1552,24 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
         }
         if (third_done || lds_get(sh + 11) >= 3) return;
         const int req = lds_get(sh + 6);
-        // not requested yet: wave 1 polls beside panels 1 and 2; beside the
-        // last panel every wave polls for itself and takes its own third
+        // not requested yet: wave 1 polls beside panels 1 and 2, and beside the
+        // last panel for all three waves (sh[18]); each then takes its own third
         bool take = req != 0 && req < p;
         if (req == 0) {
           if (p < 3) {
             if (wv == 1 && poll() && ln == 0) *as_lds(sh + 6) = p;
           } else {
-            take = poll();
+            // one decision for waves 1-3 (wave 1 polls), so that a wave that
+            // takes its third knows the other two do as well
+            if (!pf_src || pw1 - pw0 > 64) {
+              take = false;
+            } else if (wv == 1) {
+              take = poll();
+              lds_set(sh + 18, take ? 1 : 2);
+            } else {
+              lds_wait(sh + 18, 1);
+              take = lds_get(sh + 18) == 1;
+            }
           }
         }
         if (take) {   // the three thirds, one batch of sc1 loads each
@@ -1607,6 +1618,11 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
             ap_met = met && apf;
           }
         }
+        // beside the last panel every wave that took its third waits for the
+        // other two (they took theirs too), so the solve's steps 0-2 always run
+        // here once the tile is in, not only when all thirds landed by chance
+        // (cfg3 k_factor_dag 605.9 -> 601.3 us, cfg2 207.1 -> 205.6, same-box A/B)
+        if (p == 3 && third_done && sdone < 3) lds_wait(sh + 11, 3);
         if (kPipeFrom <= 3 && pf_src && p >= kPipeFrom && sdone < p && lds_get(sh + 11) >= 3) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
           for (int st = sdone; st < p; ++st) {
@@ -1744,6 +1760,7 @@ __global__ __launch_bounds__(256, kDagWorkgroupsPerCu) void k_factor_dag(DagArgs
           if (tid == 0) {
             sh[1] = 0;                                   // the target POTRF's bad flag
             sh[7] = sh[8] = sh[9] = sh[10] = sh[11] = 0;   // its fold count and pipeline flags
+            sh[18] = 0;
             sh[6] = 0;
             sh[12] = sh[13] = sh[14] = sh[15] = 0;
             if (a.trace) a.trace[8L * t + 3] = blockIdx.x | ((unsigned long long)(1 | 2 | (pref ? 4 : 0) | 8 | 16 | 32) << 32);
