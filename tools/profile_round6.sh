@@ -30,6 +30,6 @@ cp gpurun_out/p5/pmc_localize.json gpurun_out/pmc_localize_$t.json
 rm -rf gpurun_out/p5/pmc
 cat gpurun_out/pmc_localize_$t.json
 # the multi-rank path over a one-rank RCCL communicator (the RCCL calls on hardware)
-timeout -k 10 300 python bench.py --rccl-one-rank --steps 3 --warmup 1 --no-cpu-baseline --no-incremental \
+timeout -k 10 300 python bench.py --rccl-one-rank --steps 20 --warmup 3 --no-cpu-baseline --no-incremental \
   --no-localize --no-fingerprint > gpurun_out/bench_rccl_one_rank_$t.json 2> gpurun_out/bench_rccl_one_rank_$t.err || exit 1
 python3 -c "import json; d=json.loads(open('gpurun_out/bench_rccl_one_rank_$t.json').read().strip().splitlines()[-1]); print('rccl one rank', d['value'], d['transport'], d['split'])"
