@@ -62,7 +62,7 @@ double nd_beta() {
   // (debug sweeps; clamped to [0, 4]: a finite, non-negative weight)
   static const double b = std::getenv("ARSLAM_ND_BETA")
                               ? std::min(4.0, std::max(0.0, std::atof(std::getenv("ARSLAM_ND_BETA")) + 0.0))
-                              : 0.6;
+                              : 0.3;
   return b;
 }
 

@@ -230,11 +230,8 @@ def test_simulation_finds_the_deadlock_without_the_claim_cap(L, name):
         assert L.debug_dag_simulate(g, 2, seed=3, policy=pol)
 
 
-def test_fault_record_names_the_stuck_counter_and_its_producers(L):
-    """The record round 4's unexplained cfg3 fault would now carry (ticket 2772 timed out in its
-    dependency wait, DESIGN.md §9): the message names the task, the counter, the value seen and the
-    producers of the counter, with continuation targets marked -- here ticket 2772 = TRSM (80,69),
-    waiting for L_69,69 from ticket 2205, a POTRF two predecessors may claim."""
+def _fault_record_checks():
+    from ar_slam_amd import lm as L
     g = synth.config_graph("cfg3")
     rec = [2772, 1, 340, 0, 1, 3000, 3, 17]
     s = L.debug_dag_fault_detail(g, rec)
@@ -246,6 +243,23 @@ def test_fault_record_names_the_stuck_counter_and_its_producers(L):
     assert s3.endswith("smallest ticket timed out: 2205 (POTRF 69+TRSM)"), s3
     s2 = L.debug_dag_fault_detail(g, [2772, 1, 12625 * 0 + 2461 + 1620, 1, 2, 3000, 3, 17])
     assert "applied[1620] = 1 < 2" in s2 and "ticket 1981" in s2 and "ticket 2355" in s2, s2
+
+
+def test_fault_record_names_the_stuck_counter_and_its_producers(L):
+    """The record round 4's unexplained cfg3 fault would now carry (ticket 2772 timed out in its
+    dependency wait, DESIGN.md §9): the message names the task, the counter, the value seen and the
+    producers of the counter, with continuation targets marked -- here ticket 2772 = TRSM (80,69),
+    waiting for L_69,69 from ticket 2205, a POTRF two predecessors may claim.  The record belongs to
+    round 4's plan, i.e. to the dissection's height weight of then (ARSLAM_ND_BETA=0.6; the default
+    is 0.3 since round 6), so the checks run in a process of their own under that weight."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ARSLAM_ND_BETA="0.6", PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    code = "import sys; sys.path.insert(0, %r); from tests.test_plan import _fault_record_checks as f; f()" % root
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
 
 
 @pytest.mark.parametrize("name", ["small", "medium", "cfg2"])

@@ -43,9 +43,10 @@ def main():
     for r in range(rounds):
         for n in names:
             env = dict(os.environ)
-            if n.startswith("env:"):   # the default library under an environment switch: env:NAME=VALUE
-                k, v = n[4:].split("=", 1)
-                env[k] = v
+            if n.startswith("env:"):   # the default library under environment switches: env:NAME=VALUE[,NAME=VALUE]
+                for kv in n[4:].split(","):
+                    k, v = kv.split("=", 1)
+                    env[k] = v
             elif n != "base":
                 env["ARSLAM_LIB"] = os.path.join(ROOT, "ar_slam_amd", f"var_{n}.so")
             out = subprocess.run([sys.executable, __file__, "--child", cfg, "8"], env=env, capture_output=True,
