@@ -66,6 +66,22 @@ double nd_beta() {
   return b;
 }
 
+// The geometric cuts' quantile window [q, 1 - q] and the smaller side's
+// least share of the component (debug sweeps; clamped to [0.05, 0.45] and
+// [0, 0.45]).
+double nd_env(const char *name, double dflt, double lo, double hi) {
+  const char *e = std::getenv(name);
+  return e ? std::min(hi, std::max(lo, std::atof(e) + 0.0)) : dflt;
+}
+double nd_qlo() {
+  static const double q = nd_env("ARSLAM_ND_QLO", 0.3, 0.05, 0.45);
+  return q;
+}
+double nd_min_side() {
+  static const double f = nd_env("ARSLAM_ND_MIN_SIDE", 0.2, 0.0, 0.45);
+  return f;
+}
+
 // Elimination-tree height, in tile columns, of a dissection step: the
 // separator's tiles plus the larger child's height, which grows about as
 // sqrt(size) on these planar co-visibility graphs (cfg3: ~1 tile column per
@@ -259,7 +275,8 @@ struct Dissector {
         pr[i] = {dir[0] * xyz[3L * u] + dir[1] * xyz[3L * u + 1] + dir[2] * xyz[3L * u + 2], u};
       }
       std::sort(pr.begin(), pr.end());
-      for (int qi = 3 * n_q / 10; qi <= 7 * n_q / 10; qi += q_step) {   // cut at quantiles 0.30 .. 0.70
+      const int q0 = (int)std::lround(nd_qlo() * n_q);
+      for (int qi = q0; qi <= n_q - q0; qi += q_step) {   // cut at quantiles 0.30 .. 0.70
         const int cut = m * qi / n_q;
         if (cut < 1 || cut >= m) continue;
         for (int i = 0; i < m; ++i) side[pr[i].second] = i < cut ? 1 : 2;
@@ -268,7 +285,7 @@ struct Dissector {
         int na = 0, nbb = 0;
         for (int u : comp)
           if (!cover[u]) (side[u] == 1 ? na : nbb)++;
-        if (std::min(na, nbb) < m / 5) continue;
+        if (std::min(na, nbb) < (int)(nd_min_side() * m)) continue;
         // elimination-tree height in tile columns: the separator's tiles plus
         // the larger child's height, which grows about as sqrt(size) on these
         // planar graphs (cfg3's tree: ~1 tile column per sqrt(tag))
